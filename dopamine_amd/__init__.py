@@ -1,0 +1,8 @@
+"""dopamine_amd -- MI355X-native replay-sampling + Q-learning update path of Dopamine.
+
+The compute path is the in-tree HIP library ``libdopamine_amd.so`` (C ABI in
+include/dopamine_amd.h); importing ``dopamine_amd._lib`` fails loudly if it has
+not been built.  PyTorch-ROCm provides device memory, streams, the Nature-CNN
+forward/backward and torch.distributed (RCCL).
+"""
+__version__ = '0.1.0'

@@ -1,0 +1,23 @@
+"""Builds the in-tree HIP library (gfx950).  Importing this module never loads it."""
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'libdopamine_amd.so')
+SOURCES = [os.path.join(_HERE, 'csrc', f) for f in ('replay.hip', 'learner.hip')]
+HEADER = os.path.join(os.path.dirname(_HERE), 'include', 'dopamine_amd.h')
+ARCH = os.environ.get('DQ_OFFLOAD_ARCH', 'gfx950')
+
+
+def build(verbose=False):
+  """Compile the HIP sources into libdopamine_amd.so next to this file."""
+  cmd = ['hipcc', '--offload-arch=' + ARCH, '-O3', '-fPIC', '-shared', '-std=c++17',
+         '-ffp-contract=off', '-Wall', '-o', LIB_PATH] + SOURCES
+  if verbose:
+    print(' '.join(cmd))
+  subprocess.run(cmd, check=True)
+  return LIB_PATH
+
+
+if __name__ == '__main__':
+  build(verbose=True)

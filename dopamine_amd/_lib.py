@@ -1,0 +1,103 @@
+"""ctypes binding of the C ABI declared in include/dopamine_amd.h.
+
+The HIP library is the ONLY compute path: if ``libdopamine_amd.so`` is missing
+this module raises at import time -- there is no CPU fallback.
+"""
+import ctypes
+import os
+
+from dopamine_amd._build import HEADER, LIB_PATH  # noqa: F401
+
+ABI_VERSION = 1
+OK = 0
+ST_OK, ST_EMPTY_TREE, ST_MAX_ATTEMPTS, ST_TAPE_EXHAUSTED, ST_NEG_PRIORITY, ST_TOO_FEW, ST_BAD_INDEX = range(7)
+LAYOUT_RAW, LAYOUT_F32_NORM = 0, 1
+
+
+class Meta(ctypes.Structure):
+  _fields_ = [('add_count', ctypes.c_int64), ('tape_pos', ctypes.c_int64),
+              ('tape_len', ctypes.c_int64), ('max_recorded_priority', ctypes.c_double),
+              ('status', ctypes.c_int32), ('status_arg', ctypes.c_int32),
+              ('status_value', ctypes.c_double), ('reserved', ctypes.c_int64 * 2)]
+
+
+class Config(ctypes.Structure):
+  _fields_ = [('capacity', ctypes.c_int64), ('obs_bytes', ctypes.c_int64),
+              ('stack_size', ctypes.c_int32), ('update_horizon', ctypes.c_int32),
+              ('max_sample_attempts', ctypes.c_int32), ('prioritized', ctypes.c_int32),
+              ('obs_is_u8', ctypes.c_int32), ('pad_', ctypes.c_int32), ('gamma', ctypes.c_double)]
+
+
+class Storage(ctypes.Structure):
+  _fields_ = [('frames', ctypes.c_void_p), ('actions', ctypes.c_void_p),
+              ('rewards', ctypes.c_void_p), ('terminals', ctypes.c_void_p),
+              ('tree', ctypes.c_void_p), ('meta', ctypes.c_void_p), ('tape', ctypes.c_void_p),
+              ('tape_capacity', ctypes.c_int64), ('discount', ctypes.c_void_p)]
+
+
+_P = ctypes.c_void_p
+_I32 = ctypes.c_int32
+_I64 = ctypes.c_int64
+_F = ctypes.c_float
+_D = ctypes.c_double
+
+# name -> argtypes (restype int unless noted); mirrors include/dopamine_amd.h
+SIGNATURES = {
+    'dq_abi_version': [],
+    'dq_last_error': [],
+    'dq_sumtree_depth': [_I64],
+    'dq_replay_create': [ctypes.POINTER(Config), ctypes.POINTER(Storage), ctypes.POINTER(_P)],
+    'dq_replay_destroy': [_P],
+    'dq_replay_add': [_P, _I64, _P, _P, _P, _P, _P, _P],
+    'dq_replay_sample_indices': [_P, _I32, _P, _P],
+    'dq_replay_gather': [_P, _P, _I32, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    'dq_sumtree_set': [_P, _P, _P, _I64, _P],
+    'dq_sumtree_get': [_P, _P, _I64, _P, _P],
+    'dq_sumtree_rebuild': [_P, _P],
+    'dq_replay_set_meta': [_P, _I64, _D, _P],
+    'dq_replay_set_tape': [_P, _I64, _P],
+    'dq_replay_read_meta': [_P, ctypes.POINTER(Meta), _P],
+    'dq_c51_loss': [_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _F, _P, _P, _P, _P, _P],
+    'dq_dqn_huber_loss': [_P, _P, _P, _P, _P, _I32, _I32, _F, _P, _P, _P, _P],
+    'dq_iqn_loss': [_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _F, _F, _P, _P, _P, _P],
+    'dq_adam_tf1': [_P, _P, _P, _P, _P, _I64, _F, _F, _F, _F, _P],
+    'dq_rmsprop_tf1': [_P, _P, _P, _P, _P, _I64, _F, _F, _F, _F, _I32, _P],
+    'dq_sync_copy': [_P, _P, _I64, _P],
+}
+
+
+class DQError(RuntimeError):
+  pass
+
+
+def _load():
+  if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        'dopamine_amd: HIP library %s not built (run __graft_entry__.build() or '
+        'python -m dopamine_amd._build). There is no CPU fallback.' % LIB_PATH)
+  lib = ctypes.CDLL(LIB_PATH)
+  for name, args in SIGNATURES.items():
+    fn = getattr(lib, name)
+    fn.argtypes = args
+    fn.restype = ctypes.c_char_p if name == 'dq_last_error' else ctypes.c_int
+  if lib.dq_abi_version() != ABI_VERSION:
+    raise ImportError('dopamine_amd ABI mismatch: lib %d, python %d' % (lib.dq_abi_version(), ABI_VERSION))
+  return lib
+
+
+lib = _load()
+
+
+def check(rc, what=''):
+  if rc != OK:
+    raise DQError('%s failed (%d): %s' % (what, rc, lib.dq_last_error().decode()))
+
+
+def call(name, *args):
+  check(getattr(lib, name)(*args), name)
+
+
+def ptr(t):
+  """Raw device pointer of a torch tensor (or None)."""
+  return None if t is None else ctypes.c_void_p(t.data_ptr())
+

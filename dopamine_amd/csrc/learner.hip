@@ -1,0 +1,394 @@
+// Learner-side kernels: C51 target + projection + cross-entropy (+ PER weights
+// and new priorities), DQN Huber target, IQN quantile-Huber loss, and the TF1
+// Adam / RMSProp updates over one flat fp32 parameter buffer.
+// Restates the TF1 graph code of rainbow_agent.py:200-305 + 340-494,
+// dqn_agent.py:283-322, implicit_quantile_agent.py:190-321 and the TF1
+// ApplyAdam / ApplyCenteredRMSProp op semantics.
+#include "common.h"
+
+namespace dq {
+
+// ---------------------------------------------------------------------------
+// C51.  One 1024-thread block; wave w handles samples w, w+16, ...; lane = atom.
+// ---------------------------------------------------------------------------
+struct C51Args {
+  const float* ol;
+  const float* tl;
+  const int32_t* act;
+  const float* rew;
+  const uint8_t* term;
+  const float* probs;
+  const float* support;
+  int B, A, N;
+  float cg;
+  float* grad;
+  float* loss_out;
+  float* prio_out;
+  float* mean_out;
+};
+
+__global__ __launch_bounds__(1024) void k_c51(C51Args a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* s_diff = smem;                 // [B][N]  softmax - projection
+  float* s_loss = s_diff + a.B * a.N;   // [B]
+  float* s_w = s_loss + a.B;            // [B]
+  __shared__ float s_red[16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int N = a.N, A = a.A;
+  const bool on = lane < N;
+  const float z = on ? a.support[lane] : 0.0f;
+  const float vmin = a.support[0], vmax = a.support[N - 1];
+  const float dz = __fsub_rn(a.support[1], a.support[0]);
+  const float ninf = -__builtin_inff();
+  for (int b = wave; b < a.B; b += nw) {
+    // target net: probabilities, Q = sum z p, greedy action (first max)
+    float best = ninf, pbest = 0.0f;
+    for (int act = 0; act < A; ++act) {
+      const float x = on ? a.tl[((int64_t)b * A + act) * N + lane] : ninf;
+      const float mx = wave_max(x);
+      const float e = on ? expf(__fsub_rn(x, mx)) : 0.0f;
+      const float p = __fdiv_rn(e, wave_sum(e));
+      const float q = wave_sum(on ? __fmul_rn(z, p) : 0.0f);
+      if (act == 0 || q > best) {
+        best = q;
+        pbest = p;
+      }
+    }
+    // Bellman support Tz = r + gamma^n (1 - terminal) z, clipped, projected (Eq. 7)
+    const float gt = __fmul_rn(a.cg, __fsub_rn(1.0f, (float)a.term[b]));
+    const float tz = __fadd_rn(a.rew[b], __fmul_rn(gt, z));
+    const float tzc = fminf(fmaxf(tz, vmin), vmax);
+    float proj = 0.0f;
+    for (int j = 0; j < N; ++j) {
+      const float cj = __shfl(tzc, j), pj = __shfl(pbest, j);
+      float w = __fsub_rn(1.0f, __fdiv_rn(fabsf(__fsub_rn(cj, z)), dz));
+      w = fminf(fmaxf(w, 0.0f), 1.0f);
+      proj = __fadd_rn(proj, __fmul_rn(w, pj));
+    }
+    if (!on) proj = 0.0f;
+    // softmax cross-entropy on the chosen action's online logits
+    const int ab = a.act[b];
+    const float y = on ? a.ol[((int64_t)b * A + ab) * N + lane] : ninf;
+    const float my = wave_max(y);
+    const float sh = on ? __fsub_rn(y, my) : 0.0f;
+    const float ey = on ? expf(sh) : 0.0f;
+    const float sy = wave_sum(ey);
+    const float lse = logf(sy);
+    const float loss = wave_sum(on ? __fmul_rn(proj, __fsub_rn(lse, sh)) : 0.0f);
+    if (on) s_diff[b * N + lane] = __fsub_rn(__fdiv_rn(ey, sy), proj);
+    if (lane == 0) s_loss[b] = loss;
+  }
+  __syncthreads();
+  // PER importance weights  w = 1/sqrt(p + 1e-10), w /= max(w)   (rb:277-280)
+  float wmax = 0.0f;
+  for (int b = threadIdx.x; b < a.B; b += blockDim.x) {
+    const float w = a.probs ? __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(a.probs[b], 1e-10f))) : 1.0f;
+    s_w[b] = w;
+    wmax = fmaxf(wmax, w);
+  }
+  wmax = wave_max(wmax);
+  if (lane == 0) s_red[wave] = wmax;
+  __syncthreads();
+  wmax = s_red[0];
+  for (int i = 1; i < nw; ++i) wmax = fmaxf(wmax, s_red[i]);
+  __syncthreads();
+  float part = 0.0f;
+  for (int b = threadIdx.x; b < a.B; b += blockDim.x) {
+    const float w = a.probs ? __fdiv_rn(s_w[b], wmax) : 1.0f;
+    s_w[b] = w;
+    const float l = s_loss[b];
+    if (a.loss_out) a.loss_out[b] = l;
+    if (a.prio_out) a.prio_out[b] = __fsqrt_rn(__fadd_rn(l, 1e-10f));
+    part = __fadd_rn(part, __fmul_rn(w, l));
+  }
+  part = wave_sum(part);
+  if (lane == 0) s_red[wave] = part;
+  __syncthreads();
+  if (threadIdx.x == 0 && a.mean_out) {
+    float t = 0.0f;
+    for (int i = 0; i < nw; ++i) t = __fadd_rn(t, s_red[i]);
+    a.mean_out[0] = __fdiv_rn(t, (float)a.B);
+  }
+  // d mean(w * CE) / d logits: (w_b / B) (softmax - proj) on the chosen action, 0 elsewhere
+  const float invB = __fdiv_rn(1.0f, (float)a.B);
+  const int64_t total = (int64_t)a.B * A * N;
+  for (int64_t t = threadIdx.x; t < total; t += blockDim.x) {
+    const int b = (int)(t / ((int64_t)A * N));
+    const int r = (int)(t - (int64_t)b * A * N);
+    const int act = r / N, i = r - act * N;
+    a.grad[t] = (act == a.act[b]) ? __fmul_rn(__fmul_rn(s_w[b], invB), s_diff[b * N + i]) : 0.0f;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// DQN: Bellman max target + Huber(1).  One thread per sample.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_dqn(const float* oq, const float* tq, const int32_t* act,
+                                             const float* rew, const uint8_t* term, int B, int A,
+                                             float cg, float* grad, float* loss_out,
+                                             float* mean_out) {
+  __shared__ float s_red[4];
+  float part = 0.0f;
+  const float invB = __fdiv_rn(1.0f, (float)B);
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    float mx = tq[(int64_t)b * A];
+    for (int j = 1; j < A; ++j) mx = fmaxf(mx, tq[(int64_t)b * A + j]);
+    // r + cumulative_gamma * max_a Q' * (1 - terminal)   (dqn:298-299)
+    const float target =
+        __fadd_rn(rew[b], __fmul_rn(__fmul_rn(cg, mx), __fsub_rn(1.0f, (float)term[b])));
+    const int ab = act[b];
+    const float err = __fsub_rn(oq[(int64_t)b * A + ab], target);  // predictions - labels
+    const float ae = fabsf(err);
+    const float quad = fminf(ae, 1.0f);
+    const float lin = __fsub_rn(ae, quad);
+    const float loss = __fadd_rn(__fmul_rn(__fmul_rn(0.5f, quad), quad), lin);
+    if (loss_out) loss_out[b] = loss;
+    part = __fadd_rn(part, loss);
+    const float g = __fmul_rn(fminf(fmaxf(err, -1.0f), 1.0f), invB);
+    for (int j = 0; j < A; ++j) grad[(int64_t)b * A + j] = (j == ab) ? g : 0.0f;
+  }
+  part = wave_sum(part);
+  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = part;
+  __syncthreads();
+  if (threadIdx.x == 0 && mean_out) {
+    float t = 0.0f;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t = __fadd_rn(t, s_red[i]);
+    mean_out[0] = __fdiv_rn(t, (float)B);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// IQN quantile-Huber.  One 64-thread block per sample b; lane = online quantile.
+// ---------------------------------------------------------------------------
+struct IqnArgs {
+  const float* oq;
+  const float* tq;
+  const float* ta;
+  const float* tau;
+  const int32_t* act;
+  const float* rew;
+  const uint8_t* term;
+  int B, A, N, Np, K;
+  float cg, kappa;
+  float* grad;
+  float* loss_out;
+};
+
+__global__ __launch_bounds__(64) void k_iqn(IqnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float s_T[];  // [Np]
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const int B = a.B, A = a.A;
+  // greedy next action from the mean over K target quantiles (iqn:170-188)
+  float best = 0.0f;
+  int astar = 0;
+  for (int act = 0; act < A; ++act) {
+    float s = 0.0f;
+    for (int k = lane; k < a.K; k += 64) s = __fadd_rn(s, a.ta[((int64_t)k * B + b) * A + act]);
+    const float m = __fdiv_rn(wave_sum(s), (float)a.K);
+    if (act == 0 || m > best) {
+      best = m;
+      astar = act;
+    }
+  }
+  const float gt = __fmul_rn(a.cg, __fsub_rn(1.0f, (float)a.term[b]));
+  for (int j = lane; j < a.Np; j += 64)
+    s_T[j] = __fadd_rn(a.rew[b], __fmul_rn(gt, a.tq[((int64_t)j * B + b) * A + astar]));
+  __syncthreads();
+  const int ab = a.act[b];
+  const float kappa = a.kappa, hk = __fmul_rn(0.5f, kappa);
+  const float gscale = __fdiv_rn(-1.0f, __fmul_rn(__fmul_rn((float)a.Np, (float)B), kappa));
+  float rho_acc = 0.0f;
+  for (int i = lane; i < a.N; i += 64) {
+    const int64_t row = (int64_t)i * B + b;
+    const float theta = a.oq[row * A + ab];
+    const float tau = a.tau[row];
+    float rho = 0.0f, g = 0.0f;
+    for (int j = 0; j < a.Np; ++j) {
+      const float u = __fsub_rn(s_T[j], theta);
+      const float au = fabsf(u);
+      const bool inner = au <= kappa;
+      const float h = inner ? __fmul_rn(__fmul_rn(0.5f, u), u) : __fmul_rn(kappa, __fsub_rn(au, hk));
+      const float w = fabsf(__fsub_rn(tau, u < 0.0f ? 1.0f : 0.0f));
+      rho = __fadd_rn(rho, __fdiv_rn(__fmul_rn(w, h), kappa));
+      const float dh = inner ? u : (u > 0.0f ? kappa : (u < 0.0f ? -kappa : 0.0f));
+      g = __fadd_rn(g, __fmul_rn(w, dh));
+    }
+    rho_acc = __fadd_rn(rho_acc, rho);
+    const float gv = __fmul_rn(g, gscale);
+    for (int c = 0; c < A; ++c) a.grad[row * A + c] = (c == ab) ? gv : 0.0f;
+  }
+  const float tot = wave_sum(rho_acc);
+  if (lane == 0 && a.loss_out) a.loss_out[b] = __fdiv_rn(tot, (float)a.Np);
+}
+
+__global__ __launch_bounds__(64) void k_mean(const float* x, int n, float* out) {
+  float s = 0.0f;
+  for (int i = threadIdx.x; i < n; i += 64) s = __fadd_rn(s, x[i]);
+  s = wave_sum(s);
+  if (threadIdx.x == 0) out[0] = __fdiv_rn(s, (float)n);
+}
+
+// ---------------------------------------------------------------------------
+// TF1 Adam over a flat buffer.  k_adam_prep computes this step's
+// alpha = lr sqrt(1 - b2^t) / (1 - b1^t) from the float32 beta powers and
+// advances them; k_adam applies m/v/var updates (float4 vectorised).
+// ---------------------------------------------------------------------------
+__global__ void k_adam_prep(float* state, float lr, float b1, float b2) {
+  const float b1p = state[0], b2p = state[1];
+  state[2] = __fdiv_rn(__fmul_rn(lr, __fsqrt_rn(__fsub_rn(1.0f, b2p))), __fsub_rn(1.0f, b1p));
+  state[0] = __fmul_rn(b1p, b1);
+  state[1] = __fmul_rn(b2p, b2);
+}
+
+__device__ __forceinline__ void adam1(float& var, float g, float& m, float& v, float alpha,
+                                      float omb1, float omb2, float eps) {
+  m = __fadd_rn(m, __fmul_rn(__fsub_rn(g, m), omb1));
+  v = __fadd_rn(v, __fmul_rn(__fsub_rn(__fmul_rn(g, g), v), omb2));
+  var = __fsub_rn(var, __fdiv_rn(__fmul_rn(m, alpha), __fadd_rn(__fsqrt_rn(v), eps)));
+}
+
+__global__ __launch_bounds__(256) void k_adam(float* __restrict__ var, const float* __restrict__ grad,
+                                              float* __restrict__ m, float* __restrict__ v,
+                                              const float* __restrict__ state, int64_t n,
+                                              float b1, float b2, float eps) {
+  const float alpha = state[2];
+  const float omb1 = __fsub_rn(1.0f, b1), omb2 = __fsub_rn(1.0f, b2);
+  const int64_t n4 = n >> 2;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 p = ((float4*)var)[i], g = ((const float4*)grad)[i];
+    float4 mm = ((float4*)m)[i], vv = ((float4*)v)[i];
+    adam1(p.x, g.x, mm.x, vv.x, alpha, omb1, omb2, eps);
+    adam1(p.y, g.y, mm.y, vv.y, alpha, omb1, omb2, eps);
+    adam1(p.z, g.z, mm.z, vv.z, alpha, omb1, omb2, eps);
+    adam1(p.w, g.w, mm.w, vv.w, alpha, omb1, omb2, eps);
+    ((float4*)var)[i] = p;
+    ((float4*)m)[i] = mm;
+    ((float4*)v)[i] = vv;
+  }
+  for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    adam1(var[i], grad[i], m[i], v[i], alpha, omb1, omb2, eps);
+}
+
+__global__ __launch_bounds__(256) void k_rmsprop(float* var, const float* grad, float* ms, float* mg,
+                                                 float* mom, int64_t n, float lr, float rho,
+                                                 float mu, float eps, int centered) {
+  const float omr = __fsub_rn(1.0f, rho);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float g = grad[i];
+    const float s = __fadd_rn(ms[i], __fmul_rn(__fsub_rn(__fmul_rn(g, g), ms[i]), omr));
+    ms[i] = s;
+    float denom;
+    if (centered) {
+      const float a = __fadd_rn(mg[i], __fmul_rn(__fsub_rn(g, mg[i]), omr));
+      mg[i] = a;
+      denom = __fadd_rn(__fsub_rn(s, __fmul_rn(a, a)), eps);
+    } else {
+      denom = __fadd_rn(s, eps);
+    }
+    const float mo = __fadd_rn(__fmul_rn(mom[i], mu), __fdiv_rn(__fmul_rn(g, lr), __fsqrt_rn(denom)));
+    mom[i] = mo;
+    var[i] = __fsub_rn(var[i], mo);
+  }
+}
+
+static int elementwise_grid(int64_t n) {
+  int64_t blocks = (n + 1023) / 1024;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 2048) blocks = 2048;
+  return (int)blocks;
+}
+
+}  // namespace dq
+
+using namespace dq;
+
+extern "C" {
+
+int dq_c51_loss(const float* online_logits, const float* target_logits, const int32_t* actions,
+                const float* rewards, const uint8_t* terminals, const float* probs,
+                const float* support, int32_t batch, int32_t num_actions, int32_t num_atoms,
+                float cumulative_gamma, float* grad_logits, float* loss_out,
+                float* priorities_out, float* mean_loss_out, void* stream) {
+  DQ_CHECK_ARG(online_logits && target_logits && actions && rewards && terminals && support &&
+                   grad_logits,
+               "null argument");
+  DQ_CHECK_ARG(num_atoms >= 2 && num_atoms <= 64, "num_atoms must be in [2, 64]");
+  DQ_CHECK_ARG(batch >= 1 && batch <= 256 && num_actions >= 1, "batch must be in [1, 256]");
+  C51Args a{online_logits, target_logits, actions, rewards, terminals, probs, support,
+            batch, num_actions, num_atoms, cumulative_gamma, grad_logits, loss_out,
+            priorities_out, mean_loss_out};
+  const size_t shm = sizeof(float) * ((size_t)batch * num_atoms + 2 * (size_t)batch);
+  const int threads = batch >= 16 ? 1024 : 64 * batch;
+  hipLaunchKernelGGL(k_c51, dim3(1), dim3(threads), shm, (hipStream_t)stream, a);
+  DQ_CHECK_LAUNCH("k_c51");
+  return DQ_OK;
+}
+
+int dq_dqn_huber_loss(const float* online_q, const float* target_q, const int32_t* actions,
+                      const float* rewards, const uint8_t* terminals, int32_t batch,
+                      int32_t num_actions, float cumulative_gamma, float* grad_q,
+                      float* loss_out, float* mean_loss_out, void* stream) {
+  DQ_CHECK_ARG(online_q && target_q && actions && rewards && terminals && grad_q, "null argument");
+  DQ_CHECK_ARG(batch >= 1 && num_actions >= 1, "bad sizes");
+  hipLaunchKernelGGL(k_dqn, dim3(1), dim3(256), 0, (hipStream_t)stream, online_q, target_q,
+                     actions, rewards, terminals, batch, num_actions, cumulative_gamma, grad_q,
+                     loss_out, mean_loss_out);
+  DQ_CHECK_LAUNCH("k_dqn");
+  return DQ_OK;
+}
+
+int dq_iqn_loss(const float* online_qv, const float* target_qv, const float* target_qv_action,
+                const float* taus, const int32_t* actions, const float* rewards,
+                const uint8_t* terminals, int32_t batch, int32_t num_actions,
+                int32_t num_tau, int32_t num_tau_prime, int32_t num_quantile,
+                float cumulative_gamma, float kappa, float* grad_qv, float* loss_out,
+                float* mean_loss_out, void* stream) {
+  DQ_CHECK_ARG(online_qv && target_qv && target_qv_action && taus && actions && rewards &&
+                   terminals && grad_qv && loss_out,
+               "null argument (loss_out is required)");
+  DQ_CHECK_ARG(batch >= 1 && num_actions >= 1 && num_tau >= 1 && num_tau_prime >= 1 &&
+                   num_quantile >= 1 && kappa > 0.0f,
+               "bad sizes");
+  IqnArgs a{online_qv, target_qv, target_qv_action, taus, actions, rewards, terminals,
+            batch, num_actions, num_tau, num_tau_prime, num_quantile, cumulative_gamma, kappa,
+            grad_qv, loss_out};
+  hipLaunchKernelGGL(k_iqn, dim3(batch), dim3(64), sizeof(float) * num_tau_prime,
+                     (hipStream_t)stream, a);
+  DQ_CHECK_LAUNCH("k_iqn");
+  if (mean_loss_out) {
+    hipLaunchKernelGGL(k_mean, dim3(1), dim3(64), 0, (hipStream_t)stream, loss_out, batch,
+                       mean_loss_out);
+    DQ_CHECK_LAUNCH("k_mean");
+  }
+  return DQ_OK;
+}
+
+int dq_adam_tf1(float* var, const float* grad, float* m, float* v, float* state, int64_t n,
+                float lr, float beta1, float beta2, float eps, void* stream) {
+  DQ_CHECK_ARG(var && grad && m && v && state && n >= 0, "bad arguments");
+  DQ_CHECK_ARG(((uintptr_t)var | (uintptr_t)grad | (uintptr_t)m | (uintptr_t)v) % 16 == 0,
+               "adam buffers must be 16-byte aligned");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_adam_prep, dim3(1), dim3(1), 0, s, state, lr, beta1, beta2);
+  DQ_CHECK_LAUNCH("k_adam_prep");
+  if (n == 0) return DQ_OK;
+  hipLaunchKernelGGL(k_adam, dim3(elementwise_grid(n)), dim3(256), 0, s, var, grad, m, v, state, n,
+                     beta1, beta2, eps);
+  DQ_CHECK_LAUNCH("k_adam");
+  return DQ_OK;
+}
+
+int dq_rmsprop_tf1(float* var, const float* grad, float* ms, float* mg, float* mom, int64_t n,
+                   float lr, float decay, float momentum, float eps, int32_t centered,
+                   void* stream) {
+  DQ_CHECK_ARG(var && grad && ms && mom && (mg || !centered) && n >= 0, "bad arguments");
+  if (n == 0) return DQ_OK;
+  hipLaunchKernelGGL(k_rmsprop, dim3(elementwise_grid(n)), dim3(256), 0, (hipStream_t)stream, var,
+                     grad, ms, mg, mom, n, lr, decay, momentum, eps, centered);
+  DQ_CHECK_LAUNCH("k_rmsprop");
+  return DQ_OK;
+}
+
+}  // extern "C"

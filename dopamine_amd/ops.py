@@ -1,0 +1,113 @@
+"""torch-tensor wrappers over the learner kernels of the C ABI.
+
+Every function launches on torch's current stream (so it is captured by
+``torch.cuda.graph``) and never synchronises.
+"""
+import ctypes
+
+import torch
+
+from dopamine_amd import _lib
+
+p = _lib.ptr
+
+
+def _stream(t):
+  return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _c(t, dtype):
+  assert t.is_cuda and t.dtype == dtype and t.is_contiguous(), (t.dtype, t.device, dtype)
+  return t
+
+
+def c51_loss(online_logits, target_logits, actions, rewards, terminals, support, cumulative_gamma,
+             probs=None, out=None):
+  """rainbow_agent.py:200-305.  Returns dict(grad, loss, priorities, mean_loss)."""
+  B, A, N = online_logits.shape
+  f32 = torch.float32
+  if out is None:
+    dev = online_logits.device
+    out = dict(grad=torch.empty_like(online_logits), loss=torch.empty(B, dtype=f32, device=dev),
+               priorities=torch.empty(B, dtype=f32, device=dev),
+               mean_loss=torch.empty(1, dtype=f32, device=dev))
+  _lib.call('dq_c51_loss', p(_c(online_logits, f32)), p(_c(target_logits, f32)),
+            p(_c(actions, torch.int32)), p(_c(rewards, f32)), p(_c(terminals, torch.uint8)),
+            p(probs if probs is None else _c(probs, f32)), p(_c(support, f32)), B, A, N,
+            float(cumulative_gamma), p(out['grad']), p(out['loss']), p(out['priorities']),
+            p(out['mean_loss']), _stream(online_logits))
+  return out
+
+
+def dqn_huber_loss(online_q, target_q, actions, rewards, terminals, cumulative_gamma, out=None):
+  """dqn_agent.py:283-322."""
+  B, A = online_q.shape
+  f32 = torch.float32
+  if out is None:
+    dev = online_q.device
+    out = dict(grad=torch.empty_like(online_q), loss=torch.empty(B, dtype=f32, device=dev),
+               mean_loss=torch.empty(1, dtype=f32, device=dev))
+  _lib.call('dq_dqn_huber_loss', p(_c(online_q, f32)), p(_c(target_q, f32)),
+            p(_c(actions, torch.int32)), p(_c(rewards, f32)), p(_c(terminals, torch.uint8)), B, A,
+            float(cumulative_gamma), p(out['grad']), p(out['loss']), p(out['mean_loss']),
+            _stream(online_q))
+  return out
+
+
+def iqn_loss(online_qv, target_qv, target_qv_action, taus, actions, rewards, terminals,
+             cumulative_gamma, kappa=1.0, out=None):
+  """implicit_quantile_agent.py:190-321 (rows ordered q*B + b)."""
+  B = rewards.shape[0]
+  A = online_qv.shape[1]
+  N, Np, K = online_qv.shape[0] // B, target_qv.shape[0] // B, target_qv_action.shape[0] // B
+  f32 = torch.float32
+  if out is None:
+    dev = online_qv.device
+    out = dict(grad=torch.empty_like(online_qv), loss=torch.empty(B, dtype=f32, device=dev),
+               mean_loss=torch.empty(1, dtype=f32, device=dev))
+  _lib.call('dq_iqn_loss', p(_c(online_qv, f32)), p(_c(target_qv, f32)),
+            p(_c(target_qv_action, f32)), p(_c(taus.reshape(-1), f32)), p(_c(actions, torch.int32)),
+            p(_c(rewards, f32)), p(_c(terminals, torch.uint8)), B, A, N, Np, K,
+            float(cumulative_gamma), float(kappa), p(out['grad']), p(out['loss']),
+            p(out['mean_loss']), _stream(online_qv))
+  return out
+
+
+class TF1Adam(object):
+  """tf.train.AdamOptimizer over one flat fp32 buffer (ApplyAdam semantics)."""
+
+  def __init__(self, params, learning_rate=0.001, beta1=0.9, beta2=0.999, epsilon=1e-8):
+    self.params = params
+    self.lr, self.b1, self.b2, self.eps = float(learning_rate), float(beta1), float(beta2), float(epsilon)
+    self.m = torch.zeros_like(params)
+    self.v = torch.zeros_like(params)
+    self.state = torch.tensor([beta1, beta2, 0.0, 0.0], dtype=torch.float32, device=params.device)
+
+  def step(self, grad):
+    _lib.call('dq_adam_tf1', p(self.params), p(_c(grad, torch.float32)), p(self.m), p(self.v),
+              p(self.state), self.params.numel(), self.lr, self.b1, self.b2, self.eps,
+              _stream(self.params))
+
+
+class TF1RMSProp(object):
+  """tf.train.RMSPropOptimizer (rms slot initialised to one, as TF1)."""
+
+  def __init__(self, params, learning_rate=0.00025, decay=0.95, momentum=0.0, epsilon=1e-5,
+               centered=True):
+    self.params = params
+    self.lr, self.decay, self.mu, self.eps = float(learning_rate), float(decay), float(momentum), float(epsilon)
+    self.centered = bool(centered)
+    self.ms = torch.ones_like(params)
+    self.mg = torch.zeros_like(params)
+    self.mom = torch.zeros_like(params)
+
+  def step(self, grad):
+    _lib.call('dq_rmsprop_tf1', p(self.params), p(_c(grad, torch.float32)), p(self.ms), p(self.mg),
+              p(self.mom), self.params.numel(), self.lr, self.decay, self.mu, self.eps,
+              int(self.centered), _stream(self.params))
+
+
+def sync_copy(dst, src):
+  """Online -> target copy (dqn_agent.py:324-339)."""
+  assert dst.numel() == src.numel() and dst.dtype == src.dtype
+  _lib.call('dq_sync_copy', p(dst), p(src), dst.numel() * dst.element_size(), _stream(dst))

@@ -1,0 +1,555 @@
+"""Device-resident replay memory with the reference's out-of-graph API.
+
+Mirrors ``dopamine.replay_memory.circular_replay_buffer`` (reference
+circular_replay_buffer.py:80-915): the same constructor arguments, methods,
+attributes, exceptions and messages.  Storage lives in HBM (torch tensors);
+index sampling, validity checks, the frame-stack gather and the n-step reward
+run in the HIP library (dopamine_amd/csrc/replay.hip) behind the C ABI of
+include/dopamine_amd.h.  Numpy-returning methods (``sample_transition_batch``
+etc.) synchronise and return exactly what the reference returns; the learner
+uses ``sample_device`` which stays on the device and never synchronises.
+"""
+import collections
+import ctypes
+import math
+
+import numpy as np
+import torch
+
+from dopamine_amd import _lib
+from dopamine_amd.replay_memory.rng_tape import RNGTape, default_stream
+
+ReplayElement = collections.namedtuple('shape_type', ['name', 'shape', 'type'])
+
+STORE_FILENAME_PREFIX = '$store$_'
+CHECKPOINT_DURATION = 4
+
+
+def invalid_range(cursor, replay_capacity, stack_size, update_horizon):
+  """Indices around the cursor that cannot be sampled (crb:53-77)."""
+  assert cursor < replay_capacity
+  return np.array([(cursor - update_horizon + i) % replay_capacity
+                   for i in range(stack_size + update_horizon)])
+
+
+def _default_device(device):
+  if device is not None:
+    return torch.device(device)
+  if not torch.cuda.is_available():
+    raise RuntimeError('dopamine_amd replay memory needs a ROCm GPU (no CPU fallback)')
+  return torch.device('cuda', torch.cuda.current_device())
+
+
+def _stream_handle(device):
+  return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class OutOfGraphReplayBuffer(object):
+  """Circular replay memory in HBM with uniform sampling (crb:80-687)."""
+
+  _prioritized = False
+
+  def __init__(self,
+               observation_shape,
+               stack_size,
+               replay_capacity,
+               batch_size,
+               update_horizon=1,
+               gamma=0.99,
+               max_sample_attempts=1000,
+               extra_storage_types=None,
+               observation_dtype=np.uint8,
+               terminal_dtype=np.uint8,
+               action_shape=(),
+               action_dtype=np.int32,
+               reward_shape=(),
+               reward_dtype=np.float32,
+               device=None,
+               rng=None,
+               tape_words=1 << 20):
+    assert isinstance(observation_shape, tuple)
+    if replay_capacity < update_horizon + stack_size:
+      raise ValueError('There is not enough capacity to cover '
+                       'update_horizon and stack_size.')
+    if tuple(action_shape) != () or tuple(reward_shape) != ():
+      raise NotImplementedError('dopamine_amd stores scalar actions and rewards only')
+    if np.dtype(terminal_dtype).itemsize != 1:
+      raise NotImplementedError('terminal_dtype must be a 1-byte type')
+    self._action_shape = action_shape
+    self._action_dtype = action_dtype
+    self._reward_shape = reward_shape
+    self._reward_dtype = reward_dtype
+    self._observation_shape = observation_shape
+    self._stack_size = stack_size
+    self._state_shape = self._observation_shape + (self._stack_size,)
+    self._replay_capacity = replay_capacity
+    self._batch_size = batch_size
+    self._update_horizon = update_horizon
+    self._gamma = gamma
+    self._observation_dtype = observation_dtype
+    self._terminal_dtype = terminal_dtype
+    self._max_sample_attempts = max_sample_attempts
+    self._extra_storage_types = list(extra_storage_types) if extra_storage_types else []
+    self._device = _default_device(device)
+    self._obs_bytes = int(np.prod(observation_shape, dtype=np.int64)) * np.dtype(observation_dtype).itemsize
+    self._create_storage()
+    self.add_count = np.array(0)
+    self.invalid_range = np.zeros((self._stack_size))
+    self._cumulative_discount_vector = np.array(
+        [math.pow(self._gamma, n) for n in range(update_horizon)], dtype=np.float32)
+    self._discount_dev = torch.from_numpy(self._cumulative_discount_vector).to(self._device)
+    self._last_terminal = 0
+    self._rng = RNGTape(self, rng if rng is not None else default_stream(self._prioritized),
+                        tape_words, self._device)
+    self._create_handle()
+
+  # ------------------------------------------------------------------ storage
+  def _create_storage(self):
+    C, dev = self._replay_capacity, self._device
+    self._frames = torch.zeros((C, self._obs_bytes), dtype=torch.uint8, device=dev)
+    self._actions = torch.zeros((C,), dtype=torch.int32, device=dev)
+    self._rewards = torch.zeros((C,), dtype=torch.float32, device=dev)
+    self._terminals = torch.zeros((C,), dtype=torch.uint8, device=dev)
+    self._meta = torch.zeros((16,), dtype=torch.int64, device=dev)
+    self._tree = None
+    self._extras = {}
+    for e in self._extra_storage_types:
+      shape = (C,) + tuple(e.shape)
+      self._extras[e.name] = torch.zeros(shape, dtype=_torch_dtype(e.type), device=dev)
+
+  def _create_handle(self):
+    cfg = _lib.Config()
+    cfg.capacity = self._replay_capacity
+    cfg.obs_bytes = self._obs_bytes
+    cfg.stack_size = self._stack_size
+    cfg.update_horizon = self._update_horizon
+    cfg.max_sample_attempts = self._max_sample_attempts
+    cfg.prioritized = int(self._prioritized)
+    cfg.obs_is_u8 = int(np.dtype(self._observation_dtype) == np.uint8)
+    cfg.gamma = self._gamma
+    self._cfg = cfg
+    self._h = None
+    self._bind(self._rng.words, self._rng.capacity)
+
+  def _bind(self, tape, tape_cap):
+    st = _lib.Storage()
+    st.frames = self._frames.data_ptr()
+    st.actions = self._actions.data_ptr()
+    st.rewards = self._rewards.data_ptr()
+    st.terminals = self._terminals.data_ptr()
+    st.tree = self._tree.data_ptr() if self._tree is not None else None
+    st.meta = self._meta.data_ptr()
+    st.tape = tape.data_ptr()
+    st.tape_capacity = tape_cap
+    st.discount = self._discount_dev.data_ptr()
+    if self._h is not None:
+      _lib.call('dq_replay_destroy', self._h)
+    h = ctypes.c_void_p()
+    _lib.call('dq_replay_create', ctypes.byref(self._cfg), ctypes.byref(st), ctypes.byref(h))
+    self._h = h
+
+  def __del__(self):
+    h = getattr(self, '_h', None)
+    if h is not None:
+      try:
+        _lib.lib.dq_replay_destroy(h)
+      except Exception:  # interpreter shutdown
+        pass
+
+  @property
+  def _stream(self):
+    return _stream_handle(self._device)
+
+  def _read_meta(self):
+    m = _lib.Meta()
+    _lib.call('dq_replay_read_meta', self._h, ctypes.byref(m), self._stream)
+    return m
+
+  # ------------------------------------------------------------ signatures
+  def get_add_args_signature(self):
+    return self.get_storage_signature()
+
+  def get_storage_signature(self):
+    elems = [ReplayElement('observation', self._observation_shape, self._observation_dtype),
+             ReplayElement('action', self._action_shape, self._action_dtype),
+             ReplayElement('reward', self._reward_shape, self._reward_dtype),
+             ReplayElement('terminal', (), self._terminal_dtype)]
+    return elems + list(self._extra_storage_types)
+
+  def get_transition_elements(self, batch_size=None):
+    B = self._batch_size if batch_size is None else batch_size
+    elems = [
+        ReplayElement('state', (B,) + self._state_shape, self._observation_dtype),
+        ReplayElement('action', (B,) + self._action_shape, self._action_dtype),
+        ReplayElement('reward', (B,) + self._reward_shape, self._reward_dtype),
+        ReplayElement('next_state', (B,) + self._state_shape, self._observation_dtype),
+        ReplayElement('next_action', (B,) + self._action_shape, self._action_dtype),
+        ReplayElement('next_reward', (B,) + self._reward_shape, self._reward_dtype),
+        ReplayElement('terminal', (B,), self._terminal_dtype),
+        ReplayElement('indices', (B,), np.int32)]
+    for e in self._extra_storage_types:
+      elems.append(ReplayElement(e.name, (B,) + tuple(e.shape), e.type))
+    return elems
+
+  # ----------------------------------------------------------------- adding
+  def is_empty(self):
+    return self.add_count == 0
+
+  def is_full(self):
+    return self.add_count >= self._replay_capacity
+
+  def cursor(self):
+    return self.add_count % self._replay_capacity
+
+  def _check_args_length(self, *args):
+    if len(args) != len(self.get_add_args_signature()):
+      raise ValueError('Add expects {} elements, received {}'.format(
+          len(self.get_add_args_signature()), len(args)))
+
+  def _check_add_types(self, *args):
+    self._check_args_length(*args)
+    for arg, store in zip(args, self.get_add_args_signature()):
+      if isinstance(arg, np.ndarray):
+        shape = arg.shape
+      elif isinstance(arg, (tuple, list)):
+        shape = np.array(arg).shape
+      else:
+        shape = tuple()
+      if shape != tuple(store.shape):
+        raise ValueError('arg has shape {}, expected {}'.format(shape, tuple(store.shape)))
+
+  def add(self, observation, action, reward, terminal, *args):
+    """crb:234-260: pads stack_size - 1 zero transitions at episode starts."""
+    self._check_add_types(observation, action, reward, terminal, *args)
+    rows = []
+    if self.is_empty() or self._last_terminal == 1:
+      zero = [np.zeros(e.shape, dtype=e.type) for e in self.get_add_args_signature()]
+      rows.extend([zero] * (self._stack_size - 1))
+    rows.append([observation, action, reward, terminal] + list(args))
+    self._add_rows(rows)
+
+  def _priority_column(self, rows):
+    return None
+
+  def _add_rows(self, rows):
+    n = len(rows)
+    obs = np.empty((n, self._obs_bytes), np.uint8)
+    for i, r in enumerate(rows):
+      obs[i] = np.ascontiguousarray(np.asarray(r[0], dtype=self._observation_dtype)).view(np.uint8).reshape(-1)
+    act = np.array([r[1] for r in rows]).astype(np.int32)
+    rew = np.array([r[2] for r in rows]).astype(np.float32)
+    term = np.array([r[3] for r in rows]).astype(self._terminal_dtype).view(np.uint8)
+    prio = self._priority_column(rows)
+    dev = self._device
+    d_obs = torch.from_numpy(obs).to(dev, non_blocking=False)
+    d_act = torch.from_numpy(act).to(dev)
+    d_rew = torch.from_numpy(rew).to(dev)
+    d_term = torch.from_numpy(np.ascontiguousarray(term)).to(dev)
+    d_prio = torch.from_numpy(prio).to(dev) if prio is not None else None
+    base = int(self.add_count)
+    if self._extra_storage_types:
+      slots = torch.tensor([(base + i) % self._replay_capacity for i in range(n)], device=dev)
+      for j, e in enumerate(self._extra_storage_types):
+        vals = np.array([np.asarray(r[4 + j], dtype=e.type) for r in rows])
+        self._extras[e.name][slots] = torch.from_numpy(vals).to(dev)
+    _lib.call('dq_replay_add', self._h, n, _lib.ptr(d_obs), _lib.ptr(d_act), _lib.ptr(d_rew),
+              _lib.ptr(d_term), _lib.ptr(d_prio), self._stream)
+    self.add_count = np.array(base + n)
+    self._last_terminal = int(term[-1])
+    self.invalid_range = invalid_range(self.cursor(), self._replay_capacity,
+                                       self._stack_size, self._update_horizon)
+
+  # -------------------------------------------------------------- inspection
+  def get_range(self, array, start_index, end_index):
+    """crb:338-366 on a host numpy array."""
+    assert end_index > start_index, 'end_index must be larger than start_index'
+    assert end_index >= 0
+    assert start_index < self._replay_capacity
+    if not self.is_full():
+      assert end_index <= self.cursor(), 'Index {} has not been added.'.format(start_index)
+    idx = [(start_index + i) % self._replay_capacity for i in range(end_index - start_index)]
+    return array[idx, ...]
+
+  def _stack_ids(self, index):
+    return [(index - self._stack_size + 1 + k) % self._replay_capacity for k in range(self._stack_size)]
+
+  def get_observation_stack(self, index):
+    frames = self._frames[self._stack_ids(index)].cpu().numpy()
+    frames = frames.view(self._observation_dtype).reshape((self._stack_size,) + self._observation_shape)
+    return np.moveaxis(frames, 0, -1)
+
+  def get_terminal_stack(self, index):
+    return self._terminals[self._stack_ids(index)].cpu().numpy().view(self._terminal_dtype)
+
+  def is_valid_transition(self, index):
+    """crb:381-414 (host-side check, same rule as the device kernel)."""
+    if index < 0 or index >= self._replay_capacity:
+      return False
+    if not self.is_full():
+      if index >= self.cursor() - self._update_horizon:
+        return False
+      if index < self._stack_size - 1:
+        return False
+    if index in set(self.invalid_range):
+      return False
+    if self.get_terminal_stack(index)[:-1].any():
+      return False
+    return True
+
+  # ---------------------------------------------------------------- sampling
+  def _words_worst_case(self, batch_size):
+    if self._prioritized:
+      return 2 * (batch_size + self._max_sample_attempts)
+    return 4 * (batch_size + self._max_sample_attempts) + 64
+
+  def _check_status(self, meta, batch_size):
+    st = int(meta.status)
+    if st == _lib.ST_OK:
+      return
+    self._clear_status(meta)
+    if st == _lib.ST_EMPTY_TREE:
+      raise Exception('Cannot sample from an empty sum tree.')
+    if st == _lib.ST_MAX_ATTEMPTS:
+      raise RuntimeError('Max sample attempts: Tried {} times but only sampled {}'
+                         ' valid indices. Batch size is {}'.format(
+                             self._max_sample_attempts, int(meta.status_arg), batch_size))
+    if st == _lib.ST_TOO_FEW:
+      raise RuntimeError('Cannot sample a batch with fewer than stack size '
+                         '({}) + update_horizon ({}) transitions.'.format(
+                             self._stack_size, self._update_horizon))
+    if st == _lib.ST_NEG_PRIORITY:
+      raise ValueError('Sum tree values should be nonnegative. Got {}'.format(meta.status_value))
+    if st == _lib.ST_BAD_INDEX:
+      raise IndexError('index {} is out of bounds for the sum tree'.format(int(meta.status_value)))
+    raise RuntimeError('replay device status %d' % st)
+
+  def _clear_status(self, meta):
+    _lib.call('dq_replay_set_meta', self._h, int(meta.add_count), float(meta.max_recorded_priority),
+              self._stream)
+
+  def _precheck(self):
+    if not self.is_full():
+      if self.cursor() - self._update_horizon <= self._stack_size - 1:
+        raise RuntimeError('Cannot sample a batch with fewer than stack size '
+                           '({}) + update_horizon ({}) transitions.'.format(
+                               self._stack_size, self._update_horizon))
+
+  def _sample_indices_sync(self, batch_size):
+    """Launch the device sampler and bring the host RNG stream in step."""
+    self._precheck() if not self._prioritized else None
+    out = torch.empty((batch_size,), dtype=torch.int32, device=self._device)
+    words = self._words_worst_case(batch_size)
+    while True:
+      self._rng.invalidate()
+      self._rng.rebuild(words, self._stream)
+      _lib.call('dq_replay_sample_indices', self._h, batch_size, _lib.ptr(out), self._stream)
+      meta = self._read_meta()
+      if int(meta.status) == _lib.ST_TAPE_EXHAUSTED and words < self._rng.capacity:
+        self._clear_status(meta)       # nothing but the tape cursor moved: redo with more words
+        words = min(self._rng.capacity, 4 * words)
+        continue
+      break
+    self._rng.sync(self._stream, meta)
+    self._check_status(meta, batch_size)
+    return out
+
+  def sample_index_batch(self, batch_size):
+    """crb:436-477 (uniform) / prb:142-171 (prioritized); device-sampled."""
+    return [int(i) for i in self._sample_indices_sync(batch_size).cpu().numpy()]
+
+  def sample_transition_batch(self, batch_size=None, indices=None):
+    """crb:479-558: numpy tuple in get_transition_elements() order."""
+    if batch_size is None:
+      batch_size = self._batch_size
+    if indices is None:
+      d_idx = self._sample_indices_sync(batch_size)
+    else:
+      assert len(indices) == batch_size
+      d_idx = torch.as_tensor(np.asarray(indices, np.int64).astype(np.int32), device=self._device)
+    out = self._gather(d_idx, batch_size, _lib.LAYOUT_RAW)
+    S = self._stack_size
+
+    def stack(t):
+      a = t.cpu().numpy().view(self._observation_dtype).reshape((batch_size, S) + self._observation_shape)
+      return np.moveaxis(a, 1, -1)
+
+    res = [stack(out['state']), out['action'].cpu().numpy().astype(self._action_dtype),
+           out['reward'].cpu().numpy().astype(self._reward_dtype), stack(out['next_state']),
+           out['next_action'].cpu().numpy().astype(self._action_dtype),
+           out['next_reward'].cpu().numpy().astype(self._reward_dtype),
+           out['terminal'].cpu().numpy().view(np.uint8).astype(self._terminal_dtype),
+           out['indices'].cpu().numpy()]
+    for e in self._extra_storage_types:
+      res.append(out[e.name].cpu().numpy().astype(e.type))
+    if self._prioritized:
+      res.append(out['sampling_probabilities'].cpu().numpy())
+    return tuple(res)
+
+  def _alloc_batch(self, batch_size, layout):
+    B, S, dev = batch_size, self._stack_size, self._device
+    if layout == _lib.LAYOUT_F32_NORM:
+      st = (B, S) + tuple(self._observation_shape)
+      sdt = torch.float32
+    else:
+      st = (B, S, self._obs_bytes)
+      sdt = torch.uint8
+    out = {'state': torch.empty(st, dtype=sdt, device=dev),
+           'next_state': torch.empty(st, dtype=sdt, device=dev),
+           'action': torch.empty((B,), dtype=torch.int32, device=dev),
+           'reward': torch.empty((B,), dtype=torch.float32, device=dev),
+           'next_action': torch.empty((B,), dtype=torch.int32, device=dev),
+           'next_reward': torch.empty((B,), dtype=torch.float32, device=dev),
+           'terminal': torch.empty((B,), dtype=torch.uint8, device=dev),
+           'indices': torch.empty((B,), dtype=torch.int32, device=dev)}
+    if self._prioritized:
+      out['sampling_probabilities'] = torch.empty((B,), dtype=torch.float32, device=dev)
+    return out
+
+  def _gather(self, d_idx, batch_size, layout, out=None):
+    if out is None:
+      out = self._alloc_batch(batch_size, layout)
+    p = _lib.ptr
+    _lib.call('dq_replay_gather', self._h, p(d_idx), batch_size, layout, p(out['state']),
+              p(out['next_state']), p(out['action']), p(out['reward']), p(out['next_action']),
+              p(out['next_reward']), p(out['terminal']), p(out['indices']),
+              p(out.get('sampling_probabilities')), self._stream)
+    if self._extra_storage_types:
+      li = d_idx.long() % self._replay_capacity
+      for e in self._extra_storage_types:
+        out[e.name] = self._extras[e.name][li]
+    return out
+
+  # ------------------------------------------------------- device fast path
+  def sample_device(self, batch_size=None, layout=_lib.LAYOUT_F32_NORM, out=None, indices=None):
+    """Sample + gather without leaving the device or synchronising.
+
+    Returns a dict of device tensors (``state``/``next_state`` as float32 NCHW
+    normalised by 1/255 for the CNN).  The host RNG stream is brought in step
+    lazily (``sync_rng``); device-latched errors surface at the next sync."""
+    B = self._batch_size if batch_size is None else batch_size
+    if out is None:
+      out = self._alloc_batch(B, layout)
+    if indices is None:
+        self._rng.reserve(self._words_worst_case(B), self._stream)
+      if 'sample_indices' not in out:
+        out['sample_indices'] = torch.empty((B,), dtype=torch.int32, device=self._device)
+      _lib.call('dq_replay_sample_indices', self._h, B, _lib.ptr(out['sample_indices']), self._stream)
+      indices = out['sample_indices']
+    return self._gather(indices, B, layout, out)
+
+  def sync_rng(self, raise_errors=True):
+    """Bring the host RNG stream in step with the device; raise latched errors."""
+    meta = self._read_meta()
+    self._rng.sync(self._stream, meta)
+    if raise_errors:
+      self._check_status(meta, self._batch_size)
+    return meta
+
+  # -------------------------------------------------------- bulk/synthetic
+  def load_arrays(self, observations, actions, rewards, terminals, add_count, priorities=None):
+    """Bulk-replace the store (used by the synthetic benchmark and tests):
+    ``observations`` (C, obs_bytes) uint8 device/host tensor, etc."""
+    C = self._replay_capacity
+    self._frames.copy_(torch.as_tensor(observations).reshape(C, self._obs_bytes))
+    self._actions.copy_(torch.as_tensor(actions))
+    self._rewards.copy_(torch.as_tensor(rewards))
+    self._terminals.copy_(torch.as_tensor(terminals))
+    self.add_count = np.array(int(add_count))
+    self.invalid_range = invalid_range(self.cursor(), C, self._stack_size, self._update_horizon)
+    self._last_terminal = int(self._terminals[(self.cursor() - 1) % C].item())
+    maxrec = 1.0
+    if priorities is not None and self._prioritized:
+      self._set_tree_leaves(priorities)
+      maxrec = max(1.0, float(torch.as_tensor(priorities).max()))
+    _lib.call('dq_replay_set_meta', self._h, int(add_count), maxrec, self._stream)
+
+  # --------------------------------------------------------- checkpointing
+  def _return_checkpointable_elements(self):
+    elems = {STORE_FILENAME_PREFIX + n: None for n in ('observation', 'action', 'reward', 'terminal')}
+    for e in self._extra_storage_types:
+      elems[STORE_FILENAME_PREFIX + e.name] = None
+    elems['add_count'] = self.add_count
+    elems['invalid_range'] = self.invalid_range
+    return elems
+
+
+def _torch_dtype(np_dtype):
+  return torch.from_numpy(np.zeros((), dtype=np_dtype)).dtype
+
+
+class WrappedReplayBuffer(object):
+  """crb:690-915 without TF: ``transition`` holds device tensors refreshed by
+  ``sample()`` (the analogue of a session.run of the sampling py_func)."""
+
+  def __init__(self,
+               observation_shape,
+               stack_size,
+               use_staging=True,
+               replay_capacity=1000000,
+               batch_size=32,
+               update_horizon=1,
+               gamma=0.99,
+               wrapped_memory=None,
+               max_sample_attempts=1000,
+               extra_storage_types=None,
+               observation_dtype=np.uint8,
+               terminal_dtype=np.uint8,
+               action_shape=(),
+               action_dtype=np.int32,
+               reward_shape=(),
+               reward_dtype=np.float32,
+               device=None):
+    if replay_capacity < update_horizon + 1:
+      raise ValueError(
+          'Update horizon ({}) should be significantly smaller '
+          'than replay capacity ({}).'.format(update_horizon, replay_capacity))
+    if not update_horizon >= 1:
+      raise ValueError('Update horizon must be positive.')
+    if not 0.0 <= gamma <= 1.0:
+      raise ValueError('Discount factor (gamma) must be in [0, 1].')
+    self.batch_size = batch_size
+    # Staging (crb:840-872) hid host sampling latency; the device sampler has
+    # none to hide, so the flag is accepted for API compatibility only.
+    self.use_staging = use_staging
+    if wrapped_memory is not None:
+      self.memory = wrapped_memory
+    else:
+      self.memory = OutOfGraphReplayBuffer(
+          observation_shape, stack_size, replay_capacity, batch_size, update_horizon, gamma,
+          max_sample_attempts, observation_dtype=observation_dtype,
+          terminal_dtype=terminal_dtype, extra_storage_types=extra_storage_types,
+          action_shape=action_shape, action_dtype=action_dtype, reward_shape=reward_shape,
+          reward_dtype=reward_dtype, device=device)
+    layout = (_lib.LAYOUT_F32_NORM if np.dtype(observation_dtype) == np.uint8 else _lib.LAYOUT_RAW)
+    self._layout = layout
+    self.transition = collections.OrderedDict()
+    self._out = None
+
+  def add(self, observation, action, reward, terminal, *args):
+    self.memory.add(observation, action, reward, terminal, *args)
+
+  def sample(self):
+    """Refresh ``transition`` with a new device-sampled batch (no host sync)."""
+    self._out = self.memory.sample_device(self.batch_size, layout=self._layout, out=self._out)
+    self.unpack_transition(self._out)
+    return self.transition
+
+  def unpack_transition(self, out):
+    self.transition = collections.OrderedDict()
+    for e in self.memory.get_transition_elements(self.batch_size):
+      if e.name in out:
+        self.transition[e.name] = out[e.name]
+    self.states = self.transition['state']
+    self.actions = self.transition['action']
+    self.rewards = self.transition['reward']
+    self.next_states = self.transition['next_state']
+    self.next_actions = self.transition['next_action']
+    self.next_rewards = self.transition['next_reward']
+    self.terminals = self.transition['terminal']
+    self.indices = self.transition['indices']
+
+  def save(self, checkpoint_dir, iteration_number):
+    self.memory.save(checkpoint_dir, iteration_number)
+
+  def load(self, checkpoint_dir, suffix):
+    self.memory.load(checkpoint_dir, suffix)

@@ -1,0 +1,120 @@
+"""Device-resident RNG tape that continues a host MT19937 stream word for word.
+
+The reference draws its sampling randomness from two host streams:
+
+* the prioritized sampler uses Python's global ``random`` module
+  (sum_tree.py:123 ``random.random()``, sum_tree.py:165 ``random.uniform``);
+* the uniform sampler uses numpy's legacy global ``np.random``
+  (circular_replay_buffer.py:466 ``np.random.randint``).
+
+Both are MT19937.  ``random.random()`` consumes exactly two 32-bit words
+(genrand_res53) and legacy ``randint`` consumes whole 32-bit words through
+masked rejection, so the raw word sequence fully determines every draw.  This
+class copies the *next* W raw words of the host stream onto the device; the
+sampling kernels consume them and advance ``meta.tape_pos``.  At a
+synchronisation point the host stream is advanced by exactly the number of
+words the device consumed, so the Python/numpy RNG state is identical to the
+reference's after the same calls -- including the data-dependent retries.
+"""
+import random as _random
+
+import numpy as np
+import torch
+
+from dopamine_amd import _lib
+
+
+def _np_state_of(stream):
+  """(keys uint32[624], pos) of a Python Random or numpy RandomState."""
+  if isinstance(stream, np.random.RandomState) or stream is np.random:
+    st = stream.get_state()
+    return np.asarray(st[1], np.uint32), int(st[2]), st
+  st = stream.getstate()
+  return np.asarray(st[1][:624], np.uint32), int(st[1][624]), st
+
+
+def _set_stream(stream, full_state, keys, pos):
+  if isinstance(stream, np.random.RandomState) or stream is np.random:
+    stream.set_state(('MT19937', keys, pos, full_state[3], full_state[4]))
+  else:
+    stream.setstate((full_state[0], tuple(int(k) for k in keys) + (int(pos),), full_state[2]))
+
+
+class RNGTape:
+  """Keeps ``tape[0:len]`` = the next ``len`` words of ``stream`` (as of the last
+  rebuild) and ``meta.tape_pos`` = words consumed since."""
+
+  def __init__(self, replay, stream, capacity, device):
+    self._replay = replay          # the owning buffer (for its handle / meta)
+    self.stream = stream
+    self.capacity = int(capacity)
+    self.words = torch.zeros(self.capacity, dtype=torch.int32, device=device)
+    self._base = None              # full host state the tape starts from
+    self._len = 0
+    self._budget = 0               # words guaranteed left (host-side worst-case accounting)
+
+  @property
+  def valid(self):
+    return self._base is not None
+
+  def invalidate(self):
+    self._base = None
+
+  def rebuild(self, nwords, stream_handle):
+    """Draw the next ``nwords`` words of the host stream onto the device tape.
+    The host stream itself is NOT advanced (the device owns those draws)."""
+    nwords = min(int(nwords), self.capacity)
+    keys, pos, full = _np_state_of(self.stream)
+    rs = np.random.RandomState()
+    rs.set_state(('MT19937', keys, pos))
+    w = rs.randint(0, 2 ** 32, size=nwords, dtype=np.uint32).view(np.int32)
+    host = torch.from_numpy(w)
+    if self.words.is_cuda:
+      host = host.pin_memory()
+    self.words[:nwords].copy_(host, non_blocking=True)
+    self._base = full
+    self._len = nwords
+    self._budget = nwords
+    _lib.call('dq_replay_set_tape', self._replay._h, nwords, stream_handle)
+    # keep the pinned staging buffer alive until the copy is done
+    self._staging = host
+
+  def reserve(self, worst_case, stream_handle):
+    """Ensure ``worst_case`` more words are available without synchronising
+    unless the tape might run dry; returns True if it had to sync."""
+    if self.valid and self._budget >= worst_case:
+      self._budget -= worst_case
+      return False
+    synced = False
+    if self.valid:
+      self.sync(stream_handle)
+      synced = True
+    self.rebuild(max(worst_case, self.capacity), stream_handle)
+    self._budget -= worst_case
+    return synced
+
+  def sync(self, stream_handle, meta=None):
+    """Advance the host stream by the words the device consumed; invalidate."""
+    if not self.valid:
+      return meta
+    if meta is None:
+      meta = self._replay._read_meta()
+    used = int(meta.tape_pos)
+    keys, pos, _ = _np_state_of(self.stream)
+    base = self._base
+    if isinstance(self.stream, np.random.RandomState) or self.stream is np.random:
+      bkeys, bpos = np.asarray(base[1], np.uint32), int(base[2])
+    else:
+      bkeys, bpos = np.asarray(base[1][:624], np.uint32), int(base[1][624])
+    rs = np.random.RandomState()
+    rs.set_state(('MT19937', bkeys, bpos))
+    if used:
+      rs.randint(0, 2 ** 32, size=used, dtype=np.uint32)
+    st = rs.get_state()
+    _set_stream(self.stream, base, np.asarray(st[1], np.uint32), int(st[2]))
+    self._base = None
+    return meta
+
+
+def default_stream(prioritized):
+  return _random if prioritized else np.random

@@ -1,0 +1,180 @@
+/* dopamine_amd -- C ABI of the MI355X replay-sampling + Q-learning update path.
+ *
+ * The reference (K-Kielak/dopamine, TF1 + numpy) has no native ABI: its hot path
+ * sits behind the out-of-graph Python replay API and the TF graph of the agents.
+ * Each entry point below replaces one such Python/TF call; the reference
+ * interface it stands in for is cited as path:line (relative to the reference
+ * root).  Everything is plain C: opaque handles, raw pointers, sizes and an
+ * `hipStream_t` passed as `void*`.  All device buffers are owned by the caller
+ * (the Python host hands in torch allocations); the library never frees them.
+ * Every call is asynchronous on the given stream and graph-capturable except
+ * where noted "synchronous".
+ *
+ * Return values: 0 on success, negative DQ_E_* on a host-side argument/launch
+ * error (text via dq_last_error()).  Errors the reference raises *during*
+ * sampling (empty tree, max attempts, negative priority) are detected on the
+ * device and latched into dq_replay_meta.status; the host raises them with the
+ * reference's exception type and message at its next synchronisation point.
+ */
+#ifndef DOPAMINE_AMD_H
+#define DOPAMINE_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DQ_ABI_VERSION 1
+
+/* host-side return codes */
+#define DQ_OK 0
+#define DQ_E_ARG -1
+#define DQ_E_HIP -2
+
+/* device-latched status codes (dq_replay_meta.status) */
+#define DQ_ST_OK 0
+#define DQ_ST_EMPTY_TREE 1        /* sum_tree.py:116-117, 159-160 */
+#define DQ_ST_MAX_ATTEMPTS 2      /* circular_replay_buffer.py:471-475, prioritized_replay_buffer.py:159-163 */
+#define DQ_ST_TAPE_EXHAUSTED 3    /* RNG tape ran dry: host must refill before sampling */
+#define DQ_ST_NEG_PRIORITY 4      /* sum_tree.py:191-193 */
+#define DQ_ST_TOO_FEW 5           /* circular_replay_buffer.py:457-460 */
+#define DQ_ST_BAD_INDEX 6         /* leaf index outside the tree (numpy IndexError in sum_tree.py:196) */
+
+/* gather output layouts */
+#define DQ_LAYOUT_RAW 0           /* (B, stack, obs_bytes) bytes, stack-major (moveaxis on host = reference NHWC) */
+#define DQ_LAYOUT_F32_NORM 1      /* (B, stack, H*W) float32 = uint8 / 255 (atari_lib.py:96-97), CNN-ready NCHW */
+
+/* Device control block (caller allocates >= sizeof, 64-byte aligned). */
+typedef struct dq_replay_meta {
+  int64_t add_count;              /* circular_replay_buffer.py:177 */
+  int64_t tape_pos;               /* RNG words consumed from the tape */
+  int64_t tape_len;               /* RNG words valid on the tape */
+  double max_recorded_priority;   /* sum_tree.py:89, 196 */
+  int32_t status;                 /* DQ_ST_* (first error latched) */
+  int32_t status_arg;             /* e.g. #valid indices sampled before failing */
+  double status_value;            /* e.g. the negative priority */
+  int64_t reserved[2];
+} dq_replay_meta;
+
+typedef struct dq_replay_config {
+  int64_t capacity;               /* replay_capacity */
+  int64_t obs_bytes;              /* bytes of one observation (84*84 for Atari) */
+  int32_t stack_size;
+  int32_t update_horizon;
+  int32_t max_sample_attempts;
+  int32_t prioritized;            /* 1: OutOfGraphPrioritizedReplayBuffer, 0: uniform */
+  int32_t obs_is_u8;              /* enables DQ_LAYOUT_F32_NORM */
+  int32_t pad_;
+  double gamma;
+} dq_replay_config;
+
+typedef struct dq_replay_storage {   /* all device pointers, caller-owned */
+  uint8_t* frames;                /* [capacity][obs_bytes]   _store['observation'] */
+  int32_t* actions;               /* [capacity]              _store['action'] */
+  float* rewards;                 /* [capacity]              _store['reward'] */
+  uint8_t* terminals;             /* [capacity]              _store['terminal'] */
+  double* tree;                   /* [2^(depth+1)-1] heap of SumTree.nodes, or NULL (uniform) */
+  dq_replay_meta* meta;           /* control block */
+  uint32_t* tape;                 /* [tape_capacity] raw MT19937 words continuing the host stream */
+  int64_t tape_capacity;
+  float* discount;                /* [update_horizon] float32(gamma^k) (circular_replay_buffer.py:181-183) */
+} dq_replay_storage;
+
+typedef struct dq_replay dq_replay;
+
+int dq_abi_version(void);
+const char* dq_last_error(void);
+/* depth of the sum tree for a capacity: ceil(log2(capacity)) (sum_tree.py:80) */
+int dq_sumtree_depth(int64_t capacity);
+
+/* OutOfGraphReplayBuffer.__init__ (circular_replay_buffer.py:98-183) /
+ * OutOfGraphPrioritizedReplayBuffer.__init__ (prioritized_replay_buffer.py:43-97). */
+int dq_replay_create(const dq_replay_config* cfg, const dq_replay_storage* st, dq_replay** out);
+int dq_replay_destroy(dq_replay* h);
+
+/* add() / _add() for n consecutive transitions at the cursor
+ * (circular_replay_buffer.py:234-287, prioritized_replay_buffer.py:117-140).
+ * Inputs are device arrays; priorities NULL for the uniform buffer.  Padding
+ * (zero transitions) is decided by the host, which passes them explicitly. */
+int dq_replay_add(dq_replay* h, int64_t n, const uint8_t* frames, const int32_t* actions,
+                  const float* rewards, const uint8_t* terminals, const float* priorities,
+                  void* stream);
+
+/* sample_index_batch (uniform: circular_replay_buffer.py:436-477 with
+ * np.random.randint; prioritized: prioritized_replay_buffer.py:142-171 with
+ * SumTree.stratified_sample / sample, sum_tree.py:99-166).  Random numbers come
+ * from the device RNG tape; exact draw-for-draw equivalent of the reference. */
+int dq_replay_sample_indices(dq_replay* h, int32_t batch, int32_t* indices_out, void* stream);
+
+/* sample_transition_batch given indices (circular_replay_buffer.py:479-558 +
+ * prioritized_replay_buffer.py:173-201).  Any output pointer may be NULL. */
+int dq_replay_gather(dq_replay* h, const int32_t* indices, int32_t batch, int32_t layout,
+                     void* state_out, void* next_state_out, int32_t* action_out,
+                     float* reward_out, int32_t* next_action_out, float* next_reward_out,
+                     uint8_t* terminal_out, int32_t* indices_out, float* probs_out,
+                     void* stream);
+
+/* set_priority (prioritized_replay_buffer.py:203-214 -> sum_tree.py:178-205):
+ * ordered, delta-propagating float64 updates, duplicates honoured. */
+int dq_sumtree_set(dq_replay* h, const int32_t* indices, const float* priorities, int64_t n,
+                   void* stream);
+/* get_priority (prioritized_replay_buffer.py:216-235). */
+int dq_sumtree_get(dq_replay* h, const int32_t* indices, int64_t n, float* out, void* stream);
+/* Bulk (re)build of internal nodes from the leaves (parents = sum of children).
+ * Used for synthetic fills and checkpoint restore of the leaves only. */
+int dq_sumtree_rebuild(dq_replay* h, void* stream);
+
+/* Host <-> control block.  `set_meta` writes add_count / max_rec, clears status. */
+int dq_replay_set_meta(dq_replay* h, int64_t add_count, double max_recorded_priority, void* stream);
+/* Declare `len` fresh words on the tape (caller has copied them in); pos := 0. */
+int dq_replay_set_tape(dq_replay* h, int64_t len, void* stream);
+/* synchronous: copies the control block to host memory. */
+int dq_replay_read_meta(dq_replay* h, dq_replay_meta* out, void* stream);
+
+/* ---------------- learner-side kernels (stateless) ---------------- */
+
+/* Rainbow/C51 target distribution + projection + softmax cross-entropy + PER
+ * weights + new priorities (rainbow_agent.py:200-305, project_distribution
+ * rainbow_agent.py:340-494).  Logits (B, A, N) float32.  grad_logits (B,A,N) is
+ * fully written: d mean(w * loss) / d online_logits (TF CE backprop
+ * softmax - labels).  probs NULL => replay_scheme 'uniform' (weights 1).
+ * loss_out/priorities_out (B,), mean_loss_out (1,): may be NULL. */
+int dq_c51_loss(const float* online_logits, const float* target_logits, const int32_t* actions,
+                const float* rewards, const uint8_t* terminals, const float* probs,
+                const float* support, int32_t batch, int32_t num_actions, int32_t num_atoms,
+                float cumulative_gamma, float* grad_logits, float* loss_out,
+                float* priorities_out, float* mean_loss_out, void* stream);
+
+/* DQN Bellman max target + Huber(delta=1) (dqn_agent.py:283-322). */
+int dq_dqn_huber_loss(const float* online_q, const float* target_q, const int32_t* actions,
+                      const float* rewards, const uint8_t* terminals, int32_t batch,
+                      int32_t num_actions, float cumulative_gamma, float* grad_q,
+                      float* loss_out, float* mean_loss_out, void* stream);
+
+/* IQN quantile-Huber loss (implicit_quantile_agent.py:190-321).  Row order of
+ * the tiled tensors is q*B + b (atari_lib.py:174).  grad (N*B, A) fully written. */
+int dq_iqn_loss(const float* online_qv, const float* target_qv, const float* target_qv_action,
+                const float* taus, const int32_t* actions, const float* rewards,
+                const uint8_t* terminals, int32_t batch, int32_t num_actions,
+                int32_t num_tau, int32_t num_tau_prime, int32_t num_quantile,
+                float cumulative_gamma, float kappa, float* grad_qv, float* loss_out,
+                float* mean_loss_out, void* stream);
+
+/* tf.train.AdamOptimizer.apply_gradients over ONE flat fp32 parameter buffer.
+ * state[0..1] = beta1_power, beta2_power (float32, device; init beta1, beta2). */
+int dq_adam_tf1(float* var, const float* grad, float* m, float* v, float* state, int64_t n,
+                float lr, float beta1, float beta2, float eps, void* stream);
+
+/* tf.train.RMSPropOptimizer(centered=True) (dqn_agent.py:100-105; rms init 1). */
+int dq_rmsprop_tf1(float* var, const float* grad, float* ms, float* mg, float* mom, int64_t n,
+                   float lr, float decay, float momentum, float eps, int32_t centered,
+                   void* stream);
+
+/* _build_sync_op (dqn_agent.py:324-339): online -> target copy of the flat buffer. */
+int dq_sync_copy(void* dst, const void* src, int64_t bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DOPAMINE_AMD_H */

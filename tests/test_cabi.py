@@ -1,0 +1,84 @@
+"""CPU-side checks of the drop-in boundary: the HIP library loads, exports every
+symbol include/dopamine_amd.h declares, and the ctypes structs match the C ABI."""
+import ctypes
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, 'include', 'dopamine_amd.h')
+
+
+def _declared():
+  src = open(HEADER).read()
+  return sorted(set(re.findall(r'^\s*(?:int|const char\*)\s+(dq_\w+)\(', src, re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+  from dopamine_amd import _lib
+  names = _declared()
+  assert len(names) >= 18
+  for n in names:
+    assert hasattr(_lib.lib, n), n
+    assert n in _lib.SIGNATURES, 'no ctypes signature for %s' % n
+  assert set(_lib.SIGNATURES) == set(names)
+  assert _lib.lib.dq_abi_version() == _lib.ABI_VERSION
+
+
+def test_struct_layouts_match_c():
+  from dopamine_amd import _lib
+  prog = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "dopamine_amd.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(dq_replay_meta), sizeof(dq_replay_config),
+         sizeof(dq_replay_storage), offsetof(dq_replay_meta, status),
+         offsetof(dq_replay_config, gamma), offsetof(dq_replay_storage, discount));
+  return 0;
+}
+'''
+  with tempfile.TemporaryDirectory() as d:
+    c = os.path.join(d, 'sz.c')
+    open(c, 'w').write(prog)
+    exe = os.path.join(d, 'sz')
+    subprocess.run(['gcc', '-I', os.path.join(ROOT, 'include'), '-o', exe, c], check=True)
+    got = [int(x) for x in subprocess.check_output([exe]).split()]
+  exp = [ctypes.sizeof(_lib.Meta), ctypes.sizeof(_lib.Config), ctypes.sizeof(_lib.Storage),
+         _lib.Meta.status.offset, _lib.Config.gamma.offset, _lib.Storage.discount.offset]
+  assert got == exp
+
+
+def test_host_side_argument_errors_without_gpu():
+  """Argument validation happens on the host and never touches the device."""
+  from dopamine_amd import _lib
+  cfg = _lib.Config(capacity=3, obs_bytes=4, stack_size=4, update_horizon=1)
+  st = _lib.Storage()
+  h = ctypes.c_void_p()
+  rc = _lib.lib.dq_replay_create(ctypes.byref(cfg), ctypes.byref(st), ctypes.byref(h))
+  assert rc == -1
+  assert b'not enough capacity' in _lib.lib.dq_last_error()
+  assert _lib.lib.dq_sumtree_depth(1_000_000) == 20
+  assert [_lib.lib.dq_sumtree_depth(c) for c in (1, 2, 3, 4, 5, 1025)] == [0, 1, 2, 2, 3, 11]
+
+
+def test_sumtree_depth_matches_reference_formula():
+  import math
+  import numpy as np
+  from dopamine_amd import _lib
+  for c in [1, 2, 3, 7, 8, 9, 100, 1000, 4096, 4097, 50000, 1_000_000]:
+    assert _lib.lib.dq_sumtree_depth(c) == int(math.ceil(np.log2(c)))
+
+
+def test_missing_library_fails_loudly(tmp_path, monkeypatch):
+  import importlib
+  import dopamine_amd._build as b
+  monkeypatch.setattr(b, 'LIB_PATH', str(tmp_path / 'nope.so'))
+  import dopamine_amd._lib as L
+  with pytest.raises(ImportError, match='no CPU fallback'):
+    importlib.reload(L)
+  monkeypatch.undo()
+  importlib.reload(L)
