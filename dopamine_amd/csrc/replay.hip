@@ -466,7 +466,11 @@ __global__ __launch_bounds__(64) void k_sumtree_set(ReplayView v, SetArgs a) {
 
 __global__ void k_sumtree_get(ReplayView v, const int32_t* idx, int64_t n, float* out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = (float)v.tree[((int64_t)1 << v.depth) - 1 + idx[i]];
+  if (i < n) {
+    const int64_t leaf = idx[i];
+    const bool ok = leaf >= 0 && leaf < ((int64_t)1 << v.depth);
+    out[i] = ok ? (float)v.tree[((int64_t)1 << v.depth) - 1 + leaf] : 0.0f;
+  }
 }
 
 __global__ void k_sumtree_level(double* tree, int d) {

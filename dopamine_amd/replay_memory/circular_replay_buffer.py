@@ -336,7 +336,8 @@ class OutOfGraphReplayBuffer(object):
 
   def _sample_indices_sync(self, batch_size):
     """Launch the device sampler and bring the host RNG stream in step."""
-    self._precheck() if not self._prioritized else None
+    if not self._prioritized:
+      self._precheck()
     out = torch.empty((batch_size,), dtype=torch.int32, device=self._device)
     words = self._words_worst_case(batch_size)
     while True:
@@ -430,7 +431,7 @@ class OutOfGraphReplayBuffer(object):
     if out is None:
       out = self._alloc_batch(B, layout)
     if indices is None:
-        self._rng.reserve(self._words_worst_case(B), self._stream)
+      self._rng.reserve(self._words_worst_case(B), self._stream)
       if 'sample_indices' not in out:
         out['sample_indices'] = torch.empty((B,), dtype=torch.int32, device=self._device)
       _lib.call('dq_replay_sample_indices', self._h, B, _lib.ptr(out['sample_indices']), self._stream)
