@@ -1,0 +1,194 @@
+"""Benchmark: Rainbow gradient-steps/sec, batch 32, 1M-transition PER buffer
+(BASELINE.json metric, configs[2]: Rainbow/C51 Asterix, 9 actions, n=3).
+
+One step = one reference ``_train_op``: prioritized stratified sample (+retries)
+-> frame-stack gather + /255 + n-step reward -> online fwd/bwd + target fwd ->
+C51 target/projection/cross-entropy -> priority write-back -> TF1 Adam, plus the
+target sync at its reference cadence (every 8000 agent steps = 2000 gradient
+steps).  Synthetic 1M-transition buffer resident in HBM (no Atari frames
+offline).  Multi-GPU (torchrun): one learner + one 1M buffer per GPU, flat
+gradient all-reduced over RCCL each step (weak scaling).
+
+    python bench.py [--gpus N --steps K --warmup W]
+"""
+import argparse
+import ctypes
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md, HBM3E spec peak
+
+
+def parse():
+  ap = argparse.ArgumentParser()
+  ap.add_argument('--gpus', type=int, default=1)
+  ap.add_argument('--steps', type=int, default=300)
+  ap.add_argument('--warmup', type=int, default=30)
+  ap.add_argument('--capacity', type=int, default=1_000_000)
+  ap.add_argument('--batch', type=int, default=32)
+  ap.add_argument('--actions', type=int, default=9)
+  ap.add_argument('--no-graph', action='store_true')
+  ap.add_argument('--cpu-seconds', type=float, default=12.0)
+  ap.add_argument('--skip-cpu-baseline', action='store_true')
+  ap.add_argument('--gather-iters', type=int, default=400)
+  return ap.parse_args()
+
+
+def fill_synthetic(mem, A, seed):
+  """SURVEY 8(d) synthetic inputs, generated on the device."""
+  C = mem._replay_capacity
+  dev = mem._device
+  g = torch.Generator(device=dev).manual_seed(seed)
+  frames = torch.randint(0, 256, (C, mem._obs_bytes), dtype=torch.uint8, device=dev, generator=g)
+  actions = torch.randint(0, A, (C,), dtype=torch.int32, device=dev, generator=g)
+  rewards = (torch.randint(0, 3, (C,), device=dev, generator=g) - 1).float()
+  terminals = (torch.rand(C, device=dev, generator=g) < 1.0 / 500).to(torch.uint8)
+  prios = torch.rand(C, device=dev, generator=g, dtype=torch.float64) * 1.9 + 0.1
+  mem.load_arrays(frames, actions, rewards, terminals, add_count=C + 12345, priorities=prios)
+  del frames
+
+
+def time_gather(agent, iters):
+  """Average duration of the gather kernel, HIP events on the launch stream,
+  back-to-back launches captured in a HIP graph (no host launch gaps)."""
+  from dopamine_amd import _lib
+  mem = agent._replay.memory
+  out = agent._replay._out
+  idx = out['sample_indices']
+  B = agent._batch_size
+  stream = torch.cuda.current_stream()
+  for _ in range(10):
+    mem._gather(idx, B, _lib.LAYOUT_F32_NORM, out)
+  g = torch.cuda.CUDAGraph()
+  with torch.cuda.graph(g):
+    for _ in range(iters):
+      mem._gather(idx, B, _lib.LAYOUT_F32_NORM, out)
+  g.replay()
+  torch.cuda.synchronize()
+  e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+  e0.record(stream)
+  g.replay()
+  e1.record(stream)
+  e1.synchronize()
+  graph_us = e0.elapsed_time(e1) * 1e3 / iters
+  # eager back-to-back launches on the same stream, for comparison
+  e0.record(stream)
+  for _ in range(iters):
+    mem._gather(idx, B, _lib.LAYOUT_F32_NORM, out)
+  e1.record(stream)
+  e1.synchronize()
+  eager_us = e0.elapsed_time(e1) * 1e3 / iters
+  S, obs = mem._stack_size, mem._obs_bytes
+  algo_bytes = B * (2 * S * obs + 2 * S * obs * 4)   # u8 frames read + fp32 NCHW written
+  return graph_us, eager_us, algo_bytes
+
+
+def cpu_baseline(seconds, A, batch):
+  from oracle.cpu_step import CpuRainbowStep
+  threads = min(16, os.cpu_count() or 1)
+  torch.set_num_threads(threads)
+  step = CpuRainbowStep(capacity=1_000_000, batch_size=batch, num_actions=A)
+  rate, k, dt = step.time(seconds=seconds)
+  return {'value': round(rate, 3), 'unit': 'gradient-steps/s', 'cores': threads, 'kind': 'port',
+          'sample': '%d Rainbow steps (%.1f s): oracle numpy PER sampler on a 1M buffer + torch-CPU '
+                    'Nature-CNN fwd/bwd + oracle C51 loss + oracle TF1 Adam; host %s' %
+                    (k, dt, platform.processor() or platform.machine())}
+
+
+def main():
+  args = parse()
+  world = int(os.environ.get('WORLD_SIZE', '1'))
+  rank = int(os.environ.get('RANK', '0'))
+  local = int(os.environ.get('LOCAL_RANK', '0'))
+  torch.cuda.set_device(local)
+  dev = torch.device('cuda', local)
+  pg = None
+  if world > 1:
+    os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+    dist.init_process_group('nccl', device_id=dev)
+    pg = dist.group.WORLD
+  from dopamine_amd.agents.optimizers import AdamOptimizer
+  from dopamine_amd.agents.rainbow.rainbow_agent import RainbowAgent
+
+  agent = RainbowAgent(num_actions=args.actions, update_horizon=3, gamma=0.99,
+                       replay_scheme='prioritized', min_replay_history=20000, update_period=4,
+                       target_update_period=8000,
+                       optimizer=AdamOptimizer(learning_rate=0.0000625, epsilon=0.00015),
+                       replay_capacity=args.capacity, batch_size=args.batch,
+                       use_hip_graph=not args.no_graph, device=dev, seed=1000 * rank,
+                       process_group=pg)
+  import random
+  random.seed(0 + rank)
+  fill_synthetic(agent._replay.memory, args.actions, seed=1 + rank)
+  torch.cuda.synchronize()
+
+  def grad_step():
+    for _ in range(agent.update_period):   # the reference's _train_step cadence
+      agent._train_step()
+
+  for _ in range(args.warmup):
+    grad_step()
+  torch.cuda.synchronize()
+  if pg is not None:
+    dist.barrier()
+  torch.cuda.synchronize()
+  t0 = time.perf_counter()
+  for _ in range(args.steps):
+    grad_step()
+  torch.cuda.synchronize()
+  if pg is not None:
+    dist.barrier()
+  elapsed = time.perf_counter() - t0
+  if pg is not None:
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+  agent._replay.memory.sync_rng()   # raises if the device latched a sampling error
+  loss = float(agent._loss_out['mean_loss'].item())
+  assert np.isfinite(loss), 'non-finite loss'
+
+  graph_us, eager_us, algo_bytes = time_gather(agent, args.gather_iters)
+  achieved = algo_bytes / (graph_us * 1e-6) / 1e9
+
+  cpu = None
+  if rank == 0 and world == 1 and not args.skip_cpu_baseline:
+    cpu = cpu_baseline(args.cpu_seconds, args.actions, args.batch)
+
+  if rank == 0:
+    value = world * args.steps / elapsed
+    line = {
+        'metric': 'gradient-steps/sec (Rainbow, batch=32, 1M-transition buffer)',
+        'value': round(value, 2), 'unit': 'gradient-steps/s', 'n_gpus': world,
+        'steps': args.steps, 'warmup': args.warmup,
+        'ms_per_step': round(1e3 * elapsed / args.steps, 4), 'higher_is_better': True,
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'fp32', 'data': 'synthetic',
+        'config': {'workload': 'Rainbow/C51 Asterix (9 actions), prioritized sum-tree replay, '
+                               'n=3, 1M-transition 84x84x4 uint8 buffer per GPU',
+                   'global_batch': args.batch * world, 'per_gpu_batch': args.batch,
+                   'replay_capacity': args.capacity, 'parallelism': 'dp%d' % world,
+                   'hip_graph': not args.no_graph},
+        'roofline': {'kernel': 'k_gather_f32 (frame-stack gather + /255, state+next_state)',
+                     'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
+                     'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4),
+                     'traffic': None, 'algo_bytes_per_launch': algo_bytes,
+                     'avg_launch_us': round(graph_us, 3), 'avg_launch_us_eager': round(eager_us, 3)},
+        'cpu_baseline': cpu,
+        'final_mean_loss': round(loss, 5),
+    }
+    print(json.dumps(line), flush=True)
+  if pg is not None:
+    dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+  main()

@@ -1,0 +1,329 @@
+"""DQN agent with the reference's API (dopamine/agents/dqn/dqn_agent.py:76-551).
+
+Graph-mode TF1 is replaced by: device-resident replay (HIP sampler + gather),
+PyTorch-ROCm Nature-CNN forward/backward over a flat parameter buffer, the
+Bellman target + Huber loss as one HIP kernel, and the TF1 optimizer as one
+HIP kernel.  After a few eager warm-up steps the whole gradient step
+(sample -> gather -> online/target forward -> loss -> backward -> optimizer)
+is captured into a HIP graph and replayed.  ``sess`` and ``tf_device`` are
+accepted for signature compatibility.
+"""
+import math
+import os
+import random
+
+import numpy as np
+import torch
+
+from dopamine_amd import ops
+from dopamine_amd.agents import networks
+from dopamine_amd.agents.optimizers import RMSPropOptimizer
+from dopamine_amd.replay_memory import circular_replay_buffer
+
+NATURE_DQN_OBSERVATION_SHAPE = (84, 84)
+NATURE_DQN_DTYPE = np.uint8
+NATURE_DQN_STACK_SIZE = 4
+nature_dqn_network = networks.NatureDQNNetwork
+
+
+def linearly_decaying_epsilon(decay_period, step, warmup_steps, epsilon):
+  """dqn_agent.py:45-67."""
+  steps_left = decay_period + warmup_steps - step
+  bonus = (1.0 - epsilon) * steps_left / decay_period
+  bonus = np.clip(bonus, 0., 1. - epsilon)
+  return epsilon + bonus
+
+
+def identity_epsilon(unused_decay_period, unused_step, unused_warmup_steps, epsilon):
+  return epsilon
+
+
+def _device_of(tf_device, device):
+  if device is not None:
+    return torch.device(device)
+  if tf_device and 'gpu' in tf_device.lower():
+    try:
+      return torch.device('cuda', int(tf_device.rsplit(':', 1)[-1]))
+    except ValueError:
+      pass
+  return torch.device('cuda', torch.cuda.current_device())
+
+
+class DQNAgent(object):
+  """dqn_agent.py:76-551."""
+
+  def __init__(self,
+               sess=None,
+               num_actions=None,
+               observation_shape=NATURE_DQN_OBSERVATION_SHAPE,
+               observation_dtype=NATURE_DQN_DTYPE,
+               stack_size=NATURE_DQN_STACK_SIZE,
+               network=networks.NatureDQNNetwork,
+               gamma=0.99,
+               update_horizon=1,
+               min_replay_history=20000,
+               update_period=4,
+               target_update_period=8000,
+               epsilon_fn=linearly_decaying_epsilon,
+               epsilon_train=0.01,
+               epsilon_eval=0.001,
+               epsilon_decay_period=250000,
+               tf_device='/gpu:0',
+               eval_mode=False,
+               use_staging=True,
+               max_tf_checkpoints_to_keep=4,
+               optimizer=RMSPropOptimizer(learning_rate=0.00025, decay=0.95, momentum=0.0,
+                                          epsilon=0.00001, centered=True),
+               summary_writer=None,
+               summary_writing_frequency=500,
+               allow_partial_reload=False,
+               replay_capacity=1000000,
+               batch_size=32,
+               use_hip_graph=True,
+               device=None,
+               seed=0,
+               process_group=None):
+    assert num_actions is not None
+    self.num_actions = num_actions
+    self.observation_shape = tuple(observation_shape)
+    self.observation_dtype = observation_dtype
+    self.stack_size = stack_size
+    self.network = network
+    self.gamma = gamma
+    self.update_horizon = update_horizon
+    self.cumulative_gamma = math.pow(gamma, update_horizon)
+    self.min_replay_history = min_replay_history
+    self.target_update_period = target_update_period
+    self.epsilon_fn = epsilon_fn
+    self.epsilon_train = epsilon_train
+    self.epsilon_eval = epsilon_eval
+    self.epsilon_decay_period = epsilon_decay_period
+    self.update_period = update_period
+    self.eval_mode = eval_mode
+    self.training_steps = 0
+    self.optimizer = optimizer
+    self.summary_writer = summary_writer
+    self.summary_writing_frequency = summary_writing_frequency
+    self.allow_partial_reload = allow_partial_reload
+    self.max_tf_checkpoints_to_keep = max_tf_checkpoints_to_keep
+    self._replay_capacity = replay_capacity
+    self._batch_size = batch_size
+    self._device = _device_of(tf_device, device)
+    self._seed = seed
+    self._pg = process_group
+    self.use_hip_graph = use_hip_graph
+    self._graph = None
+    self._graph_opt = None
+    self._eager_steps = 0
+    self._sess = sess
+
+    state_shape = (1,) + self.observation_shape + (stack_size,)
+    self.state = np.zeros(state_shape)
+    with torch.cuda.device(self._device):
+      self._replay = self._build_replay_buffer(use_staging)
+      self._build_networks()
+      self._build_train_op()
+      self._opt = self.optimizer.build(self.online_convnet.fp.flat)
+    self._observation = None
+    self._last_observation = None
+    self.last_loss = None
+
+  # ------------------------------------------------------------ graph parts
+  def _build_replay_buffer(self, use_staging):
+    return circular_replay_buffer.WrappedReplayBuffer(
+        observation_shape=self.observation_shape, stack_size=self.stack_size,
+        use_staging=use_staging, update_horizon=self.update_horizon, gamma=self.gamma,
+        observation_dtype=self.observation_dtype, replay_capacity=self._replay_capacity,
+        batch_size=self._batch_size, device=self._device)
+
+  def _make_network(self, seed):
+    if self.network is networks.CartpoleDQNNetwork:
+      return self.network(self.num_actions, device=self._device, seed=seed)
+    return self.network(self.num_actions, stack_size=self.stack_size, device=self._device, seed=seed)
+
+  def _build_networks(self):
+    self.online_convnet = self._make_network(self._seed)
+    self.target_convnet = self._make_network(self._seed + 1)
+
+  def _build_train_op(self):
+    B, A, dev = self._batch_size, self.num_actions, self._device
+    self._loss_out = dict(grad=torch.empty((B, A), device=dev), loss=torch.empty(B, device=dev),
+                          mean_loss=torch.empty(1, device=dev))
+
+  def _state_input(self, x):
+    """(B, stack, ...) device tensor from the gather -> network input."""
+    if self.observation_shape == NATURE_DQN_OBSERVATION_SHAPE:
+      return x
+    return x.reshape(x.shape[0], -1)
+
+  def _forward_backward(self, t):
+    """Loss + backward into the flat gradient (dqn_agent.py:283-322)."""
+    with torch.no_grad():
+      tq = self.target_convnet(self._state_input(t['next_state']))
+    q = self.online_convnet(self._state_input(t['state']))
+    out = ops.dqn_huber_loss(q.detach(), tq, t['action'], t['reward'], t['terminal'],
+                             self.cumulative_gamma, out=self._loss_out)
+    self.online_convnet.fp.grad.zero_()
+    q.backward(out['grad'])
+
+  def _device_grad_step(self, reserve):
+    t = self._replay.memory.sample_device(self._batch_size, layout=self._replay._layout,
+                                          out=self._replay._out, reserve=reserve)
+    self._replay._out = t
+    self._replay.unpack_transition(t)
+    self._forward_backward(t)
+
+  def _device_opt_step(self):
+    self._opt.step(self.online_convnet.fp.grad)
+
+  def _allreduce_grads(self):
+    if self._pg is None:
+      return
+    import torch.distributed as dist
+    g = self.online_convnet.fp.grad
+    dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self._pg)
+    g.mul_(1.0 / dist.get_world_size(self._pg))
+
+  def _run_train_op(self):
+    """One gradient step (the body of sess.run(self._train_op))."""
+    mem = self._replay.memory
+    mem.reserve_rng(self._batch_size)
+    if self._graph is not None:
+      self._graph.replay()
+      self._allreduce_grads()
+      self._graph_opt.replay()
+      return
+    self._device_grad_step(reserve=False)
+    self._allreduce_grads()
+    self._device_opt_step()
+    self._eager_steps += 1
+    if self.use_hip_graph and self._eager_steps >= 3:
+      self._capture()
+
+  def _capture(self):
+    torch.cuda.synchronize(self._device)
+    g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+    # One more eager step has to be paid for by the tape (capture does not consume).
+    with torch.cuda.graph(g1):
+      self._device_grad_step(reserve=False)
+    with torch.cuda.graph(g2, pool=g1.pool()):
+      self._device_opt_step()
+    # capture recorded but did not execute: the tape position is unchanged
+    self._graph, self._graph_opt = g1, g2
+
+  def _sync_target(self):
+    ops.sync_copy(self.target_convnet.fp.flat, self.online_convnet.fp.flat)
+
+  # ------------------------------------------------------------- agent API
+  def begin_episode(self, observation):
+    self._reset_state()
+    self._record_observation(observation)
+    if not self.eval_mode:
+      self._train_step()
+    self.action = self._select_action()
+    return self.action
+
+  def step(self, reward, observation):
+    self._last_observation = self._observation
+    self._record_observation(observation)
+    if not self.eval_mode:
+      self._store_transition(self._last_observation, self.action, reward, False)
+      self._train_step()
+    self.action = self._select_action()
+    return self.action
+
+  def end_episode(self, reward):
+    if not self.eval_mode:
+      self._store_transition(self._observation, self.action, reward, True)
+
+  def _q_values(self, state_np):
+    x = torch.as_tensor(state_np, dtype=torch.float32, device=self._device)
+    x = x.permute(0, 3, 1, 2) if x.dim() == 4 else x          # NHWC -> NCHW
+    if np.dtype(self.observation_dtype) == np.uint8:
+      x = x / 255.0
+    with torch.no_grad():
+      return self._online_q(self._state_input(x.contiguous()))
+
+  def _online_q(self, x):
+    return self.online_convnet(x)
+
+  def _select_action(self):
+    """dqn_agent.py:394-416.  The replay's RNG tape is brought in step first so
+    Python's `random` stream is consumed exactly as by the reference."""
+    self._replay.memory.sync_rng()
+    if self.eval_mode:
+      epsilon = self.epsilon_eval
+    else:
+      epsilon = self.epsilon_fn(self.epsilon_decay_period, self.training_steps,
+                                self.min_replay_history, self.epsilon_train)
+    if random.random() <= epsilon:
+      return random.randint(0, self.num_actions - 1)
+    return int(torch.argmax(self._q_values(self.state), dim=1)[0].item())
+
+  def _train_step(self):
+    """dqn_agent.py:418-442."""
+    if self._replay.memory.add_count > self.min_replay_history:
+      if self.training_steps % self.update_period == 0:
+        self._run_train_op()
+        if (self.summary_writer is not None and self.training_steps > 0 and
+            self.training_steps % self.summary_writing_frequency == 0):
+          self.summary_writer.add_summary(
+              {self._loss_name: float(self._loss_out['mean_loss'].item())}, self.training_steps)
+      if self.training_steps % self.target_update_period == 0:
+        self._sync_target()
+    self.training_steps += 1
+
+  _loss_name = 'HuberLoss'
+
+  def _record_observation(self, observation):
+    self._observation = np.reshape(observation, self.observation_shape)
+    self.state = np.roll(self.state, -1, axis=-1)
+    self.state[0, ..., -1] = self._observation
+
+  def _store_transition(self, last_observation, action, reward, is_terminal):
+    self._replay.add(last_observation, action, reward, is_terminal)
+
+  def _reset_state(self):
+    self.state.fill(0)
+
+  # ---------------------------------------------------------- checkpoints
+  def _ckpt_tensors(self):
+    d = {'online': self.online_convnet.fp.flat, 'target': self.target_convnet.fp.flat}
+    for k, v in vars(self._opt).items():
+      if isinstance(v, torch.Tensor) and v.data_ptr() != self.online_convnet.fp.flat.data_ptr():
+        d['opt_' + k] = v
+    return d
+
+  def bundle_and_checkpoint(self, checkpoint_dir, iteration_number):
+    """dqn_agent.py:482-510 (torch tensors instead of a tf.train.Saver)."""
+    if not os.path.isdir(checkpoint_dir):
+      return None
+    torch.save({k: v.detach().cpu() for k, v in self._ckpt_tensors().items()},
+               os.path.join(checkpoint_dir, 'tf_ckpt-{}'.format(iteration_number)))
+    stale = iteration_number - self.max_tf_checkpoints_to_keep
+    if stale >= 0:
+      try:
+        os.remove(os.path.join(checkpoint_dir, 'tf_ckpt-{}'.format(stale)))
+      except OSError:
+        pass
+    self._replay.save(checkpoint_dir, iteration_number)
+    return {'state': self.state, 'training_steps': self.training_steps}
+
+  def unbundle(self, checkpoint_dir, iteration_number, bundle_dictionary):
+    """dqn_agent.py:512-551."""
+    try:
+      self._replay.load(checkpoint_dir, iteration_number)
+    except (FileNotFoundError, NotImplementedError):
+      if not self.allow_partial_reload:
+        return False
+    if bundle_dictionary is not None:
+      for key in self.__dict__:
+        if key in bundle_dictionary:
+          self.__dict__[key] = bundle_dictionary[key]
+    elif not self.allow_partial_reload:
+      return False
+    path = os.path.join(checkpoint_dir, 'tf_ckpt-{}'.format(iteration_number))
+    saved = torch.load(path, weights_only=True)
+    for k, v in self._ckpt_tensors().items():
+      v.copy_(saved[k].to(v.device))
+    return True

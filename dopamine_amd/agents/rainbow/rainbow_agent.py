@@ -1,0 +1,130 @@
+"""Rainbow / C51 agent (reference dopamine/agents/rainbow/rainbow_agent.py:52-494).
+
+The target distribution, the Eq.-7 projection, the softmax cross-entropy, the
+PER importance weights and the new priorities are ONE HIP kernel
+(``dq_c51_loss``); the priority write-back is the ordered sum-tree update kernel,
+stream-ordered before the optimizer exactly as the reference's
+control_dependencies order it (rainbow_agent.py:289-297).
+"""
+import numpy as np
+import torch
+
+from dopamine_amd import ops
+from dopamine_amd.agents import networks
+from dopamine_amd.agents.dqn import dqn_agent
+from dopamine_amd.agents.optimizers import AdamOptimizer
+from dopamine_amd.replay_memory import prioritized_replay_buffer
+
+
+def project_distribution(supports, weights, target_support, validate_args=False):
+  """rainbow_agent.py:340-494 as a torch expression (used for inspection and
+  by tests; the training path uses the fused HIP kernel)."""
+  supports = torch.as_tensor(supports, dtype=torch.float32)
+  weights = torch.as_tensor(weights, dtype=torch.float32)
+  target_support = torch.as_tensor(target_support, dtype=torch.float32, device=supports.device)
+  deltas = target_support[1:] - target_support[:-1]
+  delta_z = deltas[0]
+  if validate_args:
+    if supports.shape != weights.shape or supports.shape[1] != target_support.shape[0]:
+      raise ValueError('incompatible shapes')
+    if not bool((deltas > 0).all()) or not bool((deltas == delta_z).all()):
+      raise ValueError('target_support must be increasing and equally spaced')
+  clipped = supports.clamp(target_support[0], target_support[-1])[:, None, :]
+  quot = 1 - (clipped - target_support[None, :, None]).abs() / delta_z
+  return (quot.clamp(0, 1) * weights[:, None, :]).sum(-1)
+
+
+class RainbowAgent(dqn_agent.DQNAgent):
+  """rainbow_agent.py:52-337."""
+
+  def __init__(self,
+               sess=None,
+               num_actions=None,
+               observation_shape=dqn_agent.NATURE_DQN_OBSERVATION_SHAPE,
+               observation_dtype=dqn_agent.NATURE_DQN_DTYPE,
+               stack_size=dqn_agent.NATURE_DQN_STACK_SIZE,
+               network=networks.RainbowNetwork,
+               num_atoms=51,
+               vmax=10.,
+               gamma=0.99,
+               update_horizon=1,
+               min_replay_history=20000,
+               update_period=4,
+               target_update_period=8000,
+               epsilon_fn=dqn_agent.linearly_decaying_epsilon,
+               epsilon_train=0.01,
+               epsilon_eval=0.001,
+               epsilon_decay_period=250000,
+               replay_scheme='prioritized',
+               tf_device='/gpu:0',
+               use_staging=True,
+               optimizer=AdamOptimizer(learning_rate=0.00025, epsilon=0.0003125),
+               summary_writer=None,
+               summary_writing_frequency=500,
+               **kwargs):
+    vmax = float(vmax)
+    self._num_atoms = num_atoms
+    self._vmax = vmax
+    self._replay_scheme = replay_scheme
+    super().__init__(sess=sess, num_actions=num_actions, observation_shape=observation_shape,
+                     observation_dtype=observation_dtype, stack_size=stack_size, network=network,
+                     gamma=gamma, update_horizon=update_horizon,
+                     min_replay_history=min_replay_history, update_period=update_period,
+                     target_update_period=target_update_period, epsilon_fn=epsilon_fn,
+                     epsilon_train=epsilon_train, epsilon_eval=epsilon_eval,
+                     epsilon_decay_period=epsilon_decay_period, tf_device=tf_device,
+                     use_staging=use_staging, optimizer=optimizer, summary_writer=summary_writer,
+                     summary_writing_frequency=summary_writing_frequency, **kwargs)
+
+  _loss_name = 'CrossEntropyLoss'
+
+  def _build_replay_buffer(self, use_staging):
+    if self._replay_scheme not in ['uniform', 'prioritized']:
+      raise ValueError('Invalid replay scheme: {}'.format(self._replay_scheme))
+    return prioritized_replay_buffer.WrappedPrioritizedReplayBuffer(
+        observation_shape=self.observation_shape, stack_size=self.stack_size,
+        use_staging=use_staging, update_horizon=self.update_horizon, gamma=self.gamma,
+        observation_dtype=self.observation_dtype, replay_capacity=self._replay_capacity,
+        batch_size=self._batch_size, device=self._device)
+
+  def _make_network(self, seed):
+    return self.network(self.num_actions, num_atoms=self._num_atoms, stack_size=self.stack_size,
+                        device=self._device, seed=seed)
+
+  def _build_train_op(self):
+    B, A, N, dev = self._batch_size, self.num_actions, self._num_atoms, self._device
+    # tf.linspace(-vmax, vmax, num_atoms) in float32 (rainbow_agent.py:126)
+    step = np.float32(2 * self._vmax) / np.float32(N - 1)
+    sup = (np.float32(-self._vmax) + step * np.arange(N, dtype=np.float32)).astype(np.float32)
+    self._support = torch.from_numpy(sup).to(dev)
+    self._loss_out = dict(grad=torch.empty((B, A, N), device=dev), loss=torch.empty(B, device=dev),
+                          priorities=torch.empty(B, device=dev), mean_loss=torch.empty(1, device=dev))
+
+  def _online_q(self, x):
+    logits = self.online_convnet(x)
+    return (torch.softmax(logits, -1) * self._support).sum(-1)
+
+  def _forward_backward(self, t):
+    with torch.no_grad():
+      target_logits = self.target_convnet(t['next_state'])
+    logits = self.online_convnet(t['state'])
+    prioritized = self._replay_scheme == 'prioritized'
+    out = ops.c51_loss(logits.detach(), target_logits, t['action'], t['reward'], t['terminal'],
+                       self._support, self.cumulative_gamma,
+                       probs=t['sampling_probabilities'] if prioritized else None,
+                       out=self._loss_out)
+    if prioritized:
+      # sqrt(loss + 1e-10) of the UNWEIGHTED loss, before the optimizer (rb:289-297)
+      self._replay.tf_set_priority(t['indices'], out['priorities'])
+    self.online_convnet.fp.grad.zero_()
+    logits.backward(out['grad'])
+
+  def _store_transition(self, last_observation, action, reward, is_terminal, priority=None):
+    """rainbow_agent.py:307-337."""
+    if priority is None:
+      if self._replay_scheme == 'uniform':
+        priority = 1.
+      else:
+        priority = self._replay.memory.sum_tree.max_recorded_priority
+    if not self.eval_mode:
+      self._replay.add(last_observation, action, reward, is_terminal, priority)

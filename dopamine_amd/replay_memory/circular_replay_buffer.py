@@ -130,6 +130,8 @@ class OutOfGraphReplayBuffer(object):
     self._cfg = cfg
     self._h = None
     self._bind(self._rng.words, self._rng.capacity)
+    # add_count 0, SumTree.max_recorded_priority = 1.0 (sum_tree.py:89)
+    _lib.call('dq_replay_set_meta', self._h, 0, 1.0, self._stream)
 
   def _bind(self, tape, tape_cap):
     st = _lib.Storage()
@@ -421,17 +423,29 @@ class OutOfGraphReplayBuffer(object):
     return out
 
   # ------------------------------------------------------- device fast path
-  def sample_device(self, batch_size=None, layout=_lib.LAYOUT_F32_NORM, out=None, indices=None):
+  def reserve_rng(self, batch_size=None):
+    """Host-side tape bookkeeping for one upcoming device sample (call outside
+    graph capture; may synchronise and refill the tape)."""
+    B = self._batch_size if batch_size is None else batch_size
+    if not self._prioritized:
+      self._precheck()
+    return self._rng.reserve(self._words_worst_case(B), self._stream)
+
+  def sample_device(self, batch_size=None, layout=_lib.LAYOUT_F32_NORM, out=None, indices=None,
+                    reserve=True):
     """Sample + gather without leaving the device or synchronising.
 
     Returns a dict of device tensors (``state``/``next_state`` as float32 NCHW
     normalised by 1/255 for the CNN).  The host RNG stream is brought in step
-    lazily (``sync_rng``); device-latched errors surface at the next sync."""
+    lazily (``sync_rng``); device-latched errors surface at the next sync.
+    ``reserve=False`` skips the host tape bookkeeping (the caller did it with
+    ``reserve_rng``, e.g. around a HIP-graph replay)."""
     B = self._batch_size if batch_size is None else batch_size
     if out is None:
       out = self._alloc_batch(B, layout)
     if indices is None:
-      self._rng.reserve(self._words_worst_case(B), self._stream)
+      if reserve:
+        self.reserve_rng(B)
       if 'sample_indices' not in out:
         out['sample_indices'] = torch.empty((B,), dtype=torch.int32, device=self._device)
       _lib.call('dq_replay_sample_indices', self._h, B, _lib.ptr(out['sample_indices']), self._stream)

@@ -1,0 +1,98 @@
+"""End-to-end learner step on the device vs a CPU restatement of the same step
+(same sampled batch, same weights): loss, priorities, gradients and the TF1
+Adam update.  Also: HIP-graph replay == eager execution."""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import learner as OL
+
+pytestmark = pytest.mark.gpu
+
+
+def _fill(mem, A, seed):
+  C = mem._replay_capacity
+  rs = np.random.RandomState(seed)
+  mem.load_arrays(torch.from_numpy(rs.randint(0, 256, (C, 84 * 84), dtype=np.uint8)),
+                  torch.from_numpy(rs.randint(0, A, C).astype(np.int32)),
+                  torch.from_numpy(rs.choice(np.array([-1, 0, 1], np.float32), C)),
+                  torch.from_numpy((rs.rand(C) < 0.01).astype(np.uint8)), add_count=C + 77,
+                  priorities=rs.uniform(0.1, 2.0, C) if mem._prioritized else None)
+
+
+def _rainbow(**kw):
+  from dopamine_amd.agents.optimizers import AdamOptimizer
+  from dopamine_amd.agents.rainbow.rainbow_agent import RainbowAgent
+  a = RainbowAgent(num_actions=9, update_horizon=3, replay_capacity=3000, batch_size=32,
+                   min_replay_history=100, optimizer=AdamOptimizer(6.25e-5, epsilon=1.5e-4), **kw)
+  _fill(a._replay.memory, 9, 3)
+  return a
+
+
+def test_rainbow_step_matches_cpu_restatement():
+  random.seed(11)
+  a = _rainbow(use_hip_graph=False)
+  w0 = a.online_convnet.fp.flat.detach().cpu().clone()
+  tw = a.target_convnet.fp.flat.detach().cpu().clone()
+  a._run_train_op()
+  torch.cuda.synchronize()
+  t = {k: v.detach().cpu() for k, v in a._replay.transition.items()}
+  # CPU restatement on the same batch and weights
+  from dopamine_amd.agents.networks import RainbowNetwork
+  on = RainbowNetwork(9, device='cpu'); on.fp.flat.copy_(w0)
+  tg = RainbowNetwork(9, device='cpu'); tg.fp.flat.copy_(tw)
+  with torch.no_grad():
+    tl = tg(t['next_state']).double().numpy()
+  logits = on(t['state'])
+  exp = OL.c51_loss(logits.detach().double().numpy(), tl, t['action'].numpy(), t['reward'].numpy(),
+                    t['terminal'].numpy(), OL.c51_support(10.0, 51, np.float32), np.float32(0.99 ** 3),
+                    t['sampling_probabilities'].numpy())
+  np.testing.assert_allclose(a._loss_out['loss'].cpu().numpy(), exp['loss'], rtol=1e-4, atol=1e-5)
+  on.fp.grad.zero_()
+  logits.backward(torch.from_numpy(exp['grad'].astype(np.float32)))
+  np.testing.assert_allclose(a.online_convnet.fp.grad.cpu().numpy(), on.fp.grad.numpy(),
+                             rtol=1e-3, atol=1e-6)
+  adam = OL.TF1Adam(on.fp.numel, 6.25e-5, eps=1.5e-4)
+  w = w0.numpy().copy()
+  adam.step(w, a.online_convnet.fp.grad.cpu().numpy())
+  np.testing.assert_allclose(a.online_convnet.fp.flat.cpu().numpy(), w, rtol=1e-5, atol=1e-7)
+  # the priorities written back are sqrt(loss + 1e-10) of this step
+  pri = a._replay.memory.get_priority(t['indices'].numpy().astype(np.int32))
+  np.testing.assert_allclose(pri, np.sqrt(exp['loss'] + 1e-10), rtol=1e-4)
+
+
+@pytest.mark.parametrize('kind', ['rainbow', 'dqn', 'iqn'])
+def test_hip_graph_replay_matches_eager(kind):
+  from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
+  from dopamine_amd.agents.implicit_quantile.implicit_quantile_agent import ImplicitQuantileAgent
+
+  def make(graph):
+    random.seed(5); np.random.seed(5); torch.manual_seed(5)
+    if kind == 'rainbow':
+      return _rainbow(use_hip_graph=graph)
+    if kind == 'dqn':
+      a = DQNAgent(num_actions=6, replay_capacity=3000, batch_size=32, min_replay_history=100,
+                   use_hip_graph=graph)
+    else:
+      a = ImplicitQuantileAgent(num_actions=4, replay_capacity=3000, batch_size=16,
+                                num_tau_samples=8, num_tau_prime_samples=8, num_quantile_samples=4,
+                                min_replay_history=100, update_horizon=3, replay_scheme='uniform',
+                                use_hip_graph=graph)
+    _fill(a._replay.memory, a.num_actions, 3)
+    return a
+
+  res = []
+  for graph in (False, True):
+    a = make(graph)
+    idx = []
+    for _ in range(8):
+      a._run_train_op()
+      idx.append(a._replay.transition['indices'].cpu().numpy().copy())
+    a._replay.memory.sync_rng()
+    res.append((np.stack(idx), a.online_convnet.fp.flat.cpu().numpy(), float(a._loss_out['mean_loss'].item())))
+    assert (a._graph is not None) == graph
+  np.testing.assert_array_equal(res[0][0], res[1][0])
+  if kind != 'iqn':   # IQN taus come from torch's RNG, whose graph-safe offsets differ from eager
+    np.testing.assert_allclose(res[0][1], res[1][1], rtol=1e-4, atol=1e-6)
