@@ -16,6 +16,7 @@ import numpy as np
 import torch
 
 from dopamine_amd import ops
+from dopamine_amd import parallel
 from dopamine_amd.agents import networks
 from dopamine_amd.agents.optimizers import RMSPropOptimizer
 from dopamine_amd.replay_memory import circular_replay_buffer
@@ -179,10 +180,7 @@ class DQNAgent(object):
   def _allreduce_grads(self):
     if self._pg is None:
       return
-    import torch.distributed as dist
-    g = self.online_convnet.fp.grad
-    dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self._pg)
-    g.mul_(1.0 / dist.get_world_size(self._pg))
+    parallel.allreduce_mean_(self.online_convnet.fp.grad, self._pg)
 
   def _run_train_op(self):
     """One gradient step (the body of sess.run(self._train_op))."""
