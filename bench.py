@@ -154,7 +154,7 @@ def main():
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
   agent._replay.memory.sync_rng()   # raises if the device latched a sampling error
-  loss = float(agent._loss_out['mean_loss'].item())
+  loss = agent.mean_loss()
   assert np.isfinite(loss), 'non-finite loss'
 
   graph_us, eager_us, algo_bytes = time_gather(agent, args.gather_iters)

@@ -11,7 +11,7 @@ from dopamine_amd._build import HEADER, LIB_PATH  # noqa: F401
 ABI_VERSION = 1
 OK = 0
 ST_OK, ST_EMPTY_TREE, ST_MAX_ATTEMPTS, ST_TAPE_EXHAUSTED, ST_NEG_PRIORITY, ST_TOO_FEW, ST_BAD_INDEX = range(7)
-LAYOUT_RAW, LAYOUT_F32_NORM = 0, 1
+LAYOUT_RAW, LAYOUT_F32_NORM, LAYOUT_F32_NHWC = 0, 1, 2
 
 
 class Meta(ctypes.Structure):

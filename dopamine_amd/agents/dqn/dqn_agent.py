@@ -265,13 +265,16 @@ class DQNAgent(object):
         self._run_train_op()
         if (self.summary_writer is not None and self.training_steps > 0 and
             self.training_steps % self.summary_writing_frequency == 0):
-          self.summary_writer.add_summary(
-              {self._loss_name: float(self._loss_out['mean_loss'].item())}, self.training_steps)
+          self.summary_writer.add_summary({self._loss_name: self.mean_loss()}, self.training_steps)
       if self.training_steps % self.target_update_period == 0:
         self._sync_target()
     self.training_steps += 1
 
   _loss_name = 'HuberLoss'
+
+  def mean_loss(self):
+    """Mean loss of the last gradient step (the summary scalar, dqn:318-321)."""
+    return float(self._loss_out['mean_loss'].item())
 
   def _record_observation(self, observation):
     self._observation = np.reshape(observation, self.observation_shape)

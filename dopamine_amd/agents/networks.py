@@ -35,9 +35,17 @@ class FlatParams(object):
     self.params = {}
     for name, (o, shape) in self.offsets.items():
       n = int(np.prod(shape))
-      p = torch.nn.Parameter(self.flat[o:o + n].view(shape))
-      p.grad = self.grad[o:o + n].view(shape)
+      p = torch.nn.Parameter(self._view(self.flat, o, shape))
+      p.grad = self._view(self.grad, o, shape)
       self.params[name] = p
+
+  @staticmethod
+  def _view(buf, o, shape):
+    n = int(np.prod(shape))
+    if len(shape) == 4:   # conv filters stored (out, kh, kw, in): channels_last for MIOpen NHWC
+      out_c, in_c, kh, kw = shape
+      return buf[o:o + n].view(out_c, kh, kw, in_c).permute(0, 3, 1, 2)
+    return buf[o:o + n].view(shape)
 
   def __getitem__(self, name):
     return self.params[name]
@@ -89,11 +97,16 @@ class _Net(object):
 
 
 def _torso(fp, x):
-  """Nature-CNN torso with TF SAME padding: 84 -> 21 -> 11 -> 11; 7744 features."""
+  """Nature-CNN torso with TF SAME padding: 84 -> 21 -> 11 -> 11; 7744 features.
+
+  Activations are channels_last (NHWC in memory: MIOpen's NHWC kernels run
+  without layout transposes) and the flatten is in (h, w, c) order, i.e. exactly
+  TF's slim.flatten of the reference's NHWC tensors (atari_lib.py:101)."""
+  x = x.contiguous(memory_format=torch.channels_last)
   x = F.relu(F.conv2d(x, fp['conv1_w'], fp['conv1_b'], stride=4, padding=2))
   x = F.relu(F.conv2d(F.pad(x, (1, 2, 1, 2)), fp['conv2_w'], fp['conv2_b'], stride=2))
   x = F.relu(F.conv2d(x, fp['conv3_w'], fp['conv3_b'], stride=1, padding=1))
-  return x.flatten(1)
+  return x.permute(0, 2, 3, 1).flatten(1)
 
 
 def _torso_shapes(stack):

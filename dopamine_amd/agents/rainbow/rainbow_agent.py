@@ -97,8 +97,17 @@ class RainbowAgent(dqn_agent.DQNAgent):
     step = np.float32(2 * self._vmax) / np.float32(N - 1)
     sup = (np.float32(-self._vmax) + step * np.arange(N, dtype=np.float32)).astype(np.float32)
     self._support = torch.from_numpy(sup).to(dev)
+    # mean_loss=None: the summary mean is not on the gradient path (computed on demand)
     self._loss_out = dict(grad=torch.empty((B, A, N), device=dev), loss=torch.empty(B, device=dev),
-                          priorities=torch.empty(B, device=dev), mean_loss=torch.empty(1, device=dev))
+                          priorities=torch.empty(B, device=dev), mean_loss=None)
+
+  def mean_loss(self):
+    """mean(w * CE) of the last step (the CrossEntropyLoss summary, rb:298-301)."""
+    loss = self._loss_out['loss']
+    if self._replay_scheme == 'prioritized':
+      w = 1.0 / torch.sqrt(self._replay.transition['sampling_probabilities'] + 1e-10)
+      loss = loss * (w / w.max())
+    return float(loss.mean().item())
 
   def _online_q(self, x):
     logits = self.online_convnet(x)

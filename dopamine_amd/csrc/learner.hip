@@ -27,97 +27,110 @@ struct C51Args {
   float* mean_out;
 };
 
+// PER importance weight of sample b, normalised by the batch max (rb:277-280).
+// Every block recomputes the max over the B probabilities (B tiny loads) so no
+// cross-block reduction is needed.
+__device__ float per_weight(const float* probs, int B, int b, float* s_red) {
+  if (!probs) return 1.0f;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  float m = 0.0f;
+  for (int i = threadIdx.x; i < B; i += blockDim.x)
+    m = fmaxf(m, __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(probs[i], 1e-10f))));
+  m = wave_max(m);
+  if (lane == 0) s_red[wave] = m;
+  __syncthreads();
+  m = s_red[0];
+  for (int i = 1; i < nw; ++i) m = fmaxf(m, s_red[i]);
+  const float w = __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(probs[b], 1e-10f)));
+  return __fdiv_rn(w, m);
+}
+
+// One block per sample b; wave a (strided) computes the target softmax / Q of
+// action a; wave 0 then takes the greedy action (first max), builds Tz, the
+// Eq.-7 projection (lane = target atom, LDS broadcast of the source atoms) and
+// the softmax cross-entropy of the chosen online logits; the other waves zero
+// the gradient rows of the non-chosen actions.
 __global__ __launch_bounds__(1024) void k_c51(C51Args a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* s_diff = smem;                 // [B][N]  softmax - projection
-  float* s_loss = s_diff + a.B * a.N;   // [B]
-  float* s_w = s_loss + a.B;            // [B]
+  const int N = a.N, A = a.A, b = blockIdx.x;
+  float* s_p = smem;                 // [A][N] target probabilities
+  float* s_q = s_p + A * N;          // [A]    target Q
+  float* s_tz = s_q + A;             // [N]    clipped Bellman support
   __shared__ float s_red[16];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int N = a.N, A = a.A;
   const bool on = lane < N;
+  const float ninf = -__builtin_inff();
   const float z = on ? a.support[lane] : 0.0f;
+  for (int act = wave; act < A; act += nw) {
+    const float x = on ? a.tl[((int64_t)b * A + act) * N + lane] : ninf;
+    const float mx = wave_max(x);
+    const float e = on ? expf(__fsub_rn(x, mx)) : 0.0f;
+    const float p = __fdiv_rn(e, wave_sum(e));
+    const float q = wave_sum(on ? __fmul_rn(z, p) : 0.0f);
+    if (on) s_p[act * N + lane] = p;
+    if (lane == 0) s_q[act] = q;
+  }
+  const int ab = a.act[b];
+  const float w = per_weight(a.probs, a.B, b, s_red);   // contains a __syncthreads
+  const float gscale = __fmul_rn(w, __fdiv_rn(1.0f, (float)a.B));
+  for (int act = wave; act < A; act += nw) {
+    if (act == ab) continue;
+    if (on) a.grad[((int64_t)b * A + act) * N + lane] = 0.0f;
+  }
+  if (wave != 0) return;
+  int astar = 0;
+  float best = s_q[0];
+  for (int act = 1; act < A; ++act)
+    if (s_q[act] > best) {
+      best = s_q[act];
+      astar = act;
+    }
   const float vmin = a.support[0], vmax = a.support[N - 1];
   const float dz = __fsub_rn(a.support[1], a.support[0]);
-  const float ninf = -__builtin_inff();
-  for (int b = wave; b < a.B; b += nw) {
-    // target net: probabilities, Q = sum z p, greedy action (first max)
-    float best = ninf, pbest = 0.0f;
-    for (int act = 0; act < A; ++act) {
-      const float x = on ? a.tl[((int64_t)b * A + act) * N + lane] : ninf;
-      const float mx = wave_max(x);
-      const float e = on ? expf(__fsub_rn(x, mx)) : 0.0f;
-      const float p = __fdiv_rn(e, wave_sum(e));
-      const float q = wave_sum(on ? __fmul_rn(z, p) : 0.0f);
-      if (act == 0 || q > best) {
-        best = q;
-        pbest = p;
-      }
-    }
-    // Bellman support Tz = r + gamma^n (1 - terminal) z, clipped, projected (Eq. 7)
-    const float gt = __fmul_rn(a.cg, __fsub_rn(1.0f, (float)a.term[b]));
-    const float tz = __fadd_rn(a.rew[b], __fmul_rn(gt, z));
-    const float tzc = fminf(fmaxf(tz, vmin), vmax);
-    float proj = 0.0f;
+  const float gt = __fmul_rn(a.cg, __fsub_rn(1.0f, (float)a.term[b]));
+  if (on) s_tz[lane] = fminf(fmaxf(__fadd_rn(a.rew[b], __fmul_rn(gt, z)), vmin), vmax);
+  __builtin_amdgcn_s_barrier();   // single wave: orders the LDS writes above before the reads
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  const float* pst = s_p + astar * N;
+  float proj = 0.0f;
+  if (on) {
     for (int j = 0; j < N; ++j) {
-      const float cj = __shfl(tzc, j), pj = __shfl(pbest, j);
-      float w = __fsub_rn(1.0f, __fdiv_rn(fabsf(__fsub_rn(cj, z)), dz));
-      w = fminf(fmaxf(w, 0.0f), 1.0f);
-      proj = __fadd_rn(proj, __fmul_rn(w, pj));
+      float c = __fsub_rn(1.0f, __fdiv_rn(fabsf(__fsub_rn(s_tz[j], z)), dz));
+      c = fminf(fmaxf(c, 0.0f), 1.0f);
+      proj = __fadd_rn(proj, __fmul_rn(c, pst[j]));
     }
-    if (!on) proj = 0.0f;
-    // softmax cross-entropy on the chosen action's online logits
-    const int ab = a.act[b];
-    const float y = on ? a.ol[((int64_t)b * A + ab) * N + lane] : ninf;
-    const float my = wave_max(y);
-    const float sh = on ? __fsub_rn(y, my) : 0.0f;
-    const float ey = on ? expf(sh) : 0.0f;
-    const float sy = wave_sum(ey);
-    const float lse = logf(sy);
-    const float loss = wave_sum(on ? __fmul_rn(proj, __fsub_rn(lse, sh)) : 0.0f);
-    if (on) s_diff[b * N + lane] = __fsub_rn(__fdiv_rn(ey, sy), proj);
-    if (lane == 0) s_loss[b] = loss;
   }
-  __syncthreads();
-  // PER importance weights  w = 1/sqrt(p + 1e-10), w /= max(w)   (rb:277-280)
-  float wmax = 0.0f;
-  for (int b = threadIdx.x; b < a.B; b += blockDim.x) {
-    const float w = a.probs ? __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(a.probs[b], 1e-10f))) : 1.0f;
-    s_w[b] = w;
-    wmax = fmaxf(wmax, w);
+  const float y = on ? a.ol[((int64_t)b * A + ab) * N + lane] : ninf;
+  const float my = wave_max(y);
+  const float sh = on ? __fsub_rn(y, my) : 0.0f;
+  const float ey = on ? expf(sh) : 0.0f;
+  const float sy = wave_sum(ey);
+  const float loss = wave_sum(on ? __fmul_rn(proj, __fsub_rn(logf(sy), sh)) : 0.0f);
+  if (on)
+    a.grad[((int64_t)b * A + ab) * N + lane] = __fmul_rn(gscale, __fsub_rn(__fdiv_rn(ey, sy), proj));
+  if (lane == 0) {
+    if (a.loss_out) a.loss_out[b] = loss;
+    if (a.prio_out) a.prio_out[b] = __fsqrt_rn(__fadd_rn(loss, 1e-10f));
   }
-  wmax = wave_max(wmax);
-  if (lane == 0) s_red[wave] = wmax;
-  __syncthreads();
-  wmax = s_red[0];
-  for (int i = 1; i < nw; ++i) wmax = fmaxf(wmax, s_red[i]);
-  __syncthreads();
-  float part = 0.0f;
-  for (int b = threadIdx.x; b < a.B; b += blockDim.x) {
-    const float w = a.probs ? __fdiv_rn(s_w[b], wmax) : 1.0f;
-    s_w[b] = w;
-    const float l = s_loss[b];
-    if (a.loss_out) a.loss_out[b] = l;
-    if (a.prio_out) a.prio_out[b] = __fsqrt_rn(__fadd_rn(l, 1e-10f));
-    part = __fadd_rn(part, __fmul_rn(w, l));
+}
+
+// mean(w * loss) for summaries (rb:298-301); launched only when requested.
+__global__ __launch_bounds__(64) void k_wmean(const float* loss, const float* probs, int B,
+                                              float* out) {
+  float wmax = 1.0f;
+  if (probs) {
+    float m = 0.0f;
+    for (int i = threadIdx.x; i < B; i += 64)
+      m = fmaxf(m, __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(probs[i], 1e-10f))));
+    wmax = wave_max(m);
   }
-  part = wave_sum(part);
-  if (lane == 0) s_red[wave] = part;
-  __syncthreads();
-  if (threadIdx.x == 0 && a.mean_out) {
-    float t = 0.0f;
-    for (int i = 0; i < nw; ++i) t = __fadd_rn(t, s_red[i]);
-    a.mean_out[0] = __fdiv_rn(t, (float)a.B);
+  float acc = 0.0f;
+  for (int b = threadIdx.x; b < B; b += 64) {
+    const float w = probs ? __fdiv_rn(__fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(probs[b], 1e-10f))), wmax) : 1.0f;
+    acc = __fadd_rn(acc, __fmul_rn(w, loss[b]));
   }
-  // d mean(w * CE) / d logits: (w_b / B) (softmax - proj) on the chosen action, 0 elsewhere
-  const float invB = __fdiv_rn(1.0f, (float)a.B);
-  const int64_t total = (int64_t)a.B * A * N;
-  for (int64_t t = threadIdx.x; t < total; t += blockDim.x) {
-    const int b = (int)(t / ((int64_t)A * N));
-    const int r = (int)(t - (int64_t)b * A * N);
-    const int act = r / N, i = r - act * N;
-    a.grad[t] = (act == a.act[b]) ? __fmul_rn(__fmul_rn(s_w[b], invB), s_diff[b * N + i]) : 0.0f;
-  }
+  acc = wave_sum(acc);
+  if (threadIdx.x == 0) out[0] = __fdiv_rn(acc, (float)B);
 }
 
 // ---------------------------------------------------------------------------
@@ -315,14 +328,20 @@ int dq_c51_loss(const float* online_logits, const float* target_logits, const in
                    grad_logits,
                "null argument");
   DQ_CHECK_ARG(num_atoms >= 2 && num_atoms <= 64, "num_atoms must be in [2, 64]");
-  DQ_CHECK_ARG(batch >= 1 && batch <= 256 && num_actions >= 1, "batch must be in [1, 256]");
+  DQ_CHECK_ARG(batch >= 1 && num_actions >= 1 && num_actions <= 256, "bad batch / num_actions");
   C51Args a{online_logits, target_logits, actions, rewards, terminals, probs, support,
             batch, num_actions, num_atoms, cumulative_gamma, grad_logits, loss_out,
             priorities_out, mean_loss_out};
-  const size_t shm = sizeof(float) * ((size_t)batch * num_atoms + 2 * (size_t)batch);
-  const int threads = batch >= 16 ? 1024 : 64 * batch;
-  hipLaunchKernelGGL(k_c51, dim3(1), dim3(threads), shm, (hipStream_t)stream, a);
+  DQ_CHECK_ARG(!mean_loss_out || loss_out, "mean_loss_out needs loss_out");
+  const size_t shm = sizeof(float) * ((size_t)num_actions * num_atoms + num_actions + num_atoms);
+  const int waves = num_actions < 16 ? num_actions : 16;
+  hipLaunchKernelGGL(k_c51, dim3(batch), dim3(64 * waves), shm, (hipStream_t)stream, a);
   DQ_CHECK_LAUNCH("k_c51");
+  if (mean_loss_out) {
+    hipLaunchKernelGGL(k_wmean, dim3(1), dim3(64), 0, (hipStream_t)stream, loss_out, probs, batch,
+                       mean_loss_out);
+    DQ_CHECK_LAUNCH("k_wmean");
+  }
   return DQ_OK;
 }
 

@@ -299,6 +299,149 @@ struct GatherOut {
   float* probs;
 };
 
+// n-step trajectory length with every terminal byte of the trajectory loaded up
+// front (independent loads, no serial early exit).  Same result as traj_len.
+__device__ __forceinline__ int traj_len_par(const ReplayView& v, int64_t idx, bool* term) {
+  for (int j0 = 0; j0 < v.n; j0 += 8) {
+    uint8_t t[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) t[q] = (j0 + q < v.n) ? v.terminals[pymod(idx + j0 + q, v.C)] : 0;
+    int first = -1;
+#pragma unroll
+    for (int q = 7; q >= 0; --q)
+      if (t[q]) first = q;
+    if (first >= 0) {
+      *term = true;
+      return j0 + first + 1;
+    }
+  }
+  *term = false;
+  return v.n;
+}
+
+__device__ __forceinline__ int64_t stack_base(const ReplayView& v, const GatherOut& g, int b,
+                                              int which) {
+  int64_t base = pymod((int64_t)g.indices[b], v.C);
+  if (which) {
+    bool term;
+    base = pymod(base + traj_len_par(v, base, &term), v.C);
+  }
+  return base;
+}
+
+// Per-sample scalars (crb:517-555), one wave: lanes load the trajectory's
+// terminal/reward bytes in parallel, the ballot finds L, lane 0 sums the
+// float32 products left to right exactly as numpy's n < 8 reduction does.
+__device__ void write_scalars_wave(const ReplayView& v, const GatherOut& g, int b) {
+  const int lane = threadIdx.x & 63;
+  const int64_t idx = pymod((int64_t)g.indices[b], v.C);
+  float p = 0.0f;
+  bool t = false;
+  if (lane < v.n) {
+    const int64_t j = pymod(idx + lane, v.C);
+    t = v.terminals[j] != 0;
+    p = __fmul_rn(v.discount[lane], v.rewards[j]);
+  }
+  // trajectories longer than a wave are finished by lane 0 below (n > 64 is unheard of)
+  const uint64_t tm = __ballot(t);
+  int L = v.n;
+  bool term = false;
+  if (tm) {
+    L = __ffsll((unsigned long long)tm);
+    term = true;
+  }
+  float acc = 0.0f;
+  for (int k = 0; k < L && k < kWave; ++k) acc = __fadd_rn(acc, __shfl(p, k));
+  if (lane == 0) {
+    if (v.n > kWave) {  // generic tail, serial
+      bool tt;
+      L = traj_len(v, idx, &tt);
+      term = tt;
+      acc = 0.0f;
+      for (int k = 0; k < L; ++k)
+        acc = __fadd_rn(acc, __fmul_rn(v.discount[k], v.rewards[pymod(idx + k, v.C)]));
+    }
+    const int64_t nxt = pymod(idx + L, v.C);
+    if (g.action) g.action[b] = v.actions[idx];
+    if (g.reward) g.reward[b] = acc;
+    if (g.next_action) g.next_action[b] = v.actions[nxt];
+    if (g.next_reward) g.next_reward[b] = v.rewards[nxt];
+    if (g.terminal) g.terminal[b] = term ? 1 : 0;
+    if (g.indices_out) g.indices_out[b] = (int32_t)idx;
+    if (g.probs) g.probs[b] = (float)v.tree[((int64_t)1 << v.depth) - 1 + idx];
+  }
+}
+
+__device__ __forceinline__ float4 u8x4_to_f32_255(uint32_t w) {
+  float4 o;  // tf.div(tf.cast(x, f32), 255.) -- correctly rounded division
+  o.x = __fdiv_rn((float)(w & 0xffu), 255.0f);
+  o.y = __fdiv_rn((float)((w >> 8) & 0xffu), 255.0f);
+  o.z = __fdiv_rn((float)((w >> 16) & 0xffu), 255.0f);
+  o.w = __fdiv_rn((float)(w >> 24), 255.0f);
+  return o;
+}
+
+// NCHW float32: grid.y = (b, which, k) frame; each thread converts kGatherR dwords
+// strided by the block (kGatherR independent loads in flight before the stores;
+// 2 blocks per 84x84 frame -> 512 blocks at B = 32, measured best in
+// tools/bench_gather.hip).
+constexpr int kGatherR = 4;
+
+__global__ __launch_bounds__(256) void k_gather_f32(ReplayView v, GatherOut g) {
+  const int S = v.S;
+  const int slot = blockIdx.y;
+  const int b = slot / (2 * S);
+  const int r = slot - b * 2 * S;
+  const int which = r / S;
+  const int k = r - which * S;
+  if (blockIdx.x == 0 && which == 0 && k == 0 && threadIdx.x < 64) write_scalars_wave(v, g, b);
+  float* dst_base = (float*)(which ? g.next_state : g.state);
+  if (!dst_base) return;
+  const int64_t f = pymod(stack_base(v, g, b, which) - S + 1 + k, v.C);
+  const int64_t nd = v.obs_bytes >> 2;  // obs_bytes % 4 == 0 checked on host
+  const uint32_t* src = (const uint32_t*)(v.frames + f * v.obs_bytes);
+  float4* dst = (float4*)(dst_base + ((int64_t)b * S + k) * v.obs_bytes);
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x * kGatherR + threadIdx.x;
+  uint32_t w[kGatherR];
+#pragma unroll
+  for (int q = 0; q < kGatherR; ++q) {
+    const int64_t t = t0 + (int64_t)q * blockDim.x;
+    w[q] = t < nd ? src[t] : 0u;
+  }
+#pragma unroll
+  for (int q = 0; q < kGatherR; ++q) {
+    const int64_t t = t0 + (int64_t)q * blockDim.x;
+    if (t < nd) dst[t] = u8x4_to_f32_255(w[q]);
+  }
+}
+
+// NHWC float32 (the reference's state layout (B, H, W, stack), stack == 4): one
+// block column per (b, which) stack; each thread loads the same dword of the 4
+// frames (4 loads in flight) and writes 4 pixels x 4 channels = 64 contiguous bytes.
+__global__ __launch_bounds__(256) void k_gather_nhwc4(ReplayView v, GatherOut g) {
+  const int slot = blockIdx.y;
+  const int b = slot >> 1, which = slot & 1;
+  if (blockIdx.x == 0 && which == 0 && threadIdx.x < 64) write_scalars_wave(v, g, b);
+  float* dst_base = (float*)(which ? g.next_state : g.state);
+  if (!dst_base) return;
+  const int64_t base = stack_base(v, g, b, which);
+  const int64_t nd = v.obs_bytes >> 2;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nd) return;
+  uint32_t w[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    w[k] = ((const uint32_t*)(v.frames + pymod(base - 3 + k, v.C) * v.obs_bytes))[t];
+  float4 c[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) c[k] = u8x4_to_f32_255(w[k]);
+  float4* dst = (float4*)(dst_base + (int64_t)b * 4 * v.obs_bytes) + 4 * t;
+  dst[0] = make_float4(c[0].x, c[1].x, c[2].x, c[3].x);
+  dst[1] = make_float4(c[0].y, c[1].y, c[2].y, c[3].y);
+  dst[2] = make_float4(c[0].z, c[1].z, c[2].z, c[3].z);
+  dst[3] = make_float4(c[0].w, c[1].w, c[2].w, c[3].w);
+}
+
 __device__ __forceinline__ int64_t frame_of(const ReplayView& v, const GatherOut& g, int slot,
                                             int* b_out, int* which_out, int* k_out) {
   const int S = v.S;
@@ -306,53 +449,10 @@ __device__ __forceinline__ int64_t frame_of(const ReplayView& v, const GatherOut
   const int r = slot - b * 2 * S;
   const int which = r / S;
   const int k = r - which * S;
-  int64_t base = pymod((int64_t)g.indices[b], v.C);
-  if (which) {
-    bool term;
-    base = pymod(base + traj_len(v, base, &term), v.C);
-  }
   *b_out = b;
   *which_out = which;
   *k_out = k;
-  return pymod(base - S + 1 + k, v.C);
-}
-
-__device__ void write_scalars(const ReplayView& v, const GatherOut& g, int b) {
-  const int64_t idx = pymod((int64_t)g.indices[b], v.C);
-  bool term;
-  const int L = traj_len(v, idx, &term);
-  float acc = 0.0f;  // float32 products summed left to right (crb:540-541)
-  for (int k = 0; k < L; ++k)
-    acc = __fadd_rn(acc, __fmul_rn(v.discount[k], v.rewards[pymod(idx + k, v.C)]));
-  const int64_t nxt = pymod(idx + L, v.C);
-  if (g.action) g.action[b] = v.actions[idx];
-  if (g.reward) g.reward[b] = acc;
-  if (g.next_action) g.next_action[b] = v.actions[nxt];
-  if (g.next_reward) g.next_reward[b] = v.rewards[nxt];
-  if (g.terminal) g.terminal[b] = term ? 1 : 0;
-  if (g.indices_out) g.indices_out[b] = (int32_t)idx;
-  if (g.probs) g.probs[b] = (float)v.tree[((int64_t)1 << v.depth) - 1 + idx];
-}
-
-// uint8 frames -> float32 / 255 (one dword in, one float4 out per thread).
-__global__ __launch_bounds__(256) void k_gather_f32(ReplayView v, GatherOut g) {
-  int b, which, k;
-  const int slot = blockIdx.y;
-  const int64_t f = frame_of(v, g, slot, &b, &which, &k);
-  if (blockIdx.x == 0 && threadIdx.x == 0 && which == 0 && k == 0) write_scalars(v, g, b);
-  float* dst_base = (float*)(which ? g.next_state : g.state);
-  if (!dst_base) return;
-  const int64_t nd = v.obs_bytes >> 2;  // obs_bytes % 4 == 0 checked on host
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nd) return;
-  const uint32_t word = ((const uint32_t*)(v.frames + f * v.obs_bytes))[t];
-  float4 o;
-  o.x = __fdiv_rn((float)(word & 0xffu), 255.0f);
-  o.y = __fdiv_rn((float)((word >> 8) & 0xffu), 255.0f);
-  o.z = __fdiv_rn((float)((word >> 16) & 0xffu), 255.0f);
-  o.w = __fdiv_rn((float)(word >> 24), 255.0f);
-  float4* dst = (float4*)(dst_base + ((int64_t)b * v.S + k) * v.obs_bytes);
-  dst[t] = o;
+  return pymod(stack_base(v, g, b, which) - S + 1 + k, v.C);
 }
 
 // raw byte copy of each stacked frame (reference dtype preserved).
@@ -360,7 +460,7 @@ __global__ __launch_bounds__(256) void k_gather_raw(ReplayView v, GatherOut g) {
   int b, which, k;
   const int slot = blockIdx.y;
   const int64_t f = frame_of(v, g, slot, &b, &which, &k);
-  if (blockIdx.x == 0 && threadIdx.x == 0 && which == 0 && k == 0) write_scalars(v, g, b);
+  if (blockIdx.x == 0 && threadIdx.x < 64 && which == 0 && k == 0) write_scalars_wave(v, g, b);
   uint8_t* dst_base = (uint8_t*)(which ? g.next_state : g.state);
   if (!dst_base) return;
   const uint8_t* src = v.frames + f * v.obs_bytes;
@@ -612,8 +712,15 @@ int dq_replay_gather(dq_replay* h, const int32_t* indices, int32_t batch, int32_
     DQ_CHECK_ARG(h->cfg.obs_is_u8, "F32_NORM layout needs uint8 observations");
     DQ_CHECK_ARG((h->cfg.obs_bytes & 3) == 0, "F32_NORM layout needs obs_bytes % 4 == 0");
     const int64_t nd = h->cfg.obs_bytes >> 2;
-    dim3 grid((unsigned)((nd + 255) / 256), (unsigned)slots);
+    dim3 grid((unsigned)((nd + 256 * kGatherR - 1) / (256 * kGatherR)), (unsigned)slots);
     hipLaunchKernelGGL(k_gather_f32, grid, dim3(256), 0, s, h->view(), g);
+  } else if (layout == DQ_LAYOUT_F32_NHWC) {
+    DQ_CHECK_ARG(h->cfg.obs_is_u8, "F32_NHWC layout needs uint8 observations");
+    DQ_CHECK_ARG(h->cfg.stack_size == 4, "F32_NHWC layout needs stack_size == 4");
+    DQ_CHECK_ARG((h->cfg.obs_bytes & 3) == 0, "F32_NHWC layout needs obs_bytes % 4 == 0");
+    const int64_t nd = h->cfg.obs_bytes >> 2;
+    dim3 grid((unsigned)((nd + 255) / 256), (unsigned)(2 * batch));
+    hipLaunchKernelGGL(k_gather_nhwc4, grid, dim3(256), 0, s, h->view(), g);
   } else if (layout == DQ_LAYOUT_RAW) {
     const int64_t units = (h->cfg.obs_bytes & 15) == 0 ? h->cfg.obs_bytes >> 4 : h->cfg.obs_bytes;
     const int64_t bx = std::min<int64_t>((units + 255) / 256, 64);

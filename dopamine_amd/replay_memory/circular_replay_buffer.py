@@ -390,14 +390,17 @@ class OutOfGraphReplayBuffer(object):
 
   def _alloc_batch(self, batch_size, layout):
     B, S, dev = batch_size, self._stack_size, self._device
-    if layout == _lib.LAYOUT_F32_NORM:
-      st = (B, S) + tuple(self._observation_shape)
-      sdt = torch.float32
-    else:
-      st = (B, S, self._obs_bytes)
-      sdt = torch.uint8
-    out = {'state': torch.empty(st, dtype=sdt, device=dev),
-           'next_state': torch.empty(st, dtype=sdt, device=dev),
+
+    def states():
+      if layout == _lib.LAYOUT_F32_NORM:
+        return torch.empty((B, S) + tuple(self._observation_shape), dtype=torch.float32, device=dev)
+      if layout == _lib.LAYOUT_F32_NHWC:   # (B, H, W, S) memory viewed as channels_last NCHW
+        nhwc = torch.empty((B,) + tuple(self._observation_shape) + (S,), dtype=torch.float32, device=dev)
+        return nhwc.permute(0, 3, 1, 2)
+      return torch.empty((B, S, self._obs_bytes), dtype=torch.uint8, device=dev)
+
+    out = {'state': states(),
+           'next_state': states(),
            'action': torch.empty((B,), dtype=torch.int32, device=dev),
            'reward': torch.empty((B,), dtype=torch.float32, device=dev),
            'next_action': torch.empty((B,), dtype=torch.int32, device=dev),
@@ -535,7 +538,12 @@ class WrappedReplayBuffer(object):
           terminal_dtype=terminal_dtype, extra_storage_types=extra_storage_types,
           action_shape=action_shape, action_dtype=action_dtype, reward_shape=reward_shape,
           reward_dtype=reward_dtype, device=device)
-    layout = (_lib.LAYOUT_F32_NORM if np.dtype(observation_dtype) == np.uint8 else _lib.LAYOUT_RAW)
+    if np.dtype(observation_dtype) != np.uint8:
+      layout = _lib.LAYOUT_RAW
+    elif stack_size == 4 and len(observation_shape) == 2:
+      layout = _lib.LAYOUT_F32_NHWC     # Atari: CNN-ready channels_last, no transposes
+    else:
+      layout = _lib.LAYOUT_F32_NORM
     self._layout = layout
     self.transition = collections.OrderedDict()
     self._out = None

@@ -43,7 +43,8 @@ extern "C" {
 
 /* gather output layouts */
 #define DQ_LAYOUT_RAW 0           /* (B, stack, obs_bytes) bytes, stack-major (moveaxis on host = reference NHWC) */
-#define DQ_LAYOUT_F32_NORM 1      /* (B, stack, H*W) float32 = uint8 / 255 (atari_lib.py:96-97), CNN-ready NCHW */
+#define DQ_LAYOUT_F32_NORM 1      /* (B, stack, H*W) float32 = uint8 / 255 (atari_lib.py:96-97), NCHW */
+#define DQ_LAYOUT_F32_NHWC 2      /* (B, H*W, stack) float32 = uint8 / 255, the reference NHWC state (stack == 4) */
 
 /* Device control block (caller allocates >= sizeof, 64-byte aligned). */
 typedef struct dq_replay_meta {

@@ -91,7 +91,7 @@ def test_hip_graph_replay_matches_eager(kind):
       a._run_train_op()
       idx.append(a._replay.transition['indices'].cpu().numpy().copy())
     a._replay.memory.sync_rng()
-    res.append((np.stack(idx), a.online_convnet.fp.flat.cpu().numpy(), float(a._loss_out['mean_loss'].item())))
+    res.append((np.stack(idx), a.online_convnet.fp.flat.cpu().numpy(), a.mean_loss()))
     assert (a._graph is not None) == graph
   np.testing.assert_array_equal(res[0][0], res[1][0])
   if kind != 'iqn':   # IQN taus come from torch's RNG, whose graph-safe offsets differ from eager

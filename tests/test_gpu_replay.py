@@ -155,6 +155,17 @@ def test_gather_f32_normalised_matches_raw_over_255():
   np.testing.assert_array_equal(st, exp)
   np.testing.assert_array_equal(dev['next_state'].cpu().numpy(),
                                 np.moveaxis(raw[3], -1, 1).astype(np.float32) / np.float32(255))
+  # NHWC layout (the reference's (B, 84, 84, 4) order, channels_last for the CNN)
+  from dopamine_amd import _lib
+  nh = m.sample_device(32, indices=idx, layout=_lib.LAYOUT_F32_NHWC)
+  assert nh['state'].is_contiguous(memory_format=torch.channels_last)
+  np.testing.assert_array_equal(nh['state'].permute(0, 2, 3, 1).cpu().numpy(),
+                                raw[0].astype(np.float32) / np.float32(255))
+  np.testing.assert_array_equal(nh['next_state'].permute(0, 2, 3, 1).cpu().numpy(),
+                                raw[3].astype(np.float32) / np.float32(255))
+  for k in ('action', 'reward', 'next_action', 'next_reward', 'terminal', 'indices',
+            'sampling_probabilities'):
+    np.testing.assert_array_equal(nh[k].cpu().numpy(), dev[k].cpu().numpy())
   # the oracle on the same store + indices
   o = orc.PrioritizedOracle((84, 84), 4, C, 32, update_horizon=3)
   o.observation = obs.reshape(C, 84, 84); o.action = act; o.reward = rew; o.terminal = term
