@@ -57,6 +57,7 @@ SIGNATURES = {
     'dq_replay_set_meta': [_P, _I64, _D, _P],
     'dq_replay_set_tape': [_P, _I64, _P],
     'dq_replay_read_meta': [_P, ctypes.POINTER(Meta), _P],
+    'dq_replay_rewind_last_sample': [_P, _P],
     'dq_c51_loss': [_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _F, _P, _P, _P, _P, _P],
     'dq_dqn_huber_loss': [_P, _P, _P, _P, _P, _I32, _I32, _F, _P, _P, _P, _P],
     'dq_iqn_loss': [_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _F, _F, _P, _P, _P, _P],

@@ -81,6 +81,7 @@ class DQNAgent(object):
                replay_capacity=1000000,
                batch_size=32,
                use_hip_graph=True,
+               pipeline=True,
                device=None,
                seed=0,
                process_group=None):
@@ -113,9 +114,15 @@ class DQNAgent(object):
     self._seed = seed
     self._pg = process_group
     self.use_hip_graph = use_hip_graph
-    self._graph = None
+    self.pipeline = pipeline
+    self._graphs = None
     self._graph_opt = None
     self._eager_steps = 0
+    self._slot = 0
+    self._pbuf = [None, None]
+    self._ptgt = [None, None]
+    self._has_prefetch = False
+    self._prefetch_add_count = -1
     self._sess = sess
 
     state_shape = (1,) + self.observation_shape + (stack_size,)
@@ -125,6 +132,7 @@ class DQNAgent(object):
       self._build_networks()
       self._build_train_op()
       self._opt = self.optimizer.build(self.online_convnet.fp.flat)
+      self._side = torch.cuda.Stream(self._device)
     self._observation = None
     self._last_observation = None
     self.last_loss = None
@@ -157,22 +165,58 @@ class DQNAgent(object):
       return x
     return x.reshape(x.shape[0], -1)
 
-  def _forward_backward(self, t):
-    """Loss + backward into the flat gradient (dqn_agent.py:283-322)."""
+  # The gradient step is split so it can be pipelined:
+  #   _target_forward(t)      target-network outputs the loss needs (no grad)
+  #   _online_loss(t, tgt)    online forward + the loss kernel -> (output, d loss/d output)
+  #   _backward(y, g)         backward into the flat gradient
+  def _target_forward(self, t):
     with torch.no_grad():
-      tq = self.target_convnet(self._state_input(t['next_state']))
-    q = self.online_convnet(self._state_input(t['state']))
-    out = ops.dqn_huber_loss(q.detach(), tq, t['action'], t['reward'], t['terminal'],
-                             self.cumulative_gamma, out=self._loss_out)
-    self.online_convnet.fp.grad.zero_()
-    q.backward(out['grad'])
+      return {'q': self.target_convnet(self._state_input(t['next_state']))}
 
-  def _device_grad_step(self, reserve):
-    t = self._replay.memory.sample_device(self._batch_size, layout=self._replay._layout,
-                                          out=self._replay._out, reserve=reserve)
-    self._replay._out = t
-    self._replay.unpack_transition(t)
-    self._forward_backward(t)
+  def _online_loss(self, t, tgt):
+    """dqn_agent.py:283-322."""
+    q = self.online_convnet(self._state_input(t['state']))
+    out = ops.dqn_huber_loss(q.detach(), tgt['q'], t['action'], t['reward'], t['terminal'],
+                             self.cumulative_gamma, out=self._loss_out)
+    return q, out['grad']
+
+  def _backward(self, y, g):
+    self.online_convnet.fp.grad.zero_()
+    y.backward(g)
+
+  # Pipelined step.  Slot c holds step t's batch and its target-net outputs.
+  # After step t's loss kernel (and priority write-back) a second HIP stream
+  # samples + gathers step t+1's batch into slot 1-c and runs the target net on
+  # it, concurrently with step t's backward and optimizer on the main stream.
+  # Step t+1's sample still follows step t's set_priority, so draws and indices
+  # are exactly the reference's; a prefetch made stale by add() or host RNG use
+  # is rewound (dq_replay_rewind_last_sample) and redrawn.
+  def _prefetch(self, i):
+    mem = self._replay.memory
+    t = mem.sample_device(self._batch_size, layout=self._replay._layout, out=self._pbuf[i],
+                          reserve=False)
+    self._pbuf[i] = t
+    tg = self._target_forward(t)
+    if self._ptgt[i] is None:
+      self._ptgt[i] = {k: torch.empty_like(v) for k, v in tg.items()}
+    for k, v in tg.items():
+      self._ptgt[i][k].copy_(v)
+
+  def _grad_step(self, c):
+    if not self.pipeline:
+      self._prefetch(c)
+    y, g = self._online_loss(self._pbuf[c], self._ptgt[c])
+    if self.pipeline:
+      main = torch.cuda.current_stream(self._device)
+      ev = torch.cuda.Event()
+      ev.record(main)
+      self._side.wait_event(ev)
+      with torch.cuda.stream(self._side):
+        self._prefetch(1 - c)
+      self._backward(y, g)
+      main.wait_stream(self._side)
+    else:
+      self._backward(y, g)
 
   def _device_opt_step(self):
     self._opt.step(self.online_convnet.fp.grad)
@@ -182,35 +226,65 @@ class DQNAgent(object):
       return
     parallel.allreduce_mean_(self.online_convnet.fp.grad, self._pg)
 
+  def _discard_prefetch(self):
+    if self._has_prefetch:
+      self._replay.memory.rewind_last_sample()
+      self._has_prefetch = False
+
   def _run_train_op(self):
     """One gradient step (the body of sess.run(self._train_op))."""
     mem = self._replay.memory
+    c = self._slot
+    if self.pipeline:
+      if self._has_prefetch and self._prefetch_add_count != int(mem.add_count):
+        self._discard_prefetch()          # transitions were added after the prefetch
+      if not self._has_prefetch:
+        mem.reserve_rng(self._batch_size)
+        self._prefetch(c)
     mem.reserve_rng(self._batch_size)
-    if self._graph is not None:
-      self._graph.replay()
+    if self._graphs is not None:
+      self._graphs[c].replay()
       self._allreduce_grads()
       self._graph_opt.replay()
-      return
-    self._device_grad_step(reserve=False)
-    self._allreduce_grads()
-    self._device_opt_step()
-    self._eager_steps += 1
-    if self.use_hip_graph and self._eager_steps >= 3:
+    else:
+      self._grad_step(c)
+      self._allreduce_grads()
+      self._device_opt_step()
+      self._eager_steps += 1
+    self._replay._out = self._pbuf[c]
+    self._replay.unpack_transition(self._pbuf[c])
+    if self.pipeline:
+      self._slot = 1 - c
+      self._has_prefetch = True
+      self._prefetch_add_count = int(mem.add_count)
+    if self._graphs is None and self.use_hip_graph and self._eager_steps >= 3:
       self._capture()
 
   def _capture(self):
     torch.cuda.synchronize(self._device)
-    g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-    # One more eager step has to be paid for by the tape (capture does not consume).
-    with torch.cuda.graph(g1):
-      self._device_grad_step(reserve=False)
-    with torch.cuda.graph(g2, pool=g1.pool()):
+    g0 = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g0):
+      self._grad_step(0)
+    graphs = [g0]
+    if self.pipeline:
+      g1 = torch.cuda.CUDAGraph()
+      with torch.cuda.graph(g1, pool=g0.pool()):
+        self._grad_step(1)
+      graphs.append(g1)
+    else:
+      graphs.append(g0)
+    gopt = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gopt, pool=g0.pool()):
       self._device_opt_step()
-    # capture recorded but did not execute: the tape position is unchanged
-    self._graph, self._graph_opt = g1, g2
+    # capture records without executing: tape cursor and buffers are unchanged
+    self._graphs, self._graph_opt = graphs, gopt
 
   def _sync_target(self):
     ops.sync_copy(self.target_convnet.fp.flat, self.online_convnet.fp.flat)
+    if self.pipeline and self._has_prefetch:   # the prefetched target outputs are stale
+      tg = self._target_forward(self._pbuf[self._slot])
+      for k, v in tg.items():
+        self._ptgt[self._slot][k].copy_(v)
 
   # ------------------------------------------------------------- agent API
   def begin_episode(self, observation):
@@ -248,6 +322,7 @@ class DQNAgent(object):
   def _select_action(self):
     """dqn_agent.py:394-416.  The replay's RNG tape is brought in step first so
     Python's `random` stream is consumed exactly as by the reference."""
+    self._discard_prefetch()      # its draws would precede ours: give them back first
     self._replay.memory.sync_rng()
     if self.eval_mode:
       epsilon = self.epsilon_eval

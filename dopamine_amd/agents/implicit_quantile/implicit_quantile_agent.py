@@ -55,13 +55,21 @@ class ImplicitQuantileAgent(rainbow_agent.RainbowAgent):
     qv, _ = self.online_convnet(x, self.num_quantile_samples)
     return qv.view(self.num_quantile_samples, x.shape[0], -1).mean(0)
 
-  def _forward_backward(self, t):
+  def _target_forward(self, t):
     with torch.no_grad():
       tq, _ = self.target_convnet(t['next_state'], self.num_tau_prime_samples)
-      action_net = self.online_convnet if self.double_dqn else self.target_convnet
-      ta, _ = action_net(t['next_state'], self.num_quantile_samples)
+      out = {'tq': tq}
+      if not self.double_dqn:   # double DQN's argmax net is the online net of THIS step
+        out['ta'], _ = self.target_convnet(t['next_state'], self.num_quantile_samples)
+      return out
+
+  def _online_loss(self, t, tgt):
+    """implicit_quantile_agent.py:190-321."""
+    ta = tgt.get('ta')
+    if ta is None:
+      with torch.no_grad():
+        ta, _ = self.online_convnet(t['next_state'], self.num_quantile_samples)
     qv, taus = self.online_convnet(t['state'], self.num_tau_samples)
-    out = ops.iqn_loss(qv.detach(), tq, ta, taus, t['action'], t['reward'], t['terminal'],
+    out = ops.iqn_loss(qv.detach(), tgt['tq'], ta, taus, t['action'], t['reward'], t['terminal'],
                        self.cumulative_gamma, self.kappa, out=self._loss_out)
-    self.online_convnet.fp.grad.zero_()
-    qv.backward(out['grad'])
+    return qv, out['grad']

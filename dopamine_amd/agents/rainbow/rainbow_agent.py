@@ -113,20 +113,22 @@ class RainbowAgent(dqn_agent.DQNAgent):
     logits = self.online_convnet(x)
     return (torch.softmax(logits, -1) * self._support).sum(-1)
 
-  def _forward_backward(self, t):
+  def _target_forward(self, t):
     with torch.no_grad():
-      target_logits = self.target_convnet(t['next_state'])
+      return {'logits': self.target_convnet(t['next_state'])}
+
+  def _online_loss(self, t, tgt):
+    """rainbow_agent.py:200-305."""
     logits = self.online_convnet(t['state'])
     prioritized = self._replay_scheme == 'prioritized'
-    out = ops.c51_loss(logits.detach(), target_logits, t['action'], t['reward'], t['terminal'],
+    out = ops.c51_loss(logits.detach(), tgt['logits'], t['action'], t['reward'], t['terminal'],
                        self._support, self.cumulative_gamma,
                        probs=t['sampling_probabilities'] if prioritized else None,
                        out=self._loss_out)
     if prioritized:
       # sqrt(loss + 1e-10) of the UNWEIGHTED loss, before the optimizer (rb:289-297)
       self._replay.tf_set_priority(t['indices'], out['priorities'])
-    self.online_convnet.fp.grad.zero_()
-    logits.backward(out['grad'])
+    return logits, out['grad']
 
   def _store_transition(self, last_observation, action, reward, is_terminal, priority=None):
     """rainbow_agent.py:307-337."""

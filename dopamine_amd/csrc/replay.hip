@@ -134,6 +134,7 @@ __global__ __launch_bounds__(64) void k_per_sample(ReplayView v, int B, int32_t*
   dq_replay_meta* meta = v.meta;
   const int64_t add_count = meta->add_count;
   int64_t pos = meta->tape_pos;
+  const int64_t pos0 = pos;
   const int64_t len = meta->tape_len;
   const double total = v.tree[0];
   bool fail = meta->status != 0;
@@ -146,6 +147,7 @@ __global__ __launch_bounds__(64) void k_per_sample(ReplayView v, int B, int32_t*
     fail = true;
   }
   if (fail) {
+    if (lane == 0) meta->reserved[0] = pos0;
     for (int i = lane; i < B; i += kWave) out[i] = 0;
     return;
   }
@@ -189,6 +191,7 @@ __global__ __launch_bounds__(64) void k_per_sample(ReplayView v, int B, int32_t*
         break;
       }
     }
+    meta->reserved[0] = pos0;   // entry cursor, for dq_replay_rewind_last_sample
     meta->tape_pos = pos;
   }
   __syncthreads();
@@ -204,7 +207,10 @@ __global__ __launch_bounds__(64) void k_per_sample(ReplayView v, int B, int32_t*
 __global__ __launch_bounds__(64) void k_uniform_sample(ReplayView v, int B, int32_t* out) {
   const int lane = threadIdx.x;
   dq_replay_meta* meta = v.meta;
+  int64_t pos = meta->tape_pos;
+  const int64_t pos0 = pos;
   if (meta->status != 0) {
+    if (lane == 0) meta->reserved[0] = pos0;
     for (int i = lane; i < B; i += kWave) out[i] = 0;
     return;
   }
@@ -218,7 +224,10 @@ __global__ __launch_bounds__(64) void k_uniform_sample(ReplayView v, int B, int3
     min_id = v.S - 1;
     max_id = cursor - v.n;
     if (max_id <= min_id) {
-      if (lane == 0) latch(meta, DQ_ST_TOO_FEW, 0, 0.0);
+      if (lane == 0) {
+        latch(meta, DQ_ST_TOO_FEW, 0, 0.0);
+        meta->reserved[0] = pos0;
+      }
       for (int i = lane; i < B; i += kWave) out[i] = 0;
       return;
     }
@@ -227,7 +236,6 @@ __global__ __launch_bounds__(64) void k_uniform_sample(ReplayView v, int B, int3
   uint64_t mask = rng;
   mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4;
   mask |= mask >> 8; mask |= mask >> 16; mask |= mask >> 32;
-  int64_t pos = meta->tape_pos;
   const int64_t len = meta->tape_len;
   int count = 0, fails = 0;
   bool tape_dry = false;
@@ -276,9 +284,14 @@ __global__ __launch_bounds__(64) void k_uniform_sample(ReplayView v, int B, int3
   if (lane == 0) {
     if (tape_dry) latch(meta, DQ_ST_TAPE_EXHAUSTED, count, 0.0);
     else if (count != B) latch(meta, DQ_ST_MAX_ATTEMPTS, count, 0.0);
+    meta->reserved[0] = pos0;   // entry cursor, for dq_replay_rewind_last_sample
     meta->tape_pos = pos;
   }
 }
+
+// Undo the tape consumption of the most recent sample (its indices are discarded):
+// lets a speculatively prefetched batch be re-drawn after adds / host RNG use.
+__global__ void k_rewind(dq_replay_meta* m) { m->tape_pos = m->reserved[0]; }
 
 // ---------------------------------------------------------------------------
 // Frame-stack gather.  grid.y = (sample b, state|next_state, stack slot k);
@@ -777,6 +790,13 @@ int dq_replay_set_tape(dq_replay* h, int64_t len, void* stream) {
   DQ_CHECK_ARG(h && len >= 0 && len <= h->st.tape_capacity, "tape length out of range");
   hipLaunchKernelGGL(k_set_tape, dim3(1), dim3(1), 0, (hipStream_t)stream, h->st.meta, len);
   DQ_CHECK_LAUNCH("k_set_tape");
+  return DQ_OK;
+}
+
+int dq_replay_rewind_last_sample(dq_replay* h, void* stream) {
+  DQ_CHECK_ARG(h, "null handle");
+  hipLaunchKernelGGL(k_rewind, dim3(1), dim3(1), 0, (hipStream_t)stream, h->st.meta);
+  DQ_CHECK_LAUNCH("k_rewind");
   return DQ_OK;
 }
 

@@ -455,6 +455,11 @@ class OutOfGraphReplayBuffer(object):
       indices = out['sample_indices']
     return self._gather(indices, B, layout, out)
 
+  def rewind_last_sample(self):
+    """Give back the RNG-tape words of the most recent device sample (whose
+    indices are then discarded), e.g. a prefetched batch invalidated by add()."""
+    _lib.call('dq_replay_rewind_last_sample', self._h, self._stream)
+
   def sync_rng(self, raise_errors=True):
     """Bring the host RNG stream in step with the device; raise latched errors."""
     meta = self._read_meta()

@@ -130,6 +130,11 @@ int dq_sumtree_rebuild(dq_replay* h, void* stream);
 int dq_replay_set_meta(dq_replay* h, int64_t add_count, double max_recorded_priority, void* stream);
 /* Declare `len` fresh words on the tape (caller has copied them in); pos := 0. */
 int dq_replay_set_tape(dq_replay* h, int64_t len, void* stream);
+/* Undo the RNG-tape consumption of the most recent dq_replay_sample_indices call
+ * (its indices must then be discarded).  Lets a speculatively prefetched batch be
+ * redrawn when transitions were added or the host stream was used in between, so
+ * the draw order stays the reference's. */
+int dq_replay_rewind_last_sample(dq_replay* h, void* stream);
 /* synchronous: copies the control block to host memory. */
 int dq_replay_read_meta(dq_replay* h, dq_replay_meta* out, void* stream);
 

@@ -92,7 +92,30 @@ def test_hip_graph_replay_matches_eager(kind):
       idx.append(a._replay.transition['indices'].cpu().numpy().copy())
     a._replay.memory.sync_rng()
     res.append((np.stack(idx), a.online_convnet.fp.flat.cpu().numpy(), a.mean_loss()))
-    assert (a._graph is not None) == graph
+    assert (a._graphs is not None) == graph
   np.testing.assert_array_equal(res[0][0], res[1][0])
   if kind != 'iqn':   # IQN taus come from torch's RNG, whose graph-safe offsets differ from eager
     np.testing.assert_allclose(res[0][1], res[1][1], rtol=1e-4, atol=1e-6)
+
+
+def test_pipelined_prefetch_is_invalidated_by_adds_and_host_draws():
+  """The two-stream prefetch of step t+1's batch must not change what is drawn:
+  add() and the agent's own random draws between steps rewind and redraw it."""
+  res = []
+  for pipe in (False, True):
+    random.seed(3); np.random.seed(3); torch.manual_seed(3)
+    a = _rainbow(use_hip_graph=False, pipeline=pipe)
+    seq = []
+    for step in range(8):
+      a._run_train_op()
+      seq.append(a._replay.transition['indices'].cpu().numpy().copy())
+      if step % 2 == 0:
+        a._store_transition(np.full((84, 84), step, np.uint8), 1, 0.5, False)
+      if step % 3 == 1:
+        a._select_action()            # epsilon = 1 here: draws from Python's random
+    a._discard_prefetch()
+    a._replay.memory.sync_rng()
+    res.append((np.stack(seq), random.getstate(), a.online_convnet.fp.flat.cpu().numpy()))
+  np.testing.assert_array_equal(res[0][0], res[1][0])
+  assert res[0][1] == res[1][1]
+  np.testing.assert_allclose(res[0][2], res[1][2], rtol=1e-5, atol=1e-7)
