@@ -66,13 +66,14 @@ def time_gather(agent, iters):
   out = agent._replay._out
   idx = out['sample_indices']
   B = agent._batch_size
+  layout = agent._replay._layout
   stream = torch.cuda.current_stream()
   for _ in range(10):
-    mem._gather(idx, B, _lib.LAYOUT_F32_NORM, out)
+    mem._gather(idx, B, layout, out)
   g = torch.cuda.CUDAGraph()
   with torch.cuda.graph(g):
     for _ in range(iters):
-      mem._gather(idx, B, _lib.LAYOUT_F32_NORM, out)
+      mem._gather(idx, B, layout, out)
   g.replay()
   torch.cuda.synchronize()
   e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -84,13 +85,14 @@ def time_gather(agent, iters):
   # eager back-to-back launches on the same stream, for comparison
   e0.record(stream)
   for _ in range(iters):
-    mem._gather(idx, B, _lib.LAYOUT_F32_NORM, out)
+    mem._gather(idx, B, layout, out)
   e1.record(stream)
   e1.synchronize()
   eager_us = e0.elapsed_time(e1) * 1e3 / iters
   S, obs = mem._stack_size, mem._obs_bytes
   algo_bytes = B * (2 * S * obs + 2 * S * obs * 4)   # u8 frames read + fp32 NCHW written
-  return graph_us, eager_us, algo_bytes
+  name = {_lib.LAYOUT_F32_NHWC: 'k_gather_nhwc4', _lib.LAYOUT_F32_NORM: 'k_gather_f32'}[layout]
+  return graph_us, eager_us, algo_bytes, name
 
 
 def cpu_baseline(seconds, A, batch):
@@ -157,7 +159,7 @@ def main():
   loss = agent.mean_loss()
   assert np.isfinite(loss), 'non-finite loss'
 
-  graph_us, eager_us, algo_bytes = time_gather(agent, args.gather_iters)
+  graph_us, eager_us, algo_bytes, gname = time_gather(agent, args.gather_iters)
   achieved = algo_bytes / (graph_us * 1e-6) / 1e9
 
   cpu = None
@@ -177,7 +179,7 @@ def main():
                    'global_batch': args.batch * world, 'per_gpu_batch': args.batch,
                    'replay_capacity': args.capacity, 'parallelism': 'dp%d' % world,
                    'hip_graph': not args.no_graph},
-        'roofline': {'kernel': 'k_gather_f32 (frame-stack gather + /255, state+next_state)',
+        'roofline': {'kernel': gname + ' (frame-stack gather + /255, state+next_state)',
                      'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
                      'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4),
                      'traffic': None, 'algo_bytes_per_launch': algo_bytes,

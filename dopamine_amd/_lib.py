@@ -35,6 +35,16 @@ class Storage(ctypes.Structure):
               ('tape_capacity', ctypes.c_int64), ('discount', ctypes.c_void_p)]
 
 
+MAX_TENSORS = 16
+
+
+class TensorList(ctypes.Structure):
+  _fields_ = [('count', ctypes.c_int32), ('pad_', ctypes.c_int32),
+              ('var', ctypes.c_void_p * MAX_TENSORS), ('grad', ctypes.c_void_p * MAX_TENSORS),
+              ('m', ctypes.c_void_p * MAX_TENSORS), ('v', ctypes.c_void_p * MAX_TENSORS),
+              ('n', ctypes.c_int64 * MAX_TENSORS)]
+
+
 _P = ctypes.c_void_p
 _I32 = ctypes.c_int32
 _I64 = ctypes.c_int64
@@ -61,7 +71,8 @@ SIGNATURES = {
     'dq_c51_loss': [_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _F, _P, _P, _P, _P, _P],
     'dq_dqn_huber_loss': [_P, _P, _P, _P, _P, _I32, _I32, _F, _P, _P, _P, _P],
     'dq_iqn_loss': [_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _F, _F, _P, _P, _P, _P],
-    'dq_adam_tf1': [_P, _P, _P, _P, _P, _I64, _F, _F, _F, _F, _P],
+    'dq_adam_tf1': [_P, _P, _P, _P, _P, _I32, _I64, _F, _F, _F, _F, _P],
+    'dq_adam_tf1_multi': [ctypes.POINTER(TensorList), _P, _I32, _F, _F, _F, _F, _P],
     'dq_rmsprop_tf1': [_P, _P, _P, _P, _P, _I64, _F, _F, _F, _F, _I32, _P],
     'dq_sync_copy': [_P, _P, _I64, _P],
 }

@@ -116,8 +116,9 @@ class DQNAgent(object):
     self.use_hip_graph = use_hip_graph
     self.pipeline = pipeline
     self._graphs = None
-    self._graph_opt = None
+    self._graphs_opt = None
     self._eager_steps = 0
+    self._opt_steps = 0
     self._slot = 0
     self._pbuf = [None, None]
     self._ptgt = [None, None]
@@ -131,7 +132,8 @@ class DQNAgent(object):
       self._replay = self._build_replay_buffer(use_staging)
       self._build_networks()
       self._build_train_op()
-      self._opt = self.optimizer.build(self.online_convnet.fp.flat)
+      self._opt = self.optimizer.build(self.online_convnet.fp.flat,
+                                       segments=self.online_convnet.fp.segments())
       self._side = torch.cuda.Stream(self._device)
     self._observation = None
     self._last_observation = None
@@ -181,8 +183,16 @@ class DQNAgent(object):
     return q, out['grad']
 
   def _backward(self, y, g):
-    self.online_convnet.fp.grad.zero_()
+    # Fresh per-parameter gradients (no flat-buffer zeroing + accumulate kernels);
+    # the multi-tensor TF1 Adam reads them in place.
+    for prm in self.online_convnet.parameters():
+      prm.grad = None
     y.backward(g)
+    if self._needs_flat_grad():
+      self.online_convnet.fp.gather_grads()
+
+  def _needs_flat_grad(self):
+    return self._pg is not None or not getattr(self._opt, 'supports_multi', False)
 
   # Pipelined step.  Slot c holds step t's batch and its target-net outputs.
   # After step t's loss kernel (and priority write-back) a second HIP stream
@@ -218,8 +228,12 @@ class DQNAgent(object):
     else:
       self._backward(y, g)
 
-  def _device_opt_step(self):
-    self._opt.step(self.online_convnet.fp.grad)
+  def _device_opt_step(self, k):
+    """Optimizer step k (k = gradient-step parity: TF1 Adam's beta-power slot)."""
+    if self._needs_flat_grad():
+      self._opt.step(self.online_convnet.fp.grad, slot=k)
+    else:
+      self._opt.step_multi([prm.grad for prm in self.online_convnet.parameters()], slot=k)
 
   def _allreduce_grads(self):
     if self._pg is None:
@@ -234,7 +248,7 @@ class DQNAgent(object):
   def _run_train_op(self):
     """One gradient step (the body of sess.run(self._train_op))."""
     mem = self._replay.memory
-    c = self._slot
+    c, k = self._slot, self._opt_steps % 2
     if self.pipeline:
       if self._has_prefetch and self._prefetch_add_count != int(mem.add_count):
         self._discard_prefetch()          # transitions were added after the prefetch
@@ -243,14 +257,16 @@ class DQNAgent(object):
         self._prefetch(c)
     mem.reserve_rng(self._batch_size)
     if self._graphs is not None:
-      self._graphs[c].replay()
-      self._allreduce_grads()
-      self._graph_opt.replay()
+      self._graphs[k].replay()
+      if self._pg is not None:
+        self._allreduce_grads()
+        self._graphs_opt[k].replay()
     else:
       self._grad_step(c)
       self._allreduce_grads()
-      self._device_opt_step()
+      self._device_opt_step(k)
       self._eager_steps += 1
+    self._opt_steps += 1
     self._replay._out = self._pbuf[c]
     self._replay.unpack_transition(self._pbuf[c])
     if self.pipeline:
@@ -261,23 +277,27 @@ class DQNAgent(object):
       self._capture()
 
   def _capture(self):
+    """Two graphs, one per gradient-step parity k (pipeline slot and Adam
+    beta-power slot both alternate with k); with one GPU the optimizer is in the
+    same graph, with N GPUs it is a second graph after the RCCL all-reduce."""
     torch.cuda.synchronize(self._device)
-    g0 = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g0):
-      self._grad_step(0)
-    graphs = [g0]
-    if self.pipeline:
-      g1 = torch.cuda.CUDAGraph()
-      with torch.cuda.graph(g1, pool=g0.pool()):
-        self._grad_step(1)
-      graphs.append(g1)
-    else:
-      graphs.append(g0)
-    gopt = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(gopt, pool=g0.pool()):
-      self._device_opt_step()
+    graphs, graphs_opt, pool = [], [], None
+    for k in (0, 1):
+      c = k if self.pipeline else 0
+      g = torch.cuda.CUDAGraph()
+      with torch.cuda.graph(g, pool=pool):
+        self._grad_step(c)
+        if self._pg is None:
+          self._device_opt_step(k)
+      pool = g.pool()
+      graphs.append(g)
+      if self._pg is not None:
+        go = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(go, pool=pool):
+          self._device_opt_step(k)
+        graphs_opt.append(go)
     # capture records without executing: tape cursor and buffers are unchanged
-    self._graphs, self._graph_opt = graphs, gopt
+    self._graphs, self._graphs_opt = graphs, graphs_opt
 
   def _sync_target(self):
     ops.sync_copy(self.target_convnet.fp.flat, self.online_convnet.fp.flat)

@@ -39,6 +39,22 @@ class FlatParams(object):
       p.grad = self._view(self.grad, o, shape)
       self.params[name] = p
 
+    self.grad_views = [self._view(self.grad, o, s) for o, s in self.offsets.values()]
+
+  def segments(self):
+    """(offset, numel) of every parameter inside the flat buffer, in order."""
+    return [(o, int(np.prod(s))) for o, s in self.offsets.values()]
+
+  def gather_grads(self):
+    """Copy autograd's per-parameter gradients into the flat gradient buffer
+    (one multi-tensor copy kernel); returns the flat buffer."""
+    ps = list(self.params.values())
+    if all(p.grad is not None and p.grad.data_ptr() == v.data_ptr()
+           for p, v in zip(ps, self.grad_views)):
+      return self.grad
+    torch._foreach_copy_(self.grad_views, [p.grad for p in ps])
+    return self.grad
+
   @staticmethod
   def _view(buf, o, shape):
     n = int(np.prod(shape))

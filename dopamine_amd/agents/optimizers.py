@@ -9,8 +9,8 @@ class AdamOptimizer(object):
   def __init__(self, learning_rate=0.001, beta1=0.9, beta2=0.999, epsilon=1e-08, **unused):
     self.kwargs = dict(learning_rate=learning_rate, beta1=beta1, beta2=beta2, epsilon=epsilon)
 
-  def build(self, flat_params):
-    return ops.TF1Adam(flat_params, **self.kwargs)
+  def build(self, flat_params, segments=None):
+    return ops.TF1Adam(flat_params, segments=segments, **self.kwargs)
 
   def __repr__(self):
     return 'AdamOptimizer(%r)' % self.kwargs
@@ -21,7 +21,7 @@ class RMSPropOptimizer(object):
     self.kwargs = dict(learning_rate=learning_rate, decay=decay, momentum=momentum,
                        epsilon=epsilon, centered=centered)
 
-  def build(self, flat_params):
+  def build(self, flat_params, segments=None):
     return ops.TF1RMSProp(flat_params, **self.kwargs)
 
   def __repr__(self):

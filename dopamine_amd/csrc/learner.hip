@@ -242,15 +242,23 @@ __global__ __launch_bounds__(64) void k_mean(const float* x, int n, float* out) 
 }
 
 // ---------------------------------------------------------------------------
-// TF1 Adam over a flat buffer.  k_adam_prep computes this step's
-// alpha = lr sqrt(1 - b2^t) / (1 - b1^t) from the float32 beta powers and
-// advances them; k_adam applies m/v/var updates (float4 vectorised).
+// TF1 Adam (ApplyAdam): alpha = lr sqrt(1 - b2^t) / (1 - b1^t) from the float32
+// beta powers, then m/v/var updates (float4 vectorised).
 // ---------------------------------------------------------------------------
-__global__ void k_adam_prep(float* state, float lr, float b1, float b2) {
-  const float b1p = state[0], b2p = state[1];
-  state[2] = __fdiv_rn(__fmul_rn(lr, __fsqrt_rn(__fsub_rn(1.0f, b2p))), __fsub_rn(1.0f, b1p));
-  state[0] = __fmul_rn(b1p, b1);
-  state[1] = __fmul_rn(b2p, b2);
+// The float32 beta powers are double-buffered: state = {b1p, b2p}[2]; a launch
+// reads slot `slot` (this step's beta^t) and block 0 writes slot^1 = beta^(t+1)
+// (TF's beta_power *= beta after the apply, adam.py _finish), so no separate
+// "prepare" launch and no intra-launch race.
+__device__ __forceinline__ float adam_alpha(const float* state, int slot, float lr, float b1,
+                                            float b2) {
+  const float b1p = state[2 * slot], b2p = state[2 * slot + 1];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    float* nxt = const_cast<float*>(state) + 2 * (slot ^ 1);
+    nxt[0] = __fmul_rn(b1p, b1);
+    nxt[1] = __fmul_rn(b2p, b2);
+  }
+  // alpha = lr * sqrt(1 - beta2^t) / (1 - beta1^t)  (TF1 ApplyAdam)
+  return __fdiv_rn(__fmul_rn(lr, __fsqrt_rn(__fsub_rn(1.0f, b2p))), __fsub_rn(1.0f, b1p));
 }
 
 __device__ __forceinline__ void adam1(float& var, float g, float& m, float& v, float alpha,
@@ -260,15 +268,12 @@ __device__ __forceinline__ void adam1(float& var, float g, float& m, float& v, f
   var = __fsub_rn(var, __fdiv_rn(__fmul_rn(m, alpha), __fadd_rn(__fsqrt_rn(v), eps)));
 }
 
-__global__ __launch_bounds__(256) void k_adam(float* __restrict__ var, const float* __restrict__ grad,
-                                              float* __restrict__ m, float* __restrict__ v,
-                                              const float* __restrict__ state, int64_t n,
-                                              float b1, float b2, float eps) {
-  const float alpha = state[2];
-  const float omb1 = __fsub_rn(1.0f, b1), omb2 = __fsub_rn(1.0f, b2);
+__device__ __forceinline__ void adam_range(float* __restrict__ var, const float* __restrict__ grad,
+                                           float* __restrict__ m, float* __restrict__ v,
+                                           int64_t n, int64_t first4, int64_t stride4,
+                                           float alpha, float omb1, float omb2, float eps) {
   const int64_t n4 = n >> 2;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+  for (int64_t i = first4; i < n4; i += stride4) {
     float4 p = ((float4*)var)[i], g = ((const float4*)grad)[i];
     float4 mm = ((float4*)m)[i], vv = ((float4*)v)[i];
     adam1(p.x, g.x, mm.x, vv.x, alpha, omb1, omb2, eps);
@@ -279,8 +284,42 @@ __global__ __launch_bounds__(256) void k_adam(float* __restrict__ var, const flo
     ((float4*)m)[i] = mm;
     ((float4*)v)[i] = vv;
   }
-  for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+  for (int64_t i = (n4 << 2) + first4; i < n; i += stride4)
     adam1(var[i], grad[i], m[i], v[i], alpha, omb1, omb2, eps);
+}
+
+__global__ __launch_bounds__(256) void k_adam(float* __restrict__ var, const float* __restrict__ grad,
+                                              float* __restrict__ m, float* __restrict__ v,
+                                              float* state, int slot, int64_t n, float lr,
+                                              float b1, float b2, float eps) {
+  const float alpha = adam_alpha(state, slot, lr, b1, b2);
+  const float omb1 = __fsub_rn(1.0f, b1), omb2 = __fsub_rn(1.0f, b2);
+  adam_range(var, grad, m, v, n, (int64_t)blockIdx.x * blockDim.x + threadIdx.x,
+             (int64_t)gridDim.x * blockDim.x, alpha, omb1, omb2, eps);
+}
+
+// Multi-tensor form: one launch over up to 16 separately allocated gradients
+// (autograd's own grad tensors, no flat-gradient zeroing / accumulation).
+struct AdamMulti {
+  float* var[DQ_MAX_TENSORS];
+  const float* grad[DQ_MAX_TENSORS];
+  float* m[DQ_MAX_TENSORS];
+  float* v[DQ_MAX_TENSORS];
+  int64_t n[DQ_MAX_TENSORS];
+  int32_t block_start[DQ_MAX_TENSORS + 1];
+  int32_t count;
+};
+
+__global__ __launch_bounds__(256) void k_adam_multi(AdamMulti a, float* state, int slot, float lr,
+                                                    float b1, float b2, float eps) {
+  const float alpha = adam_alpha(state, slot, lr, b1, b2);
+  const float omb1 = __fsub_rn(1.0f, b1), omb2 = __fsub_rn(1.0f, b2);
+  int t = 0;
+  while (t + 1 < a.count && (int)blockIdx.x >= a.block_start[t + 1]) ++t;
+  const int64_t lb = blockIdx.x - a.block_start[t];
+  const int64_t nb = a.block_start[t + 1] - a.block_start[t];
+  adam_range(a.var[t], a.grad[t], a.m[t], a.v[t], a.n[t], lb * blockDim.x + threadIdx.x,
+             nb * blockDim.x, alpha, omb1, omb2, eps);
 }
 
 __global__ __launch_bounds__(256) void k_rmsprop(float* var, const float* grad, float* ms, float* mg,
@@ -384,18 +423,42 @@ int dq_iqn_loss(const float* online_qv, const float* target_qv, const float* tar
   return DQ_OK;
 }
 
-int dq_adam_tf1(float* var, const float* grad, float* m, float* v, float* state, int64_t n,
-                float lr, float beta1, float beta2, float eps, void* stream) {
-  DQ_CHECK_ARG(var && grad && m && v && state && n >= 0, "bad arguments");
+int dq_adam_tf1(float* var, const float* grad, float* m, float* v, float* state, int32_t slot,
+                int64_t n, float lr, float beta1, float beta2, float eps, void* stream) {
+  DQ_CHECK_ARG(var && grad && m && v && state && n >= 0 && (slot == 0 || slot == 1), "bad arguments");
   DQ_CHECK_ARG(((uintptr_t)var | (uintptr_t)grad | (uintptr_t)m | (uintptr_t)v) % 16 == 0,
                "adam buffers must be 16-byte aligned");
-  hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_adam_prep, dim3(1), dim3(1), 0, s, state, lr, beta1, beta2);
-  DQ_CHECK_LAUNCH("k_adam_prep");
-  if (n == 0) return DQ_OK;
-  hipLaunchKernelGGL(k_adam, dim3(elementwise_grid(n)), dim3(256), 0, s, var, grad, m, v, state, n,
-                     beta1, beta2, eps);
+  hipLaunchKernelGGL(k_adam, dim3(elementwise_grid(n)), dim3(256), 0, (hipStream_t)stream, var,
+                     grad, m, v, state, slot, n, lr, beta1, beta2, eps);
   DQ_CHECK_LAUNCH("k_adam");
+  return DQ_OK;
+}
+
+int dq_adam_tf1_multi(const dq_tensor_list* t, float* state, int32_t slot, float lr, float beta1,
+                      float beta2, float eps, void* stream) {
+  DQ_CHECK_ARG(t && state && (slot == 0 || slot == 1), "bad arguments");
+  DQ_CHECK_ARG(t->count >= 1 && t->count <= DQ_MAX_TENSORS, "1..16 tensors");
+  AdamMulti a;
+  a.count = t->count;
+  int32_t blocks = 0;
+  for (int i = 0; i < t->count; ++i) {
+    DQ_CHECK_ARG(t->var[i] && t->grad[i] && t->m[i] && t->v[i] && t->n[i] > 0, "null tensor");
+    DQ_CHECK_ARG(((uintptr_t)t->var[i] | (uintptr_t)t->grad[i] | (uintptr_t)t->m[i] |
+                  (uintptr_t)t->v[i]) % 16 == 0, "adam tensors must be 16-byte aligned");
+    a.var[i] = t->var[i];
+    a.grad[i] = t->grad[i];
+    a.m[i] = t->m[i];
+    a.v[i] = t->v[i];
+    a.n[i] = t->n[i];
+    a.block_start[i] = blocks;
+    int64_t nb = (t->n[i] + 4095) / 4096;   // 16 floats per thread per block pass
+    if (nb > 512) nb = 512;
+    blocks += (int32_t)nb;
+  }
+  a.block_start[t->count] = blocks;
+  hipLaunchKernelGGL(k_adam_multi, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a, state,
+                     slot, lr, beta1, beta2, eps);
+  DQ_CHECK_LAUNCH("k_adam_multi");
   return DQ_OK;
 }
 

@@ -76,17 +76,47 @@ def iqn_loss(online_qv, target_qv, target_qv_action, taus, actions, rewards, ter
 class TF1Adam(object):
   """tf.train.AdamOptimizer over one flat fp32 buffer (ApplyAdam semantics)."""
 
-  def __init__(self, params, learning_rate=0.001, beta1=0.9, beta2=0.999, epsilon=1e-8):
+  supports_multi = True
+
+  def __init__(self, params, learning_rate=0.001, beta1=0.9, beta2=0.999, epsilon=1e-8,
+               segments=None):
     self.params = params
     self.lr, self.b1, self.b2, self.eps = float(learning_rate), float(beta1), float(beta2), float(epsilon)
     self.m = torch.zeros_like(params)
     self.v = torch.zeros_like(params)
+    # {beta1_power, beta2_power} double-buffered: step t reads slot t % 2
     self.state = torch.tensor([beta1, beta2, 0.0, 0.0], dtype=torch.float32, device=params.device)
+    self.segments = segments
+    self.t = 0
 
-  def step(self, grad):
+  def _slot(self, slot):
+    if slot is None:
+      slot = self.t % 2
+      self.t += 1
+    return int(slot)
+
+  def step(self, grad, slot=None):
+    """Update from ONE flat gradient buffer (same layout as ``params``)."""
     _lib.call('dq_adam_tf1', p(self.params), p(_c(grad, torch.float32)), p(self.m), p(self.v),
-              p(self.state), self.params.numel(), self.lr, self.b1, self.b2, self.eps,
-              _stream(self.params))
+              p(self.state), self._slot(slot), self.params.numel(), self.lr, self.b1, self.b2,
+              self.eps, _stream(self.params))
+
+  def step_multi(self, grads, slot=None):
+    """Update from per-parameter gradient tensors (memory order = the parameter
+    slices ``segments`` of the flat buffer) in one launch."""
+    assert self.segments is not None and len(grads) == len(self.segments)
+    tl = _lib.TensorList()
+    tl.count = len(grads)
+    base_p, base_m, base_v = self.params.data_ptr(), self.m.data_ptr(), self.v.data_ptr()
+    for i, ((o, n), g) in enumerate(zip(self.segments, grads)):
+      assert g.numel() == n and g.dtype == torch.float32 and g.is_cuda
+      tl.var[i] = base_p + 4 * o
+      tl.grad[i] = g.data_ptr()
+      tl.m[i] = base_m + 4 * o
+      tl.v[i] = base_v + 4 * o
+      tl.n[i] = n
+    _lib.call('dq_adam_tf1_multi', ctypes.byref(tl), p(self.state), self._slot(slot), self.lr,
+              self.b1, self.b2, self.eps, _stream(self.params))
 
 
 class TF1RMSProp(object):
@@ -101,7 +131,9 @@ class TF1RMSProp(object):
     self.mg = torch.zeros_like(params)
     self.mom = torch.zeros_like(params)
 
-  def step(self, grad):
+  supports_multi = False
+
+  def step(self, grad, slot=None):
     _lib.call('dq_rmsprop_tf1', p(self.params), p(_c(grad, torch.float32)), p(self.ms), p(self.mg),
               p(self.mom), self.params.numel(), self.lr, self.decay, self.mu, self.eps,
               int(self.centered), _stream(self.params))

@@ -168,9 +168,25 @@ int dq_iqn_loss(const float* online_qv, const float* target_qv, const float* tar
                 float* mean_loss_out, void* stream);
 
 /* tf.train.AdamOptimizer.apply_gradients over ONE flat fp32 parameter buffer.
- * state[0..1] = beta1_power, beta2_power (float32, device; init beta1, beta2). */
-int dq_adam_tf1(float* var, const float* grad, float* m, float* v, float* state, int64_t n,
-                float lr, float beta1, float beta2, float eps, void* stream);
+ * state = {beta1_power, beta2_power}[2] (float32, device; slot 0 initialised to
+ * {beta1, beta2}); step t reads slot t%2 and writes beta^(t+1) into the other. */
+int dq_adam_tf1(float* var, const float* grad, float* m, float* v, float* state, int32_t slot,
+                int64_t n, float lr, float beta1, float beta2, float eps, void* stream);
+
+/* The same update over up to DQ_MAX_TENSORS separately allocated tensors in ONE
+ * launch (e.g. autograd's per-parameter gradients; no flat-gradient copy). */
+#define DQ_MAX_TENSORS 16
+typedef struct dq_tensor_list {
+  int32_t count;
+  int32_t pad_;
+  float* var[DQ_MAX_TENSORS];
+  const float* grad[DQ_MAX_TENSORS];
+  float* m[DQ_MAX_TENSORS];
+  float* v[DQ_MAX_TENSORS];
+  int64_t n[DQ_MAX_TENSORS];
+} dq_tensor_list;
+int dq_adam_tf1_multi(const dq_tensor_list* tensors, float* state, int32_t slot, float lr,
+                      float beta1, float beta2, float eps, void* stream);
 
 /* tf.train.RMSPropOptimizer(centered=True) (dqn_agent.py:100-105; rms init 1). */
 int dq_rmsprop_tf1(float* var, const float* grad, float* ms, float* mg, float* mom, int64_t n,

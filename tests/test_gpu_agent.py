@@ -52,11 +52,11 @@ def test_rainbow_step_matches_cpu_restatement():
   np.testing.assert_allclose(a._loss_out['loss'].cpu().numpy(), exp['loss'], rtol=1e-4, atol=1e-5)
   on.fp.grad.zero_()
   logits.backward(torch.from_numpy(exp['grad'].astype(np.float32)))
-  np.testing.assert_allclose(a.online_convnet.fp.grad.cpu().numpy(), on.fp.grad.numpy(),
+  np.testing.assert_allclose(a.online_convnet.fp.gather_grads().cpu().numpy(), on.fp.grad.numpy(),
                              rtol=1e-3, atol=1e-6)
   adam = OL.TF1Adam(on.fp.numel, 6.25e-5, eps=1.5e-4)
   w = w0.numpy().copy()
-  adam.step(w, a.online_convnet.fp.grad.cpu().numpy())
+  adam.step(w, a.online_convnet.fp.gather_grads().cpu().numpy())
   np.testing.assert_allclose(a.online_convnet.fp.flat.cpu().numpy(), w, rtol=1e-5, atol=1e-7)
   # the priorities written back are sqrt(loss + 1e-10) of this step
   pri = a._replay.memory.get_priority(t['indices'].numpy().astype(np.int32))

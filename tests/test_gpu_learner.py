@@ -134,3 +134,25 @@ def test_sync_copy():
   b = torch.zeros_like(a)
   ops.sync_copy(b, a)
   assert torch.equal(a, b)
+
+
+def test_adam_multi_tensor_equals_flat():
+  """One launch over per-parameter gradients == the flat-buffer update."""
+  from dopamine_amd import ops
+  from dopamine_amd.agents.networks import RainbowNetwork
+  net = RainbowNetwork(9, device='cuda', seed=0)
+  segs = net.fp.segments()
+  flat0 = net.fp.flat.clone()
+  a = ops.TF1Adam(net.fp.flat, 6.25e-5, epsilon=1.5e-4, segments=segs)
+  ref_p = flat0.clone()
+  b = ops.TF1Adam(ref_p, 6.25e-5, epsilon=1.5e-4)
+  for step in range(3):
+    grads = [torch.randn_like(prm) for prm in net.parameters()]   # param-like strides
+    flat_g = torch.zeros_like(ref_p)
+    for (o, n), g, v in zip(segs, grads, net.fp.grad_views):
+      v.copy_(g)
+    flat_g.copy_(net.fp.grad)
+    a.step_multi(grads)
+    b.step(flat_g)
+  assert torch.equal(net.fp.flat, ref_p)
+  assert torch.equal(a.state, b.state)
