@@ -21,6 +21,7 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+os.environ.setdefault('HIP_FORCE_DEV_KERNARG', '1')   # as dopamine_amd/__init__.py; before HIP init
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

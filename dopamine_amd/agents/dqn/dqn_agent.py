@@ -222,11 +222,16 @@ class DQNAgent(object):
       ev.record(main)
       self._side.wait_event(ev)
       with torch.cuda.stream(self._side):
+        self._post_loss(self._pbuf[c])
         self._prefetch(1 - c)
       self._backward(y, g)
       main.wait_stream(self._side)
     else:
+      self._post_loss(self._pbuf[c])
       self._backward(y, g)
+
+  def _post_loss(self, t):
+    """Work that needs the loss but not the gradient (PER priority write-back)."""
 
   def _device_opt_step(self, k):
     """Optimizer step k (k = gradient-step parity: TF1 Adam's beta-power slot)."""

@@ -125,10 +125,13 @@ class RainbowAgent(dqn_agent.DQNAgent):
                        self._support, self.cumulative_gamma,
                        probs=t['sampling_probabilities'] if prioritized else None,
                        out=self._loss_out)
-    if prioritized:
-      # sqrt(loss + 1e-10) of the UNWEIGHTED loss, before the optimizer (rb:289-297)
-      self._replay.tf_set_priority(t['indices'], out['priorities'])
     return logits, out['grad']
+
+  def _post_loss(self, t):
+    if self._replay_scheme == 'prioritized':
+      # sqrt(loss + 1e-10) of the UNWEIGHTED loss (rb:289-290); it precedes the
+      # next step's sample on the same stream, as control_dependencies order it.
+      self._replay.tf_set_priority(t['indices'], self._loss_out['priorities'])
 
   def _store_transition(self, last_observation, action, reward, is_terminal, priority=None):
     """rainbow_agent.py:307-337."""

@@ -439,20 +439,29 @@ __global__ __launch_bounds__(256) void k_gather_nhwc4(ReplayView v, GatherOut g)
   if (!dst_base) return;
   const int64_t base = stack_base(v, g, b, which);
   const int64_t nd = v.obs_bytes >> 2;
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nd) return;
+  const int lane = threadIdx.x & 63;
+  // this wave's 64 dwords (256 pixels) of each of the 4 frames
+  const int64_t d0 = ((int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63));
+  if (d0 >= nd) return;
+  const int64_t d = d0 + lane;
   uint32_t w[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k)
-    w[k] = ((const uint32_t*)(v.frames + pymod(base - 3 + k, v.C) * v.obs_bytes))[t];
-  float4 c[4];
+    w[k] = d < nd ? ((const uint32_t*)(v.frames + pymod(base - 3 + k, v.C) * v.obs_bytes))[d] : 0u;
+  // store j: lane l writes pixel 64j + l (its 4 channels = 16 B), so every store
+  // instruction covers 1 KiB contiguous; the bytes come from lane 16j + l/4.
+  float4* dst = (float4*)(dst_base + (int64_t)b * 4 * v.obs_bytes) + 4 * d0;
+  const int sh = 8 * (lane & 3);
 #pragma unroll
-  for (int k = 0; k < 4; ++k) c[k] = u8x4_to_f32_255(w[k]);
-  float4* dst = (float4*)(dst_base + (int64_t)b * 4 * v.obs_bytes) + 4 * t;
-  dst[0] = make_float4(c[0].x, c[1].x, c[2].x, c[3].x);
-  dst[1] = make_float4(c[0].y, c[1].y, c[2].y, c[3].y);
-  dst[2] = make_float4(c[0].z, c[1].z, c[2].z, c[3].z);
-  dst[3] = make_float4(c[0].w, c[1].w, c[2].w, c[3].w);
+  for (int j = 0; j < 4; ++j) {
+    const int src = 16 * j + (lane >> 2);
+    float4 o;
+    o.x = __fdiv_rn((float)((__shfl(w[0], src) >> sh) & 0xffu), 255.0f);
+    o.y = __fdiv_rn((float)((__shfl(w[1], src) >> sh) & 0xffu), 255.0f);
+    o.z = __fdiv_rn((float)((__shfl(w[2], src) >> sh) & 0xffu), 255.0f);
+    o.w = __fdiv_rn((float)((__shfl(w[3], src) >> sh) & 0xffu), 255.0f);
+    if (4 * d0 + 64 * j + lane < 4 * nd) dst[64 * j + lane] = o;
+  }
 }
 
 __device__ __forceinline__ int64_t frame_of(const ReplayView& v, const GatherOut& g, int slot,
