@@ -4,7 +4,7 @@ import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, 'libdopamine_amd.so')
-SOURCES = [os.path.join(_HERE, 'csrc', f) for f in ('replay.hip', 'learner.hip')]
+SOURCES = [os.path.join(_HERE, 'csrc', f) for f in ('replay.hip', 'learner.hip', 'nature_cnn.hip')]
 HEADER = os.path.join(os.path.dirname(_HERE), 'include', 'dopamine_amd.h')
 ARCH = os.environ.get('DQ_OFFLOAD_ARCH', 'gfx950')
 

@@ -1,0 +1,103 @@
+"""HIP Nature-CNN executor over a network's flat parameter buffer.
+
+Forward and backward of the DQN / Rainbow Nature-CNN (atari_lib.py:85-144) run
+as ~7 + 13 fused implicit-GEMM launches on the fp32 matrix cores
+(dopamine_amd/csrc/nature_cnn.hip) instead of ~20 + 30 PyTorch/MIOpen kernels.
+The backward writes every weight/bias gradient straight into the flat gradient
+buffer (plain stores), which the TF1 optimizer kernel then consumes.
+"""
+import ctypes
+
+import torch
+
+from dopamine_amd import _lib
+
+
+class CnnParams(ctypes.Structure):
+  _fields_ = [('in_channels', ctypes.c_int32), ('n_out', ctypes.c_int32)] + [
+      (n, ctypes.c_void_p) for n in ('conv1_w', 'conv1_b', 'conv2_w', 'conv2_b', 'conv3_w',
+                                     'conv3_b', 'fc1_w', 'fc1_b', 'fc2_w', 'fc2_b')]
+
+
+class CnnActs(ctypes.Structure):
+  _fields_ = [(n, ctypes.c_void_p) for n in ('a1', 'a2', 'a3', 'h', 'out')]
+
+
+_sigs = {
+    'dq_cnn_forward': ([ctypes.POINTER(CnnParams), ctypes.c_int32, ctypes.c_void_p,
+                        ctypes.POINTER(CnnActs), ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
+    'dq_cnn_backward': ([ctypes.POINTER(CnnParams), ctypes.POINTER(CnnParams), ctypes.c_int32,
+                         ctypes.c_void_p, ctypes.POINTER(CnnActs), ctypes.c_void_p,
+                         ctypes.POINTER(CnnActs), ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
+    'dq_cnn_workspace_floats': ([ctypes.c_int32, ctypes.c_int32], ctypes.c_size_t),
+}
+for _n, (_a, _r) in _sigs.items():
+  getattr(_lib.lib, _n).argtypes = _a
+  getattr(_lib.lib, _n).restype = _r
+
+_NAMES = ('conv1_w', 'conv1_b', 'conv2_w', 'conv2_b', 'conv3_w', 'conv3_b', 'fc1_w', 'fc1_b',
+          'fc2_w', 'fc2_b')
+
+
+def _params_struct(fp, buf, n_out, in_ch):
+  s = CnnParams(in_channels=in_ch, n_out=n_out)
+  base = buf.data_ptr()
+  for n in _NAMES:
+    o, _ = fp.offsets[n]
+    setattr(s, n, base + 4 * o)
+  return s
+
+
+class HipNatureCNN(object):
+  """Executes a ``NatureDQNNetwork`` / ``RainbowNetwork``'s parameters with the
+  HIP kernels.  ``forward`` keeps its activations for ``backward``; use one
+  executor per concurrent stream (online vs target)."""
+
+  def __init__(self, net, batch_size):
+    fp = net.fp
+    self.net = net
+    self.B = int(batch_size)
+    shape = fp.offsets['fc2_w'][1]
+    self.n_out = int(shape[0])
+    self.in_ch = int(fp.offsets['conv1_w'][1][1])
+    assert self.in_ch == 4 and fp.offsets['fc1_w'][1] == (512, 7744), 'Nature-CNN geometry only'
+    dev = fp.flat.device
+    B = self.B
+    mk = lambda *s: torch.empty(s, dtype=torch.float32, device=dev)
+    self.acts = dict(a1=mk(B, 21, 21, 32), a2=mk(B, 11, 11, 64), a3=mk(B, 7744), h=mk(B, 512),
+                     out=mk(B, self.n_out))
+    self.dacts = dict(a1=mk(B, 21, 21, 32), a2=mk(B, 11, 11, 64), a3=mk(B, 7744), h=mk(B, 512),
+                      out=mk(1))
+    self.ws = mk(int(_lib.lib.dq_cnn_workspace_floats(B, self.n_out)) + 64)
+    self._p = _params_struct(fp, fp.flat, self.n_out, self.in_ch)
+    self._g = _params_struct(fp, fp.grad, self.n_out, self.in_ch)
+    self._a = CnnActs(**{k: v.data_ptr() for k, v in self.acts.items()})
+    self._d = CnnActs(**{k: v.data_ptr() for k, v in self.dacts.items()})
+    self._x = None
+
+  @staticmethod
+  def _stream(t):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+  def forward(self, x):
+    """x: (B, 84, 84, 4) NHWC float32, or its (B, 4, 84, 84) channels_last view.
+    Returns the (B, n_out) output buffer (overwritten by the next call)."""
+    if x.dim() == 4 and x.shape[1] == self.in_ch and x.shape[-1] != self.in_ch:
+      x = x.permute(0, 2, 3, 1)              # channels_last NCHW view -> NHWC
+    assert x.shape == (self.B, 84, 84, 4) and x.is_contiguous() and x.dtype == torch.float32
+    self._x = x
+    _lib.check(_lib.lib.dq_cnn_forward(ctypes.byref(self._p), self.B, x.data_ptr(),
+                                       ctypes.byref(self._a), self.ws.data_ptr(), self._stream(x)),
+               'dq_cnn_forward')
+    return self.acts['out']
+
+  def backward(self, dout):
+    """dout: (B, n_out).  Writes all parameter gradients into net.fp.grad."""
+    dout = dout.reshape(self.B, self.n_out)
+    assert dout.is_contiguous() and self._x is not None
+    _lib.check(_lib.lib.dq_cnn_backward(ctypes.byref(self._p), ctypes.byref(self._g), self.B,
+                                        self._x.data_ptr(), ctypes.byref(self._a),
+                                        dout.data_ptr(), ctypes.byref(self._d),
+                                        self.ws.data_ptr(), self._stream(dout)),
+               'dq_cnn_backward')
+    return self.net.fp.grad

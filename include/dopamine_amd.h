@@ -193,6 +193,36 @@ int dq_rmsprop_tf1(float* var, const float* grad, float* ms, float* mg, float* m
                    float lr, float decay, float momentum, float eps, int32_t centered,
                    void* stream);
 
+/* ---------------- Nature-CNN (atari_lib.py:85-144) on fp32 MFMA ----------------
+ * Input x: (B, 84, 84, 4) NHWC float32 (the gather's DQ_LAYOUT_F32_NHWC).  Weights
+ * are views into the flat parameter buffer: conv (out, kh, kw, in), FC (out, in).
+ * Activations NHWC; the 7744 flatten is TF's (h, w, c) order. */
+typedef struct dq_cnn_params {
+  int32_t in_channels;            /* stack size, 4 */
+  int32_t n_out;                  /* num_actions (DQN) or num_actions * num_atoms (C51) */
+  float* conv1_w; float* conv1_b; /* (32, 8, 8, 4), (32) */
+  float* conv2_w; float* conv2_b; /* (64, 4, 4, 32), (64) */
+  float* conv3_w; float* conv3_b; /* (64, 3, 3, 64), (64) */
+  float* fc1_w; float* fc1_b;     /* (512, 7744), (512) */
+  float* fc2_w; float* fc2_b;     /* (n_out, 512), (n_out) */
+} dq_cnn_params;
+typedef struct dq_cnn_acts {      /* per-call activations (or their gradients) */
+  float* a1;                      /* (B, 21, 21, 32) */
+  float* a2;                      /* (B, 11, 11, 64) */
+  float* a3;                      /* (B, 7744) */
+  float* h;                       /* (B, 512) */
+  float* out;                     /* (B, n_out) */
+} dq_cnn_acts;
+/* forward: relu(conv1..3), relu(fc1), fc2 -> a->out.  ws: dq_cnn_workspace_floats() floats. */
+int dq_cnn_forward(const dq_cnn_params* p, int32_t batch, const float* x, dq_cnn_acts* a,
+                   float* ws, void* stream);
+/* backward from d out (B, n_out): writes EVERY weight/bias gradient into g (plain stores,
+ * no accumulation); d holds the intermediate activation gradients. */
+int dq_cnn_backward(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch, const float* x,
+                    const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d, float* ws,
+                    void* stream);
+size_t dq_cnn_workspace_floats(int32_t batch, int32_t n_out);
+
 /* _build_sync_op (dqn_agent.py:324-339): online -> target copy of the flat buffer. */
 int dq_sync_copy(void* dst, const void* src, int64_t bytes, void* stream);
 

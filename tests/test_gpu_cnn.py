@@ -1,0 +1,69 @@
+"""HIP Nature-CNN (fp32 MFMA implicit GEMM) vs the PyTorch network on the same
+flat parameters: forward outputs and every parameter gradient.  Tolerance is
+relative to each tensor's scale (fp32 with different summation orders)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, rtol=2e-5):
+  a, b = a.double(), b.double()
+  scale = b.abs().max().item() + 1e-30
+  err = (a - b).abs().max().item()
+  assert err <= rtol * scale, 'max err %.3g vs scale %.3g' % (err, scale)
+
+
+@pytest.mark.parametrize('kind,B,A', [('rainbow', 32, 9), ('dqn', 32, 6), ('rainbow', 7, 4)])
+def test_hip_cnn_matches_torch(kind, B, A):
+  from dopamine_amd.agents.networks import NatureDQNNetwork, RainbowNetwork
+  from dopamine_amd.cnn import HipNatureCNN
+  torch.manual_seed(0)
+  net = RainbowNetwork(A, device='cuda', seed=3) if kind == 'rainbow' else NatureDQNNetwork(A, device='cuda', seed=3)
+  with torch.no_grad():     # non-zero biases so the bias paths are exercised
+    for n, prm in net.fp.params.items():
+      if n.endswith('_b'):
+        prm.uniform_(-0.05, 0.1)
+  x_nhwc = torch.rand(B, 84, 84, 4, device='cuda')
+  x = x_nhwc.permute(0, 3, 1, 2)            # channels_last view, as the gather produces
+  y_ref = net(x).reshape(B, -1)
+  gout = torch.randn_like(y_ref)
+  for prm in net.parameters():
+    prm.grad = None
+  y_ref.backward(gout)
+  g_ref = [prm.grad.detach().clone() for prm in net.parameters()]
+
+  hip = HipNatureCNN(net, B)
+  y = hip.forward(x)
+  _close(y, y_ref.detach())
+  hip.backward(gout)
+  for (name, view), gr in zip(zip(net.fp.params.keys(), net.fp.grad_views), g_ref):
+    try:
+      _close(view, gr, rtol=5e-5)
+    except AssertionError as e:
+      raise AssertionError('%s: %s' % (name, e))
+
+
+def test_hip_cnn_graph_capturable_and_deterministic():
+  from dopamine_amd.agents.networks import RainbowNetwork
+  from dopamine_amd.cnn import HipNatureCNN
+  net = RainbowNetwork(9, device='cuda', seed=1)
+  hip = HipNatureCNN(net, 32)
+  x = torch.rand(32, 84, 84, 4, device='cuda')
+  gout = torch.randn(32, 459, device='cuda')
+  hip.forward(x); hip.backward(gout)
+  ref_y, ref_g = hip.acts['out'].clone(), net.fp.grad.clone()
+  g = torch.cuda.CUDAGraph()
+  s = torch.cuda.Stream()
+  s.wait_stream(torch.cuda.current_stream())
+  with torch.cuda.stream(s):
+    hip.forward(x); hip.backward(gout)
+  torch.cuda.current_stream().wait_stream(s)
+  with torch.cuda.graph(g):
+    hip.forward(x); hip.backward(gout)
+  net.fp.grad.zero_()
+  g.replay()
+  torch.cuda.synchronize()
+  assert torch.equal(hip.acts['out'], ref_y)
+  assert torch.equal(net.fp.grad, ref_g)     # split-K reduced in fixed order: bitwise stable
