@@ -45,6 +45,16 @@ class TensorList(ctypes.Structure):
               ('n', ctypes.c_int64 * MAX_TENSORS)]
 
 
+class CnnParams(ctypes.Structure):
+  _fields_ = [('in_channels', ctypes.c_int32), ('n_out', ctypes.c_int32)] + [
+      (n, ctypes.c_void_p) for n in ('conv1_w', 'conv1_b', 'conv2_w', 'conv2_b', 'conv3_w',
+                                     'conv3_b', 'fc1_w', 'fc1_b', 'fc2_w', 'fc2_b')]
+
+
+class CnnActs(ctypes.Structure):
+  _fields_ = [(n, ctypes.c_void_p) for n in ('a1', 'a2', 'a3', 'h', 'out')]
+
+
 _P = ctypes.c_void_p
 _I32 = ctypes.c_int32
 _I64 = ctypes.c_int64
@@ -75,7 +85,12 @@ SIGNATURES = {
     'dq_adam_tf1_multi': [ctypes.POINTER(TensorList), _P, _I32, _F, _F, _F, _F, _P],
     'dq_rmsprop_tf1': [_P, _P, _P, _P, _P, _I64, _F, _F, _F, _F, _I32, _P],
     'dq_sync_copy': [_P, _P, _I64, _P],
+    'dq_cnn_forward': [ctypes.POINTER(CnnParams), _I32, _P, ctypes.POINTER(CnnActs), _P, _P],
+    'dq_cnn_backward': [ctypes.POINTER(CnnParams), ctypes.POINTER(CnnParams), _I32, _P,
+                        ctypes.POINTER(CnnActs), _P, ctypes.POINTER(CnnActs), _P, _P],
+    'dq_cnn_workspace_floats': [_I32, _I32],
 }
+RESTYPES = {'dq_last_error': ctypes.c_char_p, 'dq_cnn_workspace_floats': ctypes.c_size_t}
 
 
 class DQError(RuntimeError):
@@ -91,7 +106,7 @@ def _load():
   for name, args in SIGNATURES.items():
     fn = getattr(lib, name)
     fn.argtypes = args
-    fn.restype = ctypes.c_char_p if name == 'dq_last_error' else ctypes.c_int
+    fn.restype = RESTYPES.get(name, ctypes.c_int)
   if lib.dq_abi_version() != ABI_VERSION:
     raise ImportError('dopamine_amd ABI mismatch: lib %d, python %d' % (lib.dq_abi_version(), ABI_VERSION))
   return lib

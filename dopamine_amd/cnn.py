@@ -13,27 +13,7 @@ import torch
 from dopamine_amd import _lib
 
 
-class CnnParams(ctypes.Structure):
-  _fields_ = [('in_channels', ctypes.c_int32), ('n_out', ctypes.c_int32)] + [
-      (n, ctypes.c_void_p) for n in ('conv1_w', 'conv1_b', 'conv2_w', 'conv2_b', 'conv3_w',
-                                     'conv3_b', 'fc1_w', 'fc1_b', 'fc2_w', 'fc2_b')]
-
-
-class CnnActs(ctypes.Structure):
-  _fields_ = [(n, ctypes.c_void_p) for n in ('a1', 'a2', 'a3', 'h', 'out')]
-
-
-_sigs = {
-    'dq_cnn_forward': ([ctypes.POINTER(CnnParams), ctypes.c_int32, ctypes.c_void_p,
-                        ctypes.POINTER(CnnActs), ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
-    'dq_cnn_backward': ([ctypes.POINTER(CnnParams), ctypes.POINTER(CnnParams), ctypes.c_int32,
-                         ctypes.c_void_p, ctypes.POINTER(CnnActs), ctypes.c_void_p,
-                         ctypes.POINTER(CnnActs), ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
-    'dq_cnn_workspace_floats': ([ctypes.c_int32, ctypes.c_int32], ctypes.c_size_t),
-}
-for _n, (_a, _r) in _sigs.items():
-  getattr(_lib.lib, _n).argtypes = _a
-  getattr(_lib.lib, _n).restype = _r
+CnnParams, CnnActs = _lib.CnnParams, _lib.CnnActs
 
 _NAMES = ('conv1_w', 'conv1_b', 'conv2_w', 'conv2_b', 'conv3_w', 'conv3_b', 'fc1_w', 'fc1_b',
           'fc2_w', 'fc2_b')
