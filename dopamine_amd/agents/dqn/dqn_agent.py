@@ -82,6 +82,7 @@ class DQNAgent(object):
                batch_size=32,
                use_hip_graph=True,
                pipeline=True,
+               use_hip_cnn=True,
                device=None,
                seed=0,
                process_group=None):
@@ -115,6 +116,7 @@ class DQNAgent(object):
     self._pg = process_group
     self.use_hip_graph = use_hip_graph
     self.pipeline = pipeline
+    self.use_hip_cnn = use_hip_cnn
     self._graphs = None
     self._graphs_opt = None
     self._eager_steps = 0
@@ -155,6 +157,28 @@ class DQNAgent(object):
   def _build_networks(self):
     self.online_convnet = self._make_network(self._seed)
     self.target_convnet = self._make_network(self._seed + 1)
+    # Nature-CNN nets run on the HIP implicit-GEMM kernels (dopamine_amd/cnn.py);
+    # the torch modules keep the parameters (flat buffer) and serve action selection.
+    self._hip = None
+    if (self.use_hip_cnn and self.network in (networks.NatureDQNNetwork, networks.RainbowNetwork)
+        and self.observation_shape == NATURE_DQN_OBSERVATION_SHAPE and self.stack_size == 4):
+      from dopamine_amd.cnn import HipNatureCNN
+      B = self._batch_size
+      self._hip = dict(online=HipNatureCNN(self.online_convnet, B),
+                       target=[HipNatureCNN(self.target_convnet, B) for _ in range(2)])
+
+  def _online_forward(self, x):
+    """Online network output for the loss (keeps what the backward needs)."""
+    if self._hip is not None:
+      return self._hip['online'].forward(x)
+    return self.online_convnet(self._state_input(x))
+
+  def _target_net(self, x, slot):
+    """Target network output (no gradient) into pipeline slot ``slot``."""
+    if self._hip is not None:
+      return self._hip['target'][slot].forward(x)
+    with torch.no_grad():
+      return self.target_convnet(self._state_input(x))
 
   def _build_train_op(self):
     B, A, dev = self._batch_size, self.num_actions, self._device
@@ -171,18 +195,20 @@ class DQNAgent(object):
   #   _target_forward(t)      target-network outputs the loss needs (no grad)
   #   _online_loss(t, tgt)    online forward + the loss kernel -> (output, d loss/d output)
   #   _backward(y, g)         backward into the flat gradient
-  def _target_forward(self, t):
-    with torch.no_grad():
-      return {'q': self.target_convnet(self._state_input(t['next_state']))}
+  def _target_forward(self, t, slot):
+    return {'q': self._target_net(t['next_state'], slot)}
 
   def _online_loss(self, t, tgt):
     """dqn_agent.py:283-322."""
-    q = self.online_convnet(self._state_input(t['state']))
+    q = self._online_forward(t['state'])
     out = ops.dqn_huber_loss(q.detach(), tgt['q'], t['action'], t['reward'], t['terminal'],
                              self.cumulative_gamma, out=self._loss_out)
     return q, out['grad']
 
   def _backward(self, y, g):
+    if self._hip is not None:       # all gradients stored into the flat buffer
+      self._hip['online'].backward(g)
+      return
     # Fresh per-parameter gradients (no flat-buffer zeroing + accumulate kernels);
     # the multi-tensor TF1 Adam reads them in place.
     for prm in self.online_convnet.parameters():
@@ -192,7 +218,8 @@ class DQNAgent(object):
       self.online_convnet.fp.gather_grads()
 
   def _needs_flat_grad(self):
-    return self._pg is not None or not getattr(self._opt, 'supports_multi', False)
+    return (self._hip is not None or self._pg is not None or
+            not getattr(self._opt, 'supports_multi', False))
 
   # Pipelined step.  Slot c holds step t's batch and its target-net outputs.
   # After step t's loss kernel (and priority write-back) a second HIP stream
@@ -206,7 +233,10 @@ class DQNAgent(object):
     t = mem.sample_device(self._batch_size, layout=self._replay._layout, out=self._pbuf[i],
                           reserve=False)
     self._pbuf[i] = t
-    tg = self._target_forward(t)
+    tg = self._target_forward(t, i)
+    if self._hip is not None:       # persistent per-slot output buffers: no copy
+      self._ptgt[i] = tg
+      return
     if self._ptgt[i] is None:
       self._ptgt[i] = {k: torch.empty_like(v) for k, v in tg.items()}
     for k, v in tg.items():
@@ -307,9 +337,10 @@ class DQNAgent(object):
   def _sync_target(self):
     ops.sync_copy(self.target_convnet.fp.flat, self.online_convnet.fp.flat)
     if self.pipeline and self._has_prefetch:   # the prefetched target outputs are stale
-      tg = self._target_forward(self._pbuf[self._slot])
+      tg = self._target_forward(self._pbuf[self._slot], self._slot)
       for k, v in tg.items():
-        self._ptgt[self._slot][k].copy_(v)
+        if v.data_ptr() != self._ptgt[self._slot][k].data_ptr():
+          self._ptgt[self._slot][k].copy_(v)
 
   # ------------------------------------------------------------- agent API
   def begin_episode(self, observation):

@@ -55,7 +55,7 @@ class ImplicitQuantileAgent(rainbow_agent.RainbowAgent):
     qv, _ = self.online_convnet(x, self.num_quantile_samples)
     return qv.view(self.num_quantile_samples, x.shape[0], -1).mean(0)
 
-  def _target_forward(self, t):
+  def _target_forward(self, t, slot):
     with torch.no_grad():
       tq, _ = self.target_convnet(t['next_state'], self.num_tau_prime_samples)
       out = {'tq': tq}

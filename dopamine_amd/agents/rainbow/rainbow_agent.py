@@ -113,13 +113,13 @@ class RainbowAgent(dqn_agent.DQNAgent):
     logits = self.online_convnet(x)
     return (torch.softmax(logits, -1) * self._support).sum(-1)
 
-  def _target_forward(self, t):
-    with torch.no_grad():
-      return {'logits': self.target_convnet(t['next_state'])}
+  def _target_forward(self, t, slot):
+    return {'logits': self._target_net(t['next_state'], slot).view(-1, self.num_actions,
+                                                                   self._num_atoms)}
 
   def _online_loss(self, t, tgt):
     """rainbow_agent.py:200-305."""
-    logits = self.online_convnet(t['state'])
+    logits = self._online_forward(t['state']).view(-1, self.num_actions, self._num_atoms)
     prioritized = self._replay_scheme == 'prioritized'
     out = ops.c51_loss(logits.detach(), tgt['logits'], t['action'], t['reward'], t['terminal'],
                        self._support, self.cumulative_gamma,

@@ -14,7 +14,7 @@ HEADER = os.path.join(ROOT, 'include', 'dopamine_amd.h')
 
 def _declared():
   src = open(HEADER).read()
-  return sorted(set(re.findall(r'^\s*(?:int|const char\*)\s+(dq_\w+)\(', src, re.M)))
+  return sorted(set(re.findall(r'^\s*(?:int|size_t|const char\*)\s+(dq_\w+)\(', src, re.M)))
 
 
 def test_library_exports_every_declared_symbol():
