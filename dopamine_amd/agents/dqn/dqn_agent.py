@@ -82,7 +82,7 @@ class DQNAgent(object):
                batch_size=32,
                use_hip_graph=True,
                pipeline=True,
-               use_hip_cnn=False,
+               use_hip_cnn=True,
                device=None,
                seed=0,
                process_group=None):

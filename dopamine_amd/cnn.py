@@ -1,7 +1,7 @@
 """HIP Nature-CNN executor over a network's flat parameter buffer.
 
 Forward and backward of the DQN / Rainbow Nature-CNN (atari_lib.py:85-144) run
-as ~7 + 13 fused implicit-GEMM launches on the fp32 matrix cores
+as 6 + 14 fused implicit-GEMM / reduce launches on the fp32 matrix cores
 (dopamine_amd/csrc/nature_cnn.hip) instead of ~20 + 30 PyTorch/MIOpen kernels.
 The backward writes every weight/bias gradient straight into the flat gradient
 buffer (plain stores), which the TF1 optimizer kernel then consumes.

@@ -1,15 +1,26 @@
 // The Nature-CNN (atari_lib.py:85-144: conv 32@8x8/4, 64@4x4/2, 64@3x3/1 with TF
 // "SAME" padding, ReLU, flatten 7744 in NHWC order, FC 512 + ReLU, FC n_out)
 // forward and backward as implicit-GEMM kernels on the exact-fp32 matrix cores
-// (v_mfma_f32_32x32x2_f32: bit-for-bit a k-ordered fp32 FMA chain).
+// (v_mfma_f32_32x32x2_f32).
 //
-// One templated tile kernel serves every product; operands are produced by
-// loaders (implicit im2col with compile-time geometry, transposed-conv gathers
-// with the ReLU mask fused, plain row-major) and results consumed by
-// epilogues (bias + ReLU, ReLU-mask, split-K partial slabs).  Split-K partials
-// are summed in slab order by a separate reduce kernel (deterministic), which
-// also routes weight/bias gradients (the bias gradient is the GEMM's extra
-// "ones" column) straight into the flat gradient buffer.
+// One templated tile kernel serves every product.  A block is always 4 waves;
+// they tile the output WM x WN (32x32 per wave) and split each K slice WK ways
+// (WM*WN*WK = 4), the WK partial accumulators being summed in wave order through
+// LDS at the end.  Operands come from loaders that produce 16-byte groups along
+// their contiguous dimension (implicit im2col with compile-time geometry, the
+// stride-1 transposed-conv gather, plain row/column-major), with a scalar path
+// only for ragged edges and unaligned leading dimensions.  Results go to
+// epilogues (bias + ReLU, ReLU-mask, plain store, weight/bias gradient -- the
+// bias gradient is the GEMM's extra "ones" column -- written straight into the
+// flat gradient buffer).  Split-K partial slabs are summed in slab order by a
+// reduce kernel (deterministic).  An in-launch last-arriver reduction (agent
+// release/acquire tickets) was measured no faster here: its fences cost what the
+// launch boundary does.
+//
+// The stride-2 conv2 input gradient is NOT an implicit GEMM over the 4x4 taps
+// (3/4 of those MACs would hit stride holes): it is the dense product
+// dcol = dy * W (pixels x (kh,kw,ci), K = 64) followed by an ordered col2im
+// gather that also applies the ReLU mask.
 //
 // Activations are NHWC fp32; weights live in the flat parameter buffer as
 // conv (out, kh, kw, in) and FC (out, in) -- the GEMM's natural [M][K] layouts.
@@ -20,14 +31,13 @@ namespace cnn {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int BK = 32;
-
 // ----------------------------------------------------------------- geometry
 template <int H_, int W_, int CI_, int KH_, int KW_, int S_, int PT_, int PL_, int OH_, int OW_, int CO_>
 struct Conv {
   static constexpr int H = H_, W = W_, CI = CI_, KH = KH_, KW = KW_, S = S_, PT = PT_, PL = PL_;
   static constexpr int OH = OH_, OW = OW_, CO = CO_;
   static constexpr int K = KH * KW * CI;     // im2col depth
+  static_assert(CI % 4 == 0 && CO % 4 == 0, "16-byte operand groups need CI, CO % 4 == 0");
 };
 // TF SAME: conv1 84 -> 21 (pad 2/2), conv2 21 -> 11 (pad 1/2), conv3 11 -> 11 (pad 1/1)
 using Conv1 = Conv<84, 84, 4, 8, 8, 4, 2, 2, 21, 21, 32>;
@@ -35,93 +45,114 @@ using Conv2 = Conv<21, 21, 32, 4, 4, 2, 1, 1, 11, 11, 64>;
 using Conv3 = Conv<11, 11, 64, 3, 3, 1, 1, 1, 11, 11, 64>;
 constexpr int kFlat = 11 * 11 * 64;   // 7744
 constexpr int kHidden = 512;
-// split-K factors (enough K-slices to put >= ~250 blocks on the 256 CUs)
-constexpr int kSplitFc1 = 16, kSplitFc2 = 8, kSplitConvW = 24, kSplitConv1W = 32;
+
+__device__ __forceinline__ float4 zero4() { return make_float4(0.0f, 0.0f, 0.0f, 0.0f); }
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
 // ------------------------------------------------------------------ loaders
-// A(m, k) / B(n, k) element producers.  kFast = true: consecutive threads walk k
-// (k contiguous in memory); false: they walk m / n.
+// get(r, k, rlim, klim): the 16-byte group of 4 consecutive operand elements
+// along the contiguous dimension (k when kFast, else r) at (r, k), zero outside
+// [0, rlim) x [0, klim) and in conv padding.  Branch-free by construction: the
+// address is clamped to a valid one, the load always issues and a select zeroes
+// it, so the loads of a whole K slice stay in flight together (a divergent
+// fallback branch would make the compiler drain vmcnt at every join).
+// Vector loaders need the ragged dimension to be a multiple of 4 (a group is
+// wholly in or out); the scalar ones (ld = n_out) pay 4 loads per group.
 
-// forward im2col of an NHWC input: rows = output pixels, k = (kh, kw, ci)
+__device__ __forceinline__ float4 sel4(bool ok, float4 v) { return ok ? v : zero4(); }
+
+// forward im2col of an NHWC input: rows = output pixels, k = (kh, kw, ci).
+// CI % 4 == 0, so a 16-byte group never straddles a (kh, kw) tap.
 template <class G>
 struct Im2col {
   static constexpr bool kFast = true;
   const float* x;
-  __device__ __forceinline__ float operator()(int m, int k) const {
+  __device__ __forceinline__ int offset(int m, int k) const {   // -1 in the padding
     const int b = m / (G::OH * G::OW), p = m - b * (G::OH * G::OW);
     const int oh = p / G::OW, ow = p - oh * G::OW;
     const int kk = k / G::CI, ci = k - kk * G::CI;
     const int kh = kk / G::KW, kw = kk - kh * G::KW;
     const int ih = oh * G::S - G::PT + kh, iw = ow * G::S - G::PL + kw;
-    if (ih < 0 || ih >= G::H || iw < 0 || iw >= G::W) return 0.0f;
-    return x[((b * G::H + ih) * G::W + iw) * G::CI + ci];
+    if (ih < 0 || ih >= G::H || iw < 0 || iw >= G::W) return -1;
+    return ((b * G::H + ih) * G::W + iw) * G::CI + ci;
+  }
+  __device__ __forceinline__ float4 get(int m, int k, int mlim, int klim) const {
+    const int o = offset(m, k);
+    const bool ok = m < mlim && k < klim && o >= 0;
+    return sel4(ok, ld4(x + (ok ? o : 0)));
   }
 };
 
 // im2col as the B operand of a weight gradient: rows k = pixels, cols n = (kh,kw,ci);
-// column n == G::K is the bias "ones" column.
+// column n == G::K is the bias "ones" column (K % 4 == 0: its group is (1, 0, 0, 0)).
 template <class G>
 struct Im2colT {
-  static constexpr bool kFast = false;   // n (ci innermost) contiguous
+  static constexpr bool kFast = false;
   const float* x;
-  __device__ __forceinline__ float operator()(int n, int k) const {
-    if (n == G::K) return 1.0f;
-    Im2col<G> f{x};
-    return f(k, n);
+  __device__ __forceinline__ float4 get(int n, int k, int, int klim) const {
+    const float4 v = Im2col<G>{x}.get(k, n, klim, G::K);
+    return (n == G::K && k < klim) ? make_float4(1.0f, 0.0f, 0.0f, 0.0f) : v;
   }
 };
 
-// gradient of a conv input (transposed conv): rows m = input pixels (b, ih, iw),
-// k = (kh, kw, co); dy is NHWC (B, OH, OW, CO).
+// stride-1 conv input gradient (transposed conv): rows m = input pixels, k = (kh, kw, co)
 template <class G>
 struct Col2im {
+  static_assert(G::S == 1, "strided input gradients go through dcol + col2im gather");
   static constexpr bool kFast = true;
   const float* dy;
-  __device__ __forceinline__ float operator()(int m, int k) const {
+  __device__ __forceinline__ float4 get(int m, int k, int mlim, int klim) const {
     const int b = m / (G::H * G::W), p = m - b * (G::H * G::W);
     const int ih = p / G::W, iw = p - ih * G::W;
     const int kk = k / G::CO, co = k - kk * G::CO;
     const int kh = kk / G::KW, kw = kk - kh * G::KW;
-    const int th = ih + G::PT - kh, tw = iw + G::PL - kw;   // = oh * S, ow * S
-    if (th < 0 || tw < 0) return 0.0f;
-    const int oh = th / G::S, ow = tw / G::S;
-    if (oh * G::S != th || ow * G::S != tw || oh >= G::OH || ow >= G::OW) return 0.0f;
-    return dy[((b * G::OH + oh) * G::OW + ow) * G::CO + co];
+    const int oh = ih + G::PT - kh, ow = iw + G::PL - kw;
+    const bool ok = m < mlim && k < klim && oh >= 0 && ow >= 0 && oh < G::OH && ow < G::OW;
+    return sel4(ok, ld4(dy + (ok ? ((b * G::OH + oh) * G::OW + ow) * G::CO + co : 0)));
   }
 };
 
 // conv weights as B of the transposed conv: B(n = ci, k = (kh, kw, co)) = W[co][kh][kw][ci]
 template <class G>
 struct WeightT {
-  static constexpr bool kFast = false;   // n = ci contiguous
+  static constexpr bool kFast = false;
   const float* w;
-  __device__ __forceinline__ float operator()(int n, int k) const {
+  __device__ __forceinline__ float4 get(int n, int k, int nlim, int klim) const {
     const int kk = k / G::CO, co = k - kk * G::CO;
-    return w[(co * (G::KH * G::KW) + kk) * G::CI + n];
+    const bool ok = n < nlim && k < klim;
+    return sel4(ok, ld4(w + (ok ? (co * (G::KH * G::KW) + kk) * G::CI + n : 0)));
   }
 };
 
-// plain row-major [rows][ld], k contiguous (x of an FC layer, weights [N][K])
+// plain row-major [rows][ld], k contiguous (x of an FC layer, weights [N][K]); ld % 4 == 0
 struct RowK {
   static constexpr bool kFast = true;
   const float* p;
   int ld;
-  __device__ __forceinline__ float operator()(int r, int k) const { return p[(int64_t)r * ld + k]; }
+  __device__ __forceinline__ float4 get(int r, int k, int rlim, int klim) const {
+    const bool ok = r < rlim && k < klim;
+    return sel4(ok, ld4(p + (ok ? (int64_t)r * ld + k : 0)));
+  }
 };
-// [k][rows] with rows contiguous: dy^T of FC dW (A), and W of FC dX as B(n = in, k = out)
+// [k][rows] with rows contiguous: dy^T of FC dW (A), W of FC dX as B(n = in, k = out); ld % 4 == 0
 struct ColK {
   static constexpr bool kFast = false;
   const float* p;
   int ld;
-  __device__ __forceinline__ float operator()(int r, int k) const { return p[(int64_t)k * ld + r]; }
+  __device__ __forceinline__ float4 get(int r, int k, int rlim, int klim) const {
+    const bool ok = r < rlim && k < klim;
+    return sel4(ok, ld4(p + (ok ? (int64_t)k * ld + r : 0)));
+  }
 };
 // FC dW's B operand: B(n, k = batch) = x[k][n], with the bias ones-column at n == ld
 struct ColKOnes {
   static constexpr bool kFast = false;
   const float* p;
   int ld;
-  __device__ __forceinline__ float operator()(int n, int k) const {
-    return n == ld ? 1.0f : p[(int64_t)k * ld + n];
+  __device__ __forceinline__ float4 get(int n, int k, int, int klim) const {
+    const bool ok = n < ld && k < klim;
+    const float4 v = sel4(ok, ld4(p + (ok ? (int64_t)k * ld + n : 0)));
+    return (n == ld && k < klim) ? make_float4(1.0f, 0.0f, 0.0f, 0.0f) : v;
   }
 };
 // conv dW's A operand: A(m = co, k = pixel) = dy[pixel][co]
@@ -129,7 +160,42 @@ template <int CO>
 struct DyT {
   static constexpr bool kFast = false;
   const float* dy;
-  __device__ __forceinline__ float operator()(int m, int k) const { return dy[(int64_t)k * CO + m]; }
+  __device__ __forceinline__ float4 get(int m, int k, int mlim, int klim) const {
+    const bool ok = m < mlim && k < klim;
+    return sel4(ok, ld4(dy + (ok ? (int64_t)k * CO + m : 0)));
+  }
+};
+// scalar forms of RowK / ColK for a leading dimension that is not a multiple of 4
+// (the n_out-wide output gradient): 4 clamped loads + selects per group
+struct RowKScalar {
+  static constexpr bool kFast = true;
+  const float* p;
+  int ld;
+  __device__ __forceinline__ float4 get(int r, int k, int rlim, int klim) const {
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool ok = r < rlim && k + j < klim;
+      const float x = p[ok ? (int64_t)r * ld + k + j : 0];
+      v[j] = ok ? x : 0.0f;
+    }
+    return make_float4(v[0], v[1], v[2], v[3]);
+  }
+};
+struct ColKScalar {
+  static constexpr bool kFast = false;
+  const float* p;
+  int ld;
+  __device__ __forceinline__ float4 get(int r, int k, int rlim, int klim) const {
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool ok = r + j < rlim && k < klim;
+      const float x = p[ok ? (int64_t)k * ld + r + j : 0];
+      v[j] = ok ? x : 0.0f;
+    }
+    return make_float4(v[0], v[1], v[2], v[3]);
+  }
 };
 
 // ---------------------------------------------------------------- epilogues
@@ -152,6 +218,13 @@ struct EpiMask {             // out[m][n] = acc * (act[m][n] > 0)   (ReLU backwa
     out[i] = act[i] > 0.0f ? v : 0.0f;
   }
 };
+struct EpiStore {            // out[m][n] = acc
+  float* out;
+  int ld;
+  __device__ __forceinline__ void operator()(int m, int n, float v, int) const {
+    out[(int64_t)m * ld + n] = v;
+  }
+};
 struct EpiPartial {          // split-K slab z
   float* ws;
   int M, N;
@@ -170,110 +243,271 @@ struct EpiGrad {             // n < nw: dW[m][n]; n == nw: db[m]
 };
 
 // ------------------------------------------------------------- tile kernel
-// Block = WM x WN waves, each owning a 32x32 output tile; K swept in BK = 32 slices
-// staged through LDS ([k][m] / [k][n], padded), next slice prefetched into
-// registers while the MFMAs of the current one run.  grid.z = split-K slices.
-template <int WM, int WN, class AL, class BL, class EP>
-__global__ __launch_bounds__(64 * WM * WN) void k_igemm(AL A, BL B, EP E, int M, int N, int K,
-                                                        int kchunk) {
-  constexpr int BM = 32 * WM, BN = 32 * WN, T = 64 * WM * WN;
-  constexpr int NA = BM * BK / T, NB = BN * BK / T;
-  __shared__ float As[BK][BM + 1];
-  __shared__ float Bs[BK][BN + 1];
+// 16-byte group g of an R x BKT operand slice -> (row rr, k offset kk).
+// kFast: 8 consecutive lanes cover 128 contiguous bytes of one row, then rows,
+// then the next 32-wide k band.  Otherwise lanes walk the rows 4 at a time.
+template <bool kFast, int R, int BKT>
+__device__ __forceinline__ void group_coord(int g, int& rr, int& kk) {
+  if (kFast) {
+    kk = 4 * ((g & 7) + 8 * (g / (8 * R)));
+    rr = (g >> 3) % R;
+  } else {
+    kk = g / (R / 4);
+    rr = 4 * (g % (R / 4));
+  }
+}
+
+// Block = WM x WN x WK waves.  The WM x WN output tiles are 32x32 (one MFMA
+// accumulator each); each K slice of BKT = 32*WK is split WK ways, one 32-wide
+// k band per wave, so a block with many waves covers a small GEMM's whole K in
+// one or two slices and keeps several waves per SIMD (address math of one wave
+// overlaps the MFMAs of another).  The next slice's operands are fetched into
+// registers while the MFMAs of the current one run.  The WK partial
+// accumulators are then summed through LDS by all threads, each output element
+// in wave order (deterministic), and handed to the epilogue with consecutive
+// threads on consecutive columns.
+template <int WM, int WN, int WK, class AL, class BL, class EP>
+__global__ __launch_bounds__(64 * WM * WN * WK) void k_igemm(AL A, BL B, EP E, int M, int N, int K,
+                                                             int kchunk) {
+  constexpr int T = 64 * WM * WN * WK;
+  constexpr int BM = 32 * WM, BN = 32 * WN, BKT = 32 * WK;
+  constexpr int SA = BM + (AL::kFast ? 1 : 4), SB = BN + (BL::kFast ? 1 : 4);
+  constexpr int NA = BM * BKT / 4 / T, NB = BN * BKT / 4 / T;
+  static_assert(NA >= 1 && NB >= 1 && NA * 4 * T == BM * BKT && NB * 4 * T == BN * BKT, "tile/threads");
+  constexpr int LDS = BKT * SA + BKT * SB;
+  constexpr int OUT = WM * WN * 1024;     // output elements per block
+  static_assert(WK * OUT <= LDS, "reduction scratch exceeds LDS tile");
+  __shared__ __attribute__((aligned(16))) float smem[LDS];
+  float* As = smem;
+  float* Bs = smem + BKT * SA;
+
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave % WM, wn = wave / WM;
+  const int wm = wave % WM, wn = (wave / WM) % WN, wk = wave / (WM * WN);
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
   const int kbeg = blockIdx.z * kchunk;
   const int kend = min(K, kbeg + kchunk);
-  float ra[NA], rb[NB];
+  float4 ra[NA], rb[NB];
 
   auto load = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-      const int e = i * T + tid;
-      int mm, kk;
-      if (AL::kFast) { mm = e / BK; kk = e - mm * BK; } else { kk = e / BM; mm = e - kk * BM; }
-      const int m = m0 + mm, k = k0 + kk;
-      ra[i] = (m < M && k < kend) ? A(m, k) : 0.0f;
+      int rr, kk;
+      group_coord<AL::kFast, BM, BKT>(i * T + tid, rr, kk);
+      ra[i] = A.get(m0 + rr, k0 + kk, M, kend);
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      const int e = i * T + tid;
-      int nn, kk;
-      if (BL::kFast) { nn = e / BK; kk = e - nn * BK; } else { kk = e / BN; nn = e - kk * BN; }
-      const int n = n0 + nn, k = k0 + kk;
-      rb[i] = (n < N && k < kend) ? B(n, k) : 0.0f;
+      int rr, kk;
+      group_coord<BL::kFast, BN, BKT>(i * T + tid, rr, kk);
+      rb[i] = B.get(n0 + rr, k0 + kk, N, kend);
+    }
+  };
+  auto put = [](float* S, int stride, bool kfast, int rr, int kk, float4 v) {
+    if (kfast) {
+      S[(kk + 0) * stride + rr] = v.x;
+      S[(kk + 1) * stride + rr] = v.y;
+      S[(kk + 2) * stride + rr] = v.z;
+      S[(kk + 3) * stride + rr] = v.w;
+    } else {
+      *reinterpret_cast<float4*>(S + kk * stride + rr) = v;
     }
   };
   auto stash = [&]() {
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-      const int e = i * T + tid;
-      int mm, kk;
-      if (AL::kFast) { mm = e / BK; kk = e - mm * BK; } else { kk = e / BM; mm = e - kk * BM; }
-      As[kk][mm] = ra[i];
+      int rr, kk;
+      group_coord<AL::kFast, BM, BKT>(i * T + tid, rr, kk);
+      put(As, SA, AL::kFast, rr, kk, ra[i]);
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      const int e = i * T + tid;
-      int nn, kk;
-      if (BL::kFast) { nn = e / BK; kk = e - nn * BK; } else { kk = e / BN; nn = e - kk * BN; }
-      Bs[kk][nn] = rb[i];
+      int rr, kk;
+      group_coord<BL::kFast, BN, BKT>(i * T + tid, rr, kk);
+      put(Bs, SB, BL::kFast, rr, kk, rb[i]);
     }
   };
 
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-  if (kbeg < kend) load(kbeg);
-  for (int k0 = kbeg; k0 < kend; k0 += BK) {
+  load(kbeg);
+  const float* pa = As + (wk * 32 + (lane >> 5)) * SA + wm * 32 + (lane & 31);
+  const float* pb = Bs + (wk * 32 + (lane >> 5)) * SB + wn * 32 + (lane & 31);
+  for (int k0 = kbeg; k0 < kend; k0 += BKT) {
     stash();
     __syncthreads();
-    if (k0 + BK < kend) load(k0 + BK);
-    const int ar = wm * 32 + (lane & 31), bc = wn * 32 + (lane & 31), kh = lane >> 5;
+    if (k0 + BKT < kend) load(k0 + BKT);
+    if (k0 + wk * 32 < kend) {              // wave-uniform: bands past the end are all zero
 #pragma unroll
-    for (int s = 0; s < BK; s += 2)
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[s + kh][ar], Bs[s + kh][bc], acc, 0, 0, 0);
+      for (int s = 0; s < 32; s += 2)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(pa[s * SA], pb[s * SB], acc, 0, 0, 0);
+    }
     __syncthreads();
   }
-  // C/D layout of the 32x32 f32 MFMA: col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5)
+  // partials -> LDS [wk][tile][r][lane]; C/D layout of the 32x32 f32 MFMA:
+  // col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5)
+  {
+    float* red = smem + (wk * WM * WN + wm + WM * wn) * 1024 + lane;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-    const int n = n0 + wn * 32 + (lane & 31);
-    if (m < M && n < N) E(m, n, acc[r], blockIdx.z);
+    for (int r = 0; r < 16; ++r) red[r * 64] = acc[r];
+  }
+  __syncthreads();
+  for (int e = tid; e < OUT; e += T) {
+    float v = smem[e];
+#pragma unroll
+    for (int j = 1; j < WK; ++j) v = __fadd_rn(v, smem[j * OUT + e]);
+    const int tile = e >> 10, r = (e >> 6) & 15, l = e & 63;
+    const int m = m0 + (tile % WM) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
+    const int n = n0 + (tile / WM) * 32 + (l & 31);
+    if (m < M && n < N) E(m, n, v, blockIdx.z);
   }
 }
 
-// ordered split-K sum + epilogue
+// ordered split-K sum + epilogue; the slab loads of a thread are all in flight together
 template <class EP>
 __global__ __launch_bounds__(256) void k_splitk_reduce(const float* ws, int splits, int M, int N, EP E) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (int64_t)M * N) return;
+  const int64_t MN = (int64_t)M * N;
   float s = ws[i];
-  for (int z = 1; z < splits; ++z) s = __fadd_rn(s, ws[(int64_t)z * M * N + i]);
+  for (int z0 = 1; z0 < splits; z0 += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = ws[(int64_t)min(z0 + u, splits - 1) * MN + i];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s = z0 + u < splits ? __fadd_rn(s, v[u]) : s;
+  }
   E((int)(i / N), (int)(i % N), s, 0);
 }
 
-// K slice per split (multiple of BK) and the resulting number of slabs
-inline int split_chunk(int K, int splits) { return ((K + splits - 1) / splits + BK - 1) / BK * BK; }
-inline int split_count(int K, int splits) { const int c = split_chunk(K, splits); return (K + c - 1) / c; }
+// strided conv input gradient from dcol[(b, oh, ow)][(kh, kw, ci)]:
+// dx[b][ih][iw][ci] = (act > 0) * sum over the taps that land on (ih, iw), in (kh, kw) order
+template <class G>
+__global__ __launch_bounds__(256) void k_col2im(const float* dcol, const float* act, float* dx,
+                                                int total4) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= total4) return;
+  constexpr int C4 = G::CI / 4;
+  const int ci = (i % C4) * 4, pix = i / C4;
+  const int b = pix / (G::H * G::W), p = pix - b * (G::H * G::W);
+  const int ih = p / G::W, iw = p - ih * G::W;
+  float4 s = zero4();
+  for (int kh = (ih + G::PT) % G::S; kh < G::KH; kh += G::S) {
+    const int th = ih + G::PT - kh;
+    if (th < 0) break;
+    const int oh = th / G::S;
+    if (oh >= G::OH) continue;
+    for (int kw = (iw + G::PL) % G::S; kw < G::KW; kw += G::S) {
+      const int tw = iw + G::PL - kw;
+      if (tw < 0) break;
+      const int ow = tw / G::S;
+      if (ow >= G::OW) continue;
+      const float4 v = ld4(dcol + ((b * G::OH + oh) * G::OW + ow) * G::K + (kh * G::KW + kw) * G::CI + ci);
+      s.x = __fadd_rn(s.x, v.x);
+      s.y = __fadd_rn(s.y, v.y);
+      s.z = __fadd_rn(s.z, v.z);
+      s.w = __fadd_rn(s.w, v.w);
+    }
+  }
+  const float4 a = ld4(act + (int64_t)i * 4);
+  float4 o;
+  o.x = a.x > 0.0f ? s.x : 0.0f;
+  o.y = a.y > 0.0f ? s.y : 0.0f;
+  o.z = a.z > 0.0f ? s.z : 0.0f;
+  o.w = a.w > 0.0f ? s.w : 0.0f;
+  *reinterpret_cast<float4*>(dx + (int64_t)i * 4) = o;
+}
 
-template <int WM, int WN, class AL, class BL, class EP>
-void launch(AL a, BL b, EP e, int M, int N, int K, int splits, float* ws, hipStream_t s) {
+// Launch context: a dry run only sizes the workspace, so the two can never disagree.
+struct Ctx {
+  hipStream_t s;
+  float* ws;       // split-K slabs / conv2 dcol
+  bool dry;
+  size_t need;
+};
+
+// K slice per split (multiple of the block's K slice)
+inline int split_chunk(int K, int splits, int bkt) {
+  return ((K + splits - 1) / splits + bkt - 1) / bkt * bkt;
+}
+
+template <int WM, int WN, int WK, class AL, class BL, class EP>
+void gemm(Ctx& c, AL a, BL b, EP e, int M, int N, int K, int splits = 1) {
+  constexpr int BKT = 32 * WK, T = 64 * WM * WN * WK;
   const unsigned gx = (M + 32 * WM - 1) / (32 * WM), gy = (N + 32 * WN - 1) / (32 * WN);
-  if (splits == 1) {
-    hipLaunchKernelGGL((k_igemm<WM, WN, AL, BL, EP>), dim3(gx, gy, 1), dim3(64 * WM * WN), 0, s, a,
-                       b, e, M, N, K, K);
+  const int kchunk = splits > 1 ? split_chunk(K, splits, BKT) : K;
+  const int nz = splits > 1 ? (K + kchunk - 1) / kchunk : 1;
+  if (nz > 1) {
+    const size_t need = (size_t)nz * M * N;
+    c.need = need > c.need ? need : c.need;
+  }
+  if (c.dry) return;
+  if (nz == 1) {
+    hipLaunchKernelGGL((k_igemm<WM, WN, WK, AL, BL, EP>), dim3(gx, gy, 1), dim3(T), 0, c.s, a, b, e,
+                       M, N, K, K);
     return;
   }
-  const int kchunk = split_chunk(K, splits), nz = split_count(K, splits);
-  EpiPartial p{ws, M, N};
-  hipLaunchKernelGGL((k_igemm<WM, WN, AL, BL, EpiPartial>), dim3(gx, gy, nz), dim3(64 * WM * WN), 0,
-                     s, a, b, p, M, N, K, kchunk);
+  hipLaunchKernelGGL((k_igemm<WM, WN, WK, AL, BL, EpiPartial>), dim3(gx, gy, nz), dim3(T), 0, c.s, a,
+                     b, EpiPartial{c.ws, M, N}, M, N, K, kchunk);
   const int64_t total = (int64_t)M * N;
-  hipLaunchKernelGGL((k_splitk_reduce<EP>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
-                     ws, nz, M, N, e);
+  hipLaunchKernelGGL((k_splitk_reduce<EP>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     c.s, c.ws, nz, M, N, e);
+}
+
+// Tile shapes: WM = WN = 1 with WK k-bands sized so K takes one or two slices
+// (BKT = 32 * WK); split-K only where the grid would otherwise leave most of the
+// 256 CUs idle (weight streaming of fc1, the pixel-deep weight gradients).
+constexpr int kSplitFc1 = 16, kSplitConvW = 8, kSplitConv1W = 28;
+
+void forward(Ctx& c, const dq_cnn_params* p, int B, const float* x, dq_cnn_acts* a) {
+  // conv1 / conv2 / conv3 + bias + ReLU  (implicit GEMM: M = pixels, N = out channels)
+  gemm<1, 1, 8>(c, Im2col<Conv1>{x}, RowK{p->conv1_w, Conv1::K},
+                EpiBiasAct{a->a1, p->conv1_b, 32, true}, B * 441, 32, Conv1::K);
+  gemm<1, 1, 16>(c, Im2col<Conv2>{a->a1}, RowK{p->conv2_w, Conv2::K},
+                 EpiBiasAct{a->a2, p->conv2_b, 64, true}, B * 121, 64, Conv2::K);
+  gemm<1, 1, 9>(c, Im2col<Conv3>{a->a2}, RowK{p->conv3_w, Conv3::K},
+                EpiBiasAct{a->a3, p->conv3_b, 64, true}, B * 121, 64, Conv3::K);
+  // fc1 (7744 -> 512) + ReLU: weight streaming, split-K over the 7744 inputs
+  gemm<1, 1, 16>(c, RowK{a->a3, kFlat}, RowK{p->fc1_w, kFlat},
+                 EpiBiasAct{a->h, p->fc1_b, kHidden, true}, B, kHidden, kFlat, kSplitFc1);
+  // fc2 (512 -> n_out), no activation
+  gemm<1, 1, 16>(c, RowK{a->h, kHidden}, RowK{p->fc2_w, kHidden},
+                 EpiBiasAct{a->out, p->fc2_b, p->n_out, false}, B, p->n_out, kHidden);
+}
+
+void backward(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int B, const float* x,
+              const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d) {
+  const int NO = p->n_out;
+  // fc2: dW2|db2 = dout^T [h | 1];  dh = (dout W2) * (h > 0)
+  gemm<2, 2, 1>(c, ColKScalar{dout, NO}, ColKOnes{a->h, kHidden},
+                EpiGrad{g->fc2_w, g->fc2_b, kHidden}, NO, kHidden + 1, B);
+  gemm<1, 1, 16>(c, RowKScalar{dout, NO}, ColK{p->fc2_w, kHidden}, EpiMask{d->h, a->h, kHidden},
+                 B, kHidden, NO);
+  // fc1: dW1|db1 = dh^T [a3 | 1];  da3 = (dh W1) * (a3 > 0)
+  gemm<2, 2, 1>(c, ColK{d->h, kHidden}, ColKOnes{a->a3, kFlat}, EpiGrad{g->fc1_w, g->fc1_b, kFlat},
+                kHidden, kFlat + 1, B);
+  gemm<1, 1, 16>(c, RowK{d->h, kHidden}, ColK{p->fc1_w, kFlat}, EpiMask{d->a3, a->a3, kFlat},
+                 B, kFlat, kHidden);
+  // conv3: dW3|db3 = da3^T [im2col(a2) | 1];  da2 = col2im(da3, W3) * (a2 > 0)
+  gemm<1, 1, 16>(c, DyT<64>{d->a3}, Im2colT<Conv3>{a->a2},
+                 EpiGrad{g->conv3_w, g->conv3_b, Conv3::K}, 64, Conv3::K + 1, B * 121, kSplitConvW);
+  gemm<1, 1, 9>(c, Col2im<Conv3>{d->a3}, WeightT<Conv3>{p->conv3_w}, EpiMask{d->a2, a->a2, 64},
+                B * 121, 64, 9 * 64);
+  // conv2: dW2|db2 = da2^T [im2col(a1) | 1];  da1 = col2im(da2 W2) * (a1 > 0)
+  gemm<1, 1, 16>(c, DyT<64>{d->a2}, Im2colT<Conv2>{a->a1},
+                 EpiGrad{g->conv2_w, g->conv2_b, Conv2::K}, 64, Conv2::K + 1, B * 121, kSplitConvW);
+  const size_t dcol = (size_t)B * 121 * Conv2::K;
+  c.need = dcol > c.need ? dcol : c.need;
+  gemm<1, 1, 2>(c, RowK{d->a2, 64}, ColK{p->conv2_w, Conv2::K}, EpiStore{c.ws, Conv2::K},
+                B * 121, Conv2::K, 64);
+  if (!c.dry) {
+    const int total4 = B * 441 * 32 / 4;
+    hipLaunchKernelGGL((k_col2im<Conv2>), dim3((total4 + 255) / 256), dim3(256), 0, c.s, c.ws,
+                       a->a1, d->a1, total4);
+  }
+  // conv1: dW1|db1 = da1^T [im2col(x) | 1]   (no input gradient needed)
+  gemm<1, 1, 16>(c, DyT<32>{d->a1}, Im2colT<Conv1>{x}, EpiGrad{g->conv1_w, g->conv1_b, Conv1::K},
+                 32, Conv1::K + 1, B * 441, kSplitConv1W);
 }
 
 }  // namespace cnn
@@ -288,21 +522,8 @@ int dq_cnn_forward(const dq_cnn_params* p, int32_t batch, const float* x, dq_cnn
                    float* ws, void* stream) {
   DQ_CHECK_ARG(p && a && x && ws && batch >= 1, "null argument");
   DQ_CHECK_ARG(p->in_channels == 4 && p->n_out >= 1, "the Nature CNN takes 84x84x4 NHWC input");
-  hipStream_t s = (hipStream_t)stream;
-  const int B = batch;
-  // conv1 / conv2 / conv3 + bias + ReLU  (implicit GEMM: M = pixels, N = out channels)
-  launch<1, 1>(Im2col<Conv1>{x}, RowK{p->conv1_w, Conv1::K}, EpiBiasAct{a->a1, p->conv1_b, 32, true},
-               B * 441, 32, Conv1::K, 1, ws, s);
-  launch<1, 1>(Im2col<Conv2>{a->a1}, RowK{p->conv2_w, Conv2::K}, EpiBiasAct{a->a2, p->conv2_b, 64, true},
-               B * 121, 64, Conv2::K, 1, ws, s);
-  launch<1, 1>(Im2col<Conv3>{a->a2}, RowK{p->conv3_w, Conv3::K}, EpiBiasAct{a->a3, p->conv3_b, 64, true},
-               B * 121, 64, Conv3::K, 1, ws, s);
-  // fc1 (7744 -> 512) + ReLU: weight-streaming, split-K over the 7744 inputs
-  launch<1, 1>(RowK{a->a3, kFlat}, RowK{p->fc1_w, kFlat}, EpiBiasAct{a->h, p->fc1_b, kHidden, true},
-               B, kHidden, kFlat, kSplitFc1, ws, s);
-  // fc2 (512 -> n_out), no activation
-  launch<1, 1>(RowK{a->h, kHidden}, RowK{p->fc2_w, kHidden}, EpiBiasAct{a->out, p->fc2_b, p->n_out, false},
-               B, p->n_out, kHidden, kSplitFc2, ws, s);
+  Ctx c{(hipStream_t)stream, ws, false, 0};
+  forward(c, p, batch, x, a);
   DQ_CHECK_LAUNCH("dq_cnn_forward");
   return DQ_OK;
 }
@@ -311,49 +532,22 @@ int dq_cnn_backward(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batc
                     const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d, float* ws,
                     void* stream) {
   DQ_CHECK_ARG(p && g && a && d && x && dout && ws && batch >= 1, "null argument");
-  hipStream_t s = (hipStream_t)stream;
-  const int B = batch, NO = p->n_out;
-  // fc2: dW2|db2 = dout^T [h | 1];  dh = (dout W2) * (h > 0)
-  launch<2, 2>(ColK{dout, NO}, ColKOnes{a->h, kHidden}, EpiGrad{g->fc2_w, g->fc2_b, kHidden},
-               NO, kHidden + 1, B, 1, ws, s);
-  launch<1, 1>(RowK{dout, NO}, ColK{p->fc2_w, kHidden}, EpiMask{d->h, a->h, kHidden},
-               B, kHidden, NO, kSplitFc2, ws, s);
-  // fc1: dW1|db1 = dh^T [a3 | 1];  da3 = (dh W1) * (a3 > 0)
-  launch<2, 2>(ColK{d->h, kHidden}, ColKOnes{a->a3, kFlat}, EpiGrad{g->fc1_w, g->fc1_b, kFlat},
-               kHidden, kFlat + 1, B, 1, ws, s);
-  launch<1, 1>(RowK{d->h, kHidden}, ColK{p->fc1_w, kFlat}, EpiMask{d->a3, a->a3, kFlat},
-               B, kFlat, kHidden, 1, ws, s);
-  // conv3: dW3|db3 = da3^T [im2col(a2) | 1];  da2 = col2im(da3, W3) * (a2 > 0)
-  launch<2, 2>(DyT<64>{d->a3}, Im2colT<Conv3>{a->a2}, EpiGrad{g->conv3_w, g->conv3_b, Conv3::K},
-               64, Conv3::K + 1, B * 121, kSplitConvW, ws, s);
-  launch<1, 1>(Col2im<Conv3>{d->a3}, WeightT<Conv3>{p->conv3_w}, EpiMask{d->a2, a->a2, 64},
-               B * 121, 64, 9 * 64, 1, ws, s);
-  // conv2: dW2|db2 = da2^T [im2col(a1) | 1];  da1 = col2im(da2, W2) * (a1 > 0)
-  launch<2, 2>(DyT<64>{d->a2}, Im2colT<Conv2>{a->a1}, EpiGrad{g->conv2_w, g->conv2_b, Conv2::K},
-               64, Conv2::K + 1, B * 121, kSplitConvW, ws, s);
-  launch<1, 1>(Col2im<Conv2>{d->a2}, WeightT<Conv2>{p->conv2_w}, EpiMask{d->a1, a->a1, 32},
-               B * 441, 32, 16 * 64, 1, ws, s);
-  // conv1: dW1|db1 = da1^T [im2col(x) | 1]   (no input gradient needed)
-  launch<1, 1>(DyT<32>{d->a1}, Im2colT<Conv1>{x}, EpiGrad{g->conv1_w, g->conv1_b, Conv1::K},
-               32, Conv1::K + 1, B * 441, kSplitConv1W, ws, s);
+  DQ_CHECK_ARG(p->in_channels == 4 && p->n_out >= 1, "the Nature CNN takes 84x84x4 NHWC input");
+  Ctx c{(hipStream_t)stream, ws, false, 0};
+  backward(c, p, g, batch, x, a, dout, d);
   DQ_CHECK_LAUNCH("dq_cnn_backward");
   return DQ_OK;
 }
 
 size_t dq_cnn_workspace_floats(int32_t batch, int32_t n_out) {
-  // largest split-K slab set among the launches above
-  size_t m = 0;
-  auto upd = [&](int K, int splits, size_t MN) {
-    const size_t v = (size_t)split_count(K, splits) * MN;
-    m = v > m ? v : m;
-  };
-  upd(kFlat, kSplitFc1, (size_t)batch * kHidden);
-  upd(kHidden, kSplitFc2, (size_t)batch * n_out);
-  upd(n_out, kSplitFc2, (size_t)batch * kHidden);
-  upd(batch * 121, kSplitConvW, (size_t)64 * (Conv3::K + 1));
-  upd(batch * 121, kSplitConvW, (size_t)64 * (Conv2::K + 1));
-  upd(batch * 441, kSplitConv1W, (size_t)32 * (Conv1::K + 1));
-  return m;
+  dq_cnn_params p = {};
+  dq_cnn_acts a = {};
+  p.in_channels = 4;
+  p.n_out = n_out;
+  Ctx c{nullptr, nullptr, true, 0};
+  forward(c, &p, batch, nullptr, &a);
+  backward(c, &p, &p, batch, nullptr, &a, nullptr, &a);
+  return c.need;
 }
 
 }  // extern "C"

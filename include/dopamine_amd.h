@@ -213,7 +213,8 @@ typedef struct dq_cnn_acts {      /* per-call activations (or their gradients) *
   float* h;                       /* (B, 512) */
   float* out;                     /* (B, n_out) */
 } dq_cnn_acts;
-/* forward: relu(conv1..3), relu(fc1), fc2 -> a->out.  ws: dq_cnn_workspace_floats() floats. */
+/* forward: relu(conv1..3), relu(fc1), fc2 -> a->out.  ws: dq_cnn_workspace_floats() floats
+   (split-K slabs); one ws per stream that runs the network concurrently. */
 int dq_cnn_forward(const dq_cnn_params* p, int32_t batch, const float* x, dq_cnn_acts* a,
                    float* ws, void* stream);
 /* backward from d out (B, n_out): writes EVERY weight/bias gradient into g (plain stores,
