@@ -88,6 +88,9 @@ SIGNATURES = {
     'dq_cnn_forward': [ctypes.POINTER(CnnParams), _I32, _P, ctypes.POINTER(CnnActs), _P, _P],
     'dq_cnn_backward': [ctypes.POINTER(CnnParams), ctypes.POINTER(CnnParams), _I32, _P,
                         ctypes.POINTER(CnnActs), _P, ctypes.POINTER(CnnActs), _P, _P],
+    'dq_cnn_backward_layer': [ctypes.POINTER(CnnParams), ctypes.POINTER(CnnParams), _I32, _P,
+                              ctypes.POINTER(CnnActs), _P, ctypes.POINTER(CnnActs), _P, _I32, _I32,
+                              _P],
     'dq_cnn_workspace_floats': [_I32, _I32],
 }
 RESTYPES = {'dq_last_error': ctypes.c_char_p, 'dq_cnn_workspace_floats': ctypes.c_size_t}

@@ -48,7 +48,11 @@ class HipNatureCNN(object):
                      out=mk(B, self.n_out))
     self.dacts = dict(a1=mk(B, 21, 21, 32), a2=mk(B, 11, 11, 64), a3=mk(B, 7744), h=mk(B, 512),
                       out=mk(1))
-    self.ws = mk(int(_lib.lib.dq_cnn_workspace_floats(B, self.n_out)) + 64)
+    nws = int(_lib.lib.dq_cnn_workspace_floats(B, self.n_out)) + 64
+    self.ws = mk(nws)
+    self.ws_dw = mk(nws)       # split-K slabs of the weight gradients on the second stream
+    self._dw_stream = None
+    self._events = None
     self._p = _params_struct(fp, fp.flat, self.n_out, self.in_ch)
     self._g = _params_struct(fp, fp.grad, self.n_out, self.in_ch)
     self._a = CnnActs(**{k: v.data_ptr() for k, v in self.acts.items()})
@@ -71,13 +75,45 @@ class HipNatureCNN(object):
                'dq_cnn_forward')
     return self.acts['out']
 
-  def backward(self, dout):
-    """dout: (B, n_out).  Writes all parameter gradients into net.fp.grad."""
+  def backward(self, dout, parallel=False):
+    """dout: (B, n_out).  Writes all parameter gradients into net.fp.grad.
+
+    parallel: the weight gradients run on a second stream, each forked after
+    the input gradient it needs and joined before returning (stream-ordered,
+    HIP-graph capturable).  Measured SLOWER on MI355X inside a graph (141.6 vs
+    95.9 us per backward, tools/bench_hipcnn.py): the cross-queue edges cost
+    more than the overlap buys, and the 135-147 KB-LDS blocks cannot share a CU
+    with the other stream's.  Kept for experimentation; off by default."""
     dout = dout.reshape(self.B, self.n_out)
     assert dout.is_contiguous() and self._x is not None
-    _lib.check(_lib.lib.dq_cnn_backward(ctypes.byref(self._p), ctypes.byref(self._g), self.B,
-                                        self._x.data_ptr(), ctypes.byref(self._a),
-                                        dout.data_ptr(), ctypes.byref(self._d),
-                                        self.ws.data_ptr(), self._stream(dout)),
-               'dq_cnn_backward')
+    if not parallel:
+      _lib.check(_lib.lib.dq_cnn_backward(ctypes.byref(self._p), ctypes.byref(self._g), self.B,
+                                          self._x.data_ptr(), ctypes.byref(self._a),
+                                          dout.data_ptr(), ctypes.byref(self._d),
+                                          self.ws.data_ptr(), self._stream(dout)),
+                 'dq_cnn_backward')
+      return self.net.fp.grad
+    main = torch.cuda.current_stream(dout.device)
+    if self._dw_stream is None:
+      self._dw_stream = torch.cuda.Stream(dout.device)
+      self._events = [torch.cuda.Event() for _ in range(5)]
+    side, ev = self._dw_stream, self._events
+
+    def layer(i, part, stream, ws):
+      _lib.check(_lib.lib.dq_cnn_backward_layer(
+          ctypes.byref(self._p), ctypes.byref(self._g), self.B, self._x.data_ptr(),
+          ctypes.byref(self._a), dout.data_ptr(), ctypes.byref(self._d), ws.data_ptr(), i, part,
+          ctypes.c_void_p(stream.cuda_stream)), 'dq_cnn_backward_layer')
+
+    # ev[i] marks "input gradient of layer i-1 done" (ev[0]: dout ready)
+    ev[0].record(main)
+    for i in range(4):                     # fc2, fc1, conv3, conv2
+      side.wait_event(ev[i])
+      layer(i, 1, side, self.ws_dw)
+      layer(i, 0, main, self.ws)
+      if i < 3:
+        ev[i + 1].record(main)
+    layer(4, 1, main, self.ws)             # conv1 weight gradient: last on the chain
+    ev[4].record(side)
+    main.wait_event(ev[4])
     return self.net.fp.grad

@@ -475,39 +475,68 @@ void forward(Ctx& c, const dq_cnn_params* p, int B, const float* x, dq_cnn_acts*
                  EpiBiasAct{a->out, p->fc2_b, p->n_out, false}, B, p->n_out, kHidden);
 }
 
+// Backward of one layer: part 1 = weight/bias gradient, part 0 = input gradient.
+// Layers 0..4 = fc2, fc1, conv3, conv2, conv1 (conv1 has no input gradient).
+// dW(L) needs only dX(L-1)'s output, so the two parts can run on two streams.
+bool backward_layer(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int B, const float* x,
+                    const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d, int layer, int part) {
+  const int NO = p->n_out;
+  switch (layer * 2 + part) {
+    case 0 * 2 + 1:   // fc2: dW2|db2 = dout^T [h | 1]
+      gemm<2, 2, 1>(c, ColKScalar{dout, NO}, ColKOnes{a->h, kHidden},
+                    EpiGrad{g->fc2_w, g->fc2_b, kHidden}, NO, kHidden + 1, B);
+      return true;
+    case 0 * 2 + 0:   // dh = (dout W2) * (h > 0)
+      gemm<1, 1, 16>(c, RowKScalar{dout, NO}, ColK{p->fc2_w, kHidden}, EpiMask{d->h, a->h, kHidden},
+                     B, kHidden, NO);
+      return true;
+    case 1 * 2 + 1:   // fc1: dW1|db1 = dh^T [a3 | 1]
+      gemm<2, 2, 1>(c, ColK{d->h, kHidden}, ColKOnes{a->a3, kFlat},
+                    EpiGrad{g->fc1_w, g->fc1_b, kFlat}, kHidden, kFlat + 1, B);
+      return true;
+    case 1 * 2 + 0:   // da3 = (dh W1) * (a3 > 0)
+      gemm<1, 1, 16>(c, RowK{d->h, kHidden}, ColK{p->fc1_w, kFlat}, EpiMask{d->a3, a->a3, kFlat},
+                     B, kFlat, kHidden);
+      return true;
+    case 2 * 2 + 1:   // conv3: dW3|db3 = da3^T [im2col(a2) | 1]
+      gemm<1, 1, 16>(c, DyT<64>{d->a3}, Im2colT<Conv3>{a->a2},
+                     EpiGrad{g->conv3_w, g->conv3_b, Conv3::K}, 64, Conv3::K + 1, B * 121, kSplitConvW);
+      return true;
+    case 2 * 2 + 0:   // da2 = col2im(da3, W3) * (a2 > 0)
+      gemm<1, 1, 9>(c, Col2im<Conv3>{d->a3}, WeightT<Conv3>{p->conv3_w}, EpiMask{d->a2, a->a2, 64},
+                    B * 121, 64, 9 * 64);
+      return true;
+    case 3 * 2 + 1:   // conv2: dW2|db2 = da2^T [im2col(a1) | 1]
+      gemm<1, 1, 16>(c, DyT<64>{d->a2}, Im2colT<Conv2>{a->a1},
+                     EpiGrad{g->conv2_w, g->conv2_b, Conv2::K}, 64, Conv2::K + 1, B * 121, kSplitConvW);
+      return true;
+    case 3 * 2 + 0: {  // da1 = col2im(da2 W2) * (a1 > 0)
+      const size_t dcol = (size_t)B * 121 * Conv2::K;
+      c.need = dcol > c.need ? dcol : c.need;
+      gemm<1, 1, 2>(c, RowK{d->a2, 64}, ColK{p->conv2_w, Conv2::K}, EpiStore{c.ws, Conv2::K},
+                    B * 121, Conv2::K, 64);
+      if (!c.dry) {
+        const int total4 = B * 441 * 32 / 4;
+        hipLaunchKernelGGL((k_col2im<Conv2>), dim3((total4 + 255) / 256), dim3(256), 0, c.s, c.ws,
+                           a->a1, d->a1, total4);
+      }
+      return true;
+    }
+    case 4 * 2 + 1:   // conv1: dW1|db1 = da1^T [im2col(x) | 1]   (no input gradient needed)
+      gemm<1, 1, 16>(c, DyT<32>{d->a1}, Im2colT<Conv1>{x}, EpiGrad{g->conv1_w, g->conv1_b, Conv1::K},
+                     32, Conv1::K + 1, B * 441, kSplitConv1W);
+      return true;
+    default:
+      return false;
+  }
+}
+
 void backward(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int B, const float* x,
               const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d) {
-  const int NO = p->n_out;
-  // fc2: dW2|db2 = dout^T [h | 1];  dh = (dout W2) * (h > 0)
-  gemm<2, 2, 1>(c, ColKScalar{dout, NO}, ColKOnes{a->h, kHidden},
-                EpiGrad{g->fc2_w, g->fc2_b, kHidden}, NO, kHidden + 1, B);
-  gemm<1, 1, 16>(c, RowKScalar{dout, NO}, ColK{p->fc2_w, kHidden}, EpiMask{d->h, a->h, kHidden},
-                 B, kHidden, NO);
-  // fc1: dW1|db1 = dh^T [a3 | 1];  da3 = (dh W1) * (a3 > 0)
-  gemm<2, 2, 1>(c, ColK{d->h, kHidden}, ColKOnes{a->a3, kFlat}, EpiGrad{g->fc1_w, g->fc1_b, kFlat},
-                kHidden, kFlat + 1, B);
-  gemm<1, 1, 16>(c, RowK{d->h, kHidden}, ColK{p->fc1_w, kFlat}, EpiMask{d->a3, a->a3, kFlat},
-                 B, kFlat, kHidden);
-  // conv3: dW3|db3 = da3^T [im2col(a2) | 1];  da2 = col2im(da3, W3) * (a2 > 0)
-  gemm<1, 1, 16>(c, DyT<64>{d->a3}, Im2colT<Conv3>{a->a2},
-                 EpiGrad{g->conv3_w, g->conv3_b, Conv3::K}, 64, Conv3::K + 1, B * 121, kSplitConvW);
-  gemm<1, 1, 9>(c, Col2im<Conv3>{d->a3}, WeightT<Conv3>{p->conv3_w}, EpiMask{d->a2, a->a2, 64},
-                B * 121, 64, 9 * 64);
-  // conv2: dW2|db2 = da2^T [im2col(a1) | 1];  da1 = col2im(da2 W2) * (a1 > 0)
-  gemm<1, 1, 16>(c, DyT<64>{d->a2}, Im2colT<Conv2>{a->a1},
-                 EpiGrad{g->conv2_w, g->conv2_b, Conv2::K}, 64, Conv2::K + 1, B * 121, kSplitConvW);
-  const size_t dcol = (size_t)B * 121 * Conv2::K;
-  c.need = dcol > c.need ? dcol : c.need;
-  gemm<1, 1, 2>(c, RowK{d->a2, 64}, ColK{p->conv2_w, Conv2::K}, EpiStore{c.ws, Conv2::K},
-                B * 121, Conv2::K, 64);
-  if (!c.dry) {
-    const int total4 = B * 441 * 32 / 4;
-    hipLaunchKernelGGL((k_col2im<Conv2>), dim3((total4 + 255) / 256), dim3(256), 0, c.s, c.ws,
-                       a->a1, d->a1, total4);
+  for (int layer = 0; layer < 5; ++layer) {
+    backward_layer(c, p, g, B, x, a, dout, d, layer, 1);
+    backward_layer(c, p, g, B, x, a, dout, d, layer, 0);
   }
-  // conv1: dW1|db1 = da1^T [im2col(x) | 1]   (no input gradient needed)
-  gemm<1, 1, 16>(c, DyT<32>{d->a1}, Im2colT<Conv1>{x}, EpiGrad{g->conv1_w, g->conv1_b, Conv1::K},
-                 32, Conv1::K + 1, B * 441, kSplitConv1W);
 }
 
 }  // namespace cnn
@@ -536,6 +565,19 @@ int dq_cnn_backward(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batc
   Ctx c{(hipStream_t)stream, ws, false, 0};
   backward(c, p, g, batch, x, a, dout, d);
   DQ_CHECK_LAUNCH("dq_cnn_backward");
+  return DQ_OK;
+}
+
+int dq_cnn_backward_layer(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch,
+                          const float* x, const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d,
+                          float* ws, int32_t layer, int32_t part, void* stream) {
+  DQ_CHECK_ARG(p && g && a && d && x && dout && ws && batch >= 1, "null argument");
+  DQ_CHECK_ARG(p->in_channels == 4 && p->n_out >= 1, "the Nature CNN takes 84x84x4 NHWC input");
+  Ctx c{(hipStream_t)stream, ws, false, 0};
+  DQ_CHECK_ARG((part == 0 || part == 1) && backward_layer(c, p, g, batch, x, a, dout, d, layer, part),
+               "layer must be 0..4 (fc2, fc1, conv3, conv2, conv1), part 0 (input grad, not conv1) "
+               "or 1 (weight grad)");
+  DQ_CHECK_LAUNCH("dq_cnn_backward_layer");
   return DQ_OK;
 }
 

@@ -222,6 +222,12 @@ int dq_cnn_forward(const dq_cnn_params* p, int32_t batch, const float* x, dq_cnn
 int dq_cnn_backward(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch, const float* x,
                     const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d, float* ws,
                     void* stream);
+/* one layer of the backward: layer 0..4 = fc2, fc1, conv3, conv2, conv1; part 1 = weight and
+   bias gradient, part 0 = input gradient (not for conv1).  dW(L) depends only on dX(L-1),
+   so the weight gradients may run on a second stream, each with its own ws. */
+int dq_cnn_backward_layer(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch,
+                          const float* x, const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d,
+                          float* ws, int32_t layer, int32_t part, void* stream);
 size_t dq_cnn_workspace_floats(int32_t batch, int32_t n_out);
 
 /* _build_sync_op (dqn_agent.py:324-339): online -> target copy of the flat buffer. */

@@ -37,12 +37,18 @@ def test_hip_cnn_matches_torch(kind, B, A):
   hip = HipNatureCNN(net, B)
   y = hip.forward(x)
   _close(y, y_ref.detach())
-  hip.backward(gout)
-  for (name, view), gr in zip(zip(net.fp.params.keys(), net.fp.grad_views), g_ref):
-    try:
-      _close(view, gr, rtol=5e-5)
-    except AssertionError as e:
-      raise AssertionError('%s: %s' % (name, e))
+  grads = {}
+  for parallel in (True, False):       # weight grads on a second stream / one stream
+    net.fp.grad.fill_(float('nan'))
+    hip.backward(gout, parallel=parallel)
+    torch.cuda.synchronize()
+    grads[parallel] = torch.cat([v.reshape(-1) for v in net.fp.grad_views])  # skips alignment pads
+    for (name, view), gr in zip(zip(net.fp.params.keys(), net.fp.grad_views), g_ref):
+      try:
+        _close(view, gr, rtol=5e-5)
+      except AssertionError as e:
+        raise AssertionError('%s (parallel=%s): %s' % (name, parallel, e))
+  assert torch.equal(grads[True], grads[False])
 
 
 def test_hip_cnn_graph_capturable_and_deterministic():
