@@ -266,25 +266,35 @@ __device__ __forceinline__ void group_coord(int g, int& rr, int& kk) {
 // accumulators are then summed through LDS by all threads, each output element
 // in wave order (deterministic), and handed to the epilogue with consecutive
 // threads on consecutive columns.
+template <int WM, int WN, int WK>
+struct Tile {
+  static constexpr int T = 64 * WM * WN * WK;
+  static constexpr int BM = 32 * WM, BN = 32 * WN, BKT = 32 * WK;
+  template <class AL, class BL>
+  static constexpr int lds() {      // operand slices, or the WK > 1 reduction scratch
+    const int tile = BKT * (BM + (AL::kFast ? 1 : 4)) + BKT * (BN + (BL::kFast ? 1 : 4));
+    const int red = WK > 1 ? WK * WM * WN * 1024 : 0;
+    return tile > red ? tile : red;
+  }
+};
+
 template <int WM, int WN, int WK, class AL, class BL, class EP>
-__global__ __launch_bounds__(64 * WM * WN * WK) void k_igemm(AL A, BL B, EP E, int M, int N, int K,
-                                                             int kchunk) {
-  constexpr int T = 64 * WM * WN * WK;
-  constexpr int BM = 32 * WM, BN = 32 * WN, BKT = 32 * WK;
+__device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& E, int M, int N,
+                                            int K, int kchunk, int bx, int by, int bz,
+                                            float* smem) {
+  using TL = Tile<WM, WN, WK>;
+  constexpr int T = TL::T, BM = TL::BM, BN = TL::BN, BKT = TL::BKT;
   constexpr int SA = BM + (AL::kFast ? 1 : 4), SB = BN + (BL::kFast ? 1 : 4);
   constexpr int NA = BM * BKT / 4 / T, NB = BN * BKT / 4 / T;
   static_assert(NA >= 1 && NB >= 1 && NA * 4 * T == BM * BKT && NB * 4 * T == BN * BKT, "tile/threads");
-  constexpr int LDS = BKT * SA + BKT * SB;
   constexpr int OUT = WM * WN * 1024;     // output elements per block
-  static_assert(WK * OUT <= LDS, "reduction scratch exceeds LDS tile");
-  __shared__ __attribute__((aligned(16))) float smem[LDS];
   float* As = smem;
   float* Bs = smem + BKT * SA;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = (wave / WM) % WN, wk = wave / (WM * WN);
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-  const int kbeg = blockIdx.z * kchunk;
+  const int m0 = bx * BM, n0 = by * BN;
+  const int kbeg = bz * kchunk;
   const int kend = min(K, kbeg + kchunk);
   float4 ra[NA], rb[NB];
 
@@ -344,8 +354,17 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_igemm(AL A, BL B, EP E, i
     }
     __syncthreads();
   }
-  // partials -> LDS [wk][tile][r][lane]; C/D layout of the 32x32 f32 MFMA:
-  // col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5)
+  // C/D layout of the 32x32 f32 MFMA: col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5)
+  if (WK == 1) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const int n = n0 + wn * 32 + (lane & 31);
+      if (m < M && n < N) E(m, n, acc[r], bz);
+    }
+    return;
+  }
+  // partials -> LDS [wk][tile][r][lane]
   {
     float* red = smem + (wk * WM * WN + wm + WM * wn) * 1024 + lane;
 #pragma unroll
@@ -359,14 +378,21 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_igemm(AL A, BL B, EP E, i
     const int tile = e >> 10, r = (e >> 6) & 15, l = e & 63;
     const int m = m0 + (tile % WM) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
     const int n = n0 + (tile / WM) * 32 + (l & 31);
-    if (m < M && n < N) E(m, n, v, blockIdx.z);
+    if (m < M && n < N) E(m, n, v, bz);
   }
 }
 
-// ordered split-K sum + epilogue; the slab loads of a thread are all in flight together
+template <int WM, int WN, int WK, class AL, class BL, class EP>
+__global__ __launch_bounds__(64 * WM * WN * WK) void k_igemm(AL A, BL B, EP E, int M, int N, int K,
+                                                             int kchunk) {
+  __shared__ __attribute__((aligned(16))) float smem[Tile<WM, WN, WK>::template lds<AL, BL>()];
+  igemm_block<WM, WN, WK>(A, B, E, M, N, K, kchunk, blockIdx.x, blockIdx.y, blockIdx.z, smem);
+}
+
+// ordered split-K sum + epilogue: element i of the (M x N) result, slab loads in flight together
 template <class EP>
-__global__ __launch_bounds__(256) void k_splitk_reduce(const float* ws, int splits, int M, int N, EP E) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void splitk_sum(const float* ws, int splits, int M, int N, const EP& E,
+                                           int64_t i) {
   if (i >= (int64_t)M * N) return;
   const int64_t MN = (int64_t)M * N;
   float s = ws[i];
@@ -380,12 +406,16 @@ __global__ __launch_bounds__(256) void k_splitk_reduce(const float* ws, int spli
   E((int)(i / N), (int)(i % N), s, 0);
 }
 
+template <class EP>
+__global__ __launch_bounds__(256) void k_splitk_reduce(const float* ws, int splits, int M, int N, EP E) {
+  splitk_sum(ws, splits, M, N, E, (int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+}
+
 // strided conv input gradient from dcol[(b, oh, ow)][(kh, kw, ci)]:
 // dx[b][ih][iw][ci] = (act > 0) * sum over the taps that land on (ih, iw), in (kh, kw) order
 template <class G>
-__global__ __launch_bounds__(256) void k_col2im(const float* dcol, const float* act, float* dx,
-                                                int total4) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
+__device__ __forceinline__ void col2im_group(const float* dcol, const float* act, float* dx, int i,
+                                             int total4) {
   if (i >= total4) return;
   constexpr int C4 = G::CI / 4;
   const int ci = (i % C4) * 4, pix = i / C4;
@@ -418,12 +448,99 @@ __global__ __launch_bounds__(256) void k_col2im(const float* dcol, const float* 
   *reinterpret_cast<float4*>(dx + (int64_t)i * 4) = o;
 }
 
+template <class G>
+__global__ __launch_bounds__(256) void k_col2im(const float* dcol, const float* act, float* dx,
+                                                int total4) {
+  col2im_group<G>(dcol, act, dx, blockIdx.x * 256 + threadIdx.x, total4);
+}
+
+// ------------------------------------------------------------ grouped launches
+// Independent operations of the backward (layer L's weight gradient beside layer
+// L+1's input gradient, a split-K reduce beside the next GEMMs) share ONE launch:
+// each op owns a contiguous range of blockIdx.x.  All ops of a group run with
+// the same block size kGroupT, and the block's LDS is the largest op's.
+constexpr int kGroupT = 1024;
+
+template <int WM, int WN, int WK, class AL, class BL, class EP>
+struct GemmOp {
+  static_assert(64 * WM * WN * WK == kGroupT, "grouped GEMMs use 16-wave blocks");
+  static constexpr int kLds = Tile<WM, WN, WK>::template lds<AL, BL>();
+  AL a;
+  BL b;
+  EP e;
+  int M, N, K, kchunk, gx, gy, gz;
+  __device__ __forceinline__ void run(int blk, float* smem) const {
+    const int bx = blk % gx, by = (blk / gx) % gy, bz = blk / (gx * gy);
+    igemm_block<WM, WN, WK>(a, b, e, M, N, K, kchunk, bx, by, bz, smem);
+  }
+  int blocks() const { return gx * gy * gz; }
+};
+
+template <class EP>
+struct ReduceOp {                 // ordered split-K sum of nz slabs + epilogue
+  static constexpr int kLds = 0;
+  const float* ws;
+  int nz, M, N;
+  EP e;
+  __device__ __forceinline__ void run(int blk, float*) const {
+    splitk_sum(ws, nz, M, N, e, (int64_t)blk * kGroupT + threadIdx.x);
+  }
+  int blocks() const { return (int)(((int64_t)M * N + kGroupT - 1) / kGroupT); }
+};
+
+template <class G>
+struct Col2imOp {
+  static constexpr int kLds = 0;
+  const float* dcol;
+  const float* act;
+  float* dx;
+  int total4;
+  __device__ __forceinline__ void run(int blk, float*) const {
+    col2im_group<G>(dcol, act, dx, blk * kGroupT + threadIdx.x, total4);
+  }
+  int blocks() const { return (total4 + kGroupT - 1) / kGroupT; }
+};
+
+template <class... Ops>
+constexpr int max_lds() {
+  int m = 1;
+  ((m = Ops::kLds > m ? Ops::kLds : m), ...);
+  return m;
+}
+
+template <class Op>
+__device__ __forceinline__ bool dispatch(const Op& op, int nb, int& blk, float* smem) {
+  if (blk < nb) {
+    op.run(blk, smem);
+    return true;
+  }
+  blk -= nb;
+  return false;
+}
+
+template <class... Ops>
+struct GroupArgs {
+  int nblocks[sizeof...(Ops)];
+};
+
+template <class... Ops>
+__global__ __launch_bounds__(kGroupT) void k_grouped(GroupArgs<Ops...> g, Ops... ops) {
+  __shared__ __attribute__((aligned(16))) float smem[max_lds<Ops...>()];
+  int blk = blockIdx.x, i = 0;
+  ((dispatch(ops, g.nblocks[i++], blk, smem)) || ...);
+}
+
 // Launch context: a dry run only sizes the workspace, so the two can never disagree.
 struct Ctx {
   hipStream_t s;
   float* ws;       // split-K slabs / conv2 dcol
   bool dry;
   size_t need;
+  size_t take(size_t n) {        // carve a private workspace region (grouped ops run together)
+    const size_t o = need;
+    need += (n + 3) / 4 * 4;
+    return o;
+  }
 };
 
 // K slice per split (multiple of the block's K slice)
@@ -454,6 +571,25 @@ void gemm(Ctx& c, AL a, BL b, EP e, int M, int N, int K, int splits = 1) {
                      c.s, c.ws, nz, M, N, e);
 }
 
+// a grouped GEMM op; split-K ops write slabs into ws + off (EpiPartial)
+template <int WM, int WN, int WK, class AL, class BL, class EP>
+GemmOp<WM, WN, WK, AL, BL, EP> gemm_op(AL a, BL b, EP e, int M, int N, int K, int kchunk) {
+  GemmOp<WM, WN, WK, AL, BL, EP> op{a, b, e, M, N, K, kchunk, 0, 0, 0};
+  op.gx = (M + 32 * WM - 1) / (32 * WM);
+  op.gy = (N + 32 * WN - 1) / (32 * WN);
+  op.gz = (K + kchunk - 1) / kchunk;
+  return op;
+}
+
+template <class... Ops>
+void group(Ctx& c, Ops... ops) {
+  if (c.dry) return;
+  GroupArgs<Ops...> g;
+  int i = 0, total = 0;
+  ((g.nblocks[i++] = ops.blocks(), total += ops.blocks()), ...);
+  hipLaunchKernelGGL((k_grouped<Ops...>), dim3(total), dim3(kGroupT), 0, c.s, g, ops...);
+}
+
 // Tile shapes: WM = WN = 1 with WK k-bands sized so K takes one or two slices
 // (BKT = 32 * WK); split-K only where the grid would otherwise leave most of the
 // 256 CUs idle (weight streaming of fc1, the pixel-deep weight gradients).
@@ -477,13 +613,13 @@ void forward(Ctx& c, const dq_cnn_params* p, int B, const float* x, dq_cnn_acts*
 
 // Backward of one layer: part 1 = weight/bias gradient, part 0 = input gradient.
 // Layers 0..4 = fc2, fc1, conv3, conv2, conv1 (conv1 has no input gradient).
-// dW(L) needs only dX(L-1)'s output, so the two parts can run on two streams.
+// Same tiles and split factors as the grouped schedule below: bitwise identical.
 bool backward_layer(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int B, const float* x,
                     const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d, int layer, int part) {
   const int NO = p->n_out;
   switch (layer * 2 + part) {
     case 0 * 2 + 1:   // fc2: dW2|db2 = dout^T [h | 1]
-      gemm<2, 2, 1>(c, ColKScalar{dout, NO}, ColKOnes{a->h, kHidden},
+      gemm<4, 4, 1>(c, ColKScalar{dout, NO}, ColKOnes{a->h, kHidden},
                     EpiGrad{g->fc2_w, g->fc2_b, kHidden}, NO, kHidden + 1, B);
       return true;
     case 0 * 2 + 0:   // dh = (dout W2) * (h > 0)
@@ -491,7 +627,7 @@ bool backward_layer(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int 
                      B, kHidden, NO);
       return true;
     case 1 * 2 + 1:   // fc1: dW1|db1 = dh^T [a3 | 1]
-      gemm<2, 2, 1>(c, ColK{d->h, kHidden}, ColKOnes{a->a3, kFlat},
+      gemm<4, 4, 1>(c, ColK{d->h, kHidden}, ColKOnes{a->a3, kFlat},
                     EpiGrad{g->fc1_w, g->fc1_b, kFlat}, kHidden, kFlat + 1, B);
       return true;
     case 1 * 2 + 0:   // da3 = (dh W1) * (a3 > 0)
@@ -503,8 +639,8 @@ bool backward_layer(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int 
                      EpiGrad{g->conv3_w, g->conv3_b, Conv3::K}, 64, Conv3::K + 1, B * 121, kSplitConvW);
       return true;
     case 2 * 2 + 0:   // da2 = col2im(da3, W3) * (a2 > 0)
-      gemm<1, 1, 9>(c, Col2im<Conv3>{d->a3}, WeightT<Conv3>{p->conv3_w}, EpiMask{d->a2, a->a2, 64},
-                    B * 121, 64, 9 * 64);
+      gemm<1, 1, 16>(c, Col2im<Conv3>{d->a3}, WeightT<Conv3>{p->conv3_w}, EpiMask{d->a2, a->a2, 64},
+                     B * 121, 64, Conv3::K);
       return true;
     case 3 * 2 + 1:   // conv2: dW2|db2 = da2^T [im2col(a1) | 1]
       gemm<1, 1, 16>(c, DyT<64>{d->a2}, Im2colT<Conv2>{a->a1},
@@ -513,7 +649,7 @@ bool backward_layer(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int 
     case 3 * 2 + 0: {  // da1 = col2im(da2 W2) * (a1 > 0)
       const size_t dcol = (size_t)B * 121 * Conv2::K;
       c.need = dcol > c.need ? dcol : c.need;
-      gemm<1, 1, 2>(c, RowK{d->a2, 64}, ColK{p->conv2_w, Conv2::K}, EpiStore{c.ws, Conv2::K},
+      gemm<4, 4, 1>(c, RowK{d->a2, 64}, ColK{p->conv2_w, Conv2::K}, EpiStore{c.ws, Conv2::K},
                     B * 121, Conv2::K, 64);
       if (!c.dry) {
         const int total4 = B * 441 * 32 / 4;
@@ -531,12 +667,62 @@ bool backward_layer(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int 
   }
 }
 
-void backward(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int B, const float* x,
-              const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d) {
-  for (int layer = 0; layer < 5; ++layer) {
-    backward_layer(c, p, g, B, x, a, dout, d, layer, 1);
-    backward_layer(c, p, g, B, x, a, dout, d, layer, 0);
-  }
+// Backward in 7 grouped launches (13 kernels' worth of work):
+//   1: dh                      (fc2 input grad)
+//   2: dW fc2     | da3        (fc1 input grad)
+//   3: dW fc1     | da2        (conv3 input grad)
+//   4: dW conv3 slabs | dcol   (conv2 input grad, dense part)
+//   5: sum conv3 slabs | dW conv2 slabs | da1 = col2im(dcol)
+//   6: sum conv2 slabs | dW conv1 slabs
+//   7: sum conv1 slabs
+// Each GEMM writes its gradient/activation exactly as the per-layer form does
+// (same tiles, same summation order), so the two are bitwise identical.
+void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int B,
+                      const float* x, const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d) {
+  const int NO = p->n_out;
+  using W16 = Tile<1, 1, 16>;
+  // workspace regions (ops of one launch never share one)
+  const int K3 = B * 121, K1 = B * 441;
+  const int ch3 = split_chunk(K3, kSplitConvW, W16::BKT), nz3 = (K3 + ch3 - 1) / ch3;
+  const int ch1 = split_chunk(K1, kSplitConv1W, W16::BKT), nz1 = (K1 + ch1 - 1) / ch1;
+  const size_t o3 = c.take((size_t)nz3 * 64 * (Conv3::K + 1));
+  const size_t o2 = c.take((size_t)nz3 * 64 * (Conv2::K + 1));
+  const size_t od = c.take((size_t)K3 * Conv2::K);
+  const size_t o1 = c.take((size_t)nz1 * 32 * (Conv1::K + 1));
+  float* ws = c.ws;
+  if (c.dry) return;
+  auto dX_fc2 = gemm_op<1, 1, 16>(RowKScalar{dout, NO}, ColK{p->fc2_w, kHidden},
+                                  EpiMask{d->h, a->h, kHidden}, B, kHidden, NO, NO);
+  auto dW_fc2 = gemm_op<4, 4, 1>(ColKScalar{dout, NO}, ColKOnes{a->h, kHidden},
+                                 EpiGrad{g->fc2_w, g->fc2_b, kHidden}, NO, kHidden + 1, B, B);
+  auto dX_fc1 = gemm_op<1, 1, 16>(RowK{d->h, kHidden}, ColK{p->fc1_w, kFlat},
+                                  EpiMask{d->a3, a->a3, kFlat}, B, kFlat, kHidden, kHidden);
+  auto dW_fc1 = gemm_op<4, 4, 1>(ColK{d->h, kHidden}, ColKOnes{a->a3, kFlat},
+                                 EpiGrad{g->fc1_w, g->fc1_b, kFlat}, kHidden, kFlat + 1, B, B);
+  auto dX_c3 = gemm_op<1, 1, 16>(Col2im<Conv3>{d->a3}, WeightT<Conv3>{p->conv3_w},
+                                 EpiMask{d->a2, a->a2, 64}, K3, 64, Conv3::K, Conv3::K);
+  auto dW_c3 = gemm_op<1, 1, 16>(DyT<64>{d->a3}, Im2colT<Conv3>{a->a2},
+                                 EpiPartial{ws + o3, 64, Conv3::K + 1}, 64, Conv3::K + 1, K3, ch3);
+  auto dcol = gemm_op<4, 4, 1>(RowK{d->a2, 64}, ColK{p->conv2_w, Conv2::K},
+                               EpiStore{ws + od, Conv2::K}, K3, Conv2::K, 64, 64);
+  auto sum_c3 = ReduceOp<EpiGrad>{ws + o3, nz3, 64, Conv3::K + 1,
+                                  EpiGrad{g->conv3_w, g->conv3_b, Conv3::K}};
+  auto dW_c2 = gemm_op<1, 1, 16>(DyT<64>{d->a2}, Im2colT<Conv2>{a->a1},
+                                 EpiPartial{ws + o2, 64, Conv2::K + 1}, 64, Conv2::K + 1, K3, ch3);
+  auto da1 = Col2imOp<Conv2>{ws + od, a->a1, d->a1, B * 441 * 32 / 4};
+  auto sum_c2 = ReduceOp<EpiGrad>{ws + o2, nz3, 64, Conv2::K + 1,
+                                  EpiGrad{g->conv2_w, g->conv2_b, Conv2::K}};
+  auto dW_c1 = gemm_op<1, 1, 16>(DyT<32>{d->a1}, Im2colT<Conv1>{x},
+                                 EpiPartial{ws + o1, 32, Conv1::K + 1}, 32, Conv1::K + 1, K1, ch1);
+  auto sum_c1 = ReduceOp<EpiGrad>{ws + o1, nz1, 32, Conv1::K + 1,
+                                  EpiGrad{g->conv1_w, g->conv1_b, Conv1::K}};
+  group(c, dX_fc2);
+  group(c, dW_fc2, dX_fc1);
+  group(c, dW_fc1, dX_c3);
+  group(c, dW_c3, dcol);
+  group(c, sum_c3, dW_c2, da1);
+  group(c, sum_c2, dW_c1);
+  group(c, sum_c1);
 }
 
 }  // namespace cnn
@@ -563,7 +749,7 @@ int dq_cnn_backward(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batc
   DQ_CHECK_ARG(p && g && a && d && x && dout && ws && batch >= 1, "null argument");
   DQ_CHECK_ARG(p->in_channels == 4 && p->n_out >= 1, "the Nature CNN takes 84x84x4 NHWC input");
   Ctx c{(hipStream_t)stream, ws, false, 0};
-  backward(c, p, g, batch, x, a, dout, d);
+  backward_grouped(c, p, g, batch, x, a, dout, d);
   DQ_CHECK_LAUNCH("dq_cnn_backward");
   return DQ_OK;
 }
@@ -586,10 +772,19 @@ size_t dq_cnn_workspace_floats(int32_t batch, int32_t n_out) {
   dq_cnn_acts a = {};
   p.in_channels = 4;
   p.n_out = n_out;
-  Ctx c{nullptr, nullptr, true, 0};
-  forward(c, &p, batch, nullptr, &a);
-  backward(c, &p, &p, batch, nullptr, &a, nullptr, &a);
-  return c.need;
+  size_t need = 0;
+  Ctx f{nullptr, nullptr, true, 0};
+  forward(f, &p, batch, nullptr, &a);
+  need = f.need > need ? f.need : need;
+  for (int layer = 0; layer < 5; ++layer)
+    for (int part = 0; part < 2; ++part) {
+      Ctx l{nullptr, nullptr, true, 0};
+      backward_layer(l, &p, &p, batch, nullptr, &a, nullptr, &a, layer, part);
+      need = l.need > need ? l.need : need;
+    }
+  Ctx g{nullptr, nullptr, true, 0};
+  backward_grouped(g, &p, &p, batch, nullptr, &a, nullptr, &a);
+  return g.need > need ? g.need : need;
 }
 
 }  // extern "C"
