@@ -38,6 +38,12 @@ class Storage(ctypes.Structure):
 MAX_TENSORS = 16
 
 
+class AdamArgs(ctypes.Structure):
+  _fields_ = [('var', ctypes.c_void_p), ('m', ctypes.c_void_p), ('v', ctypes.c_void_p),
+              ('state', ctypes.c_void_p), ('slot', ctypes.c_int32), ('lr', ctypes.c_float),
+              ('beta1', ctypes.c_float), ('beta2', ctypes.c_float), ('epsilon', ctypes.c_float)]
+
+
 class TensorList(ctypes.Structure):
   _fields_ = [('count', ctypes.c_int32), ('pad_', ctypes.c_int32),
               ('var', ctypes.c_void_p * MAX_TENSORS), ('grad', ctypes.c_void_p * MAX_TENSORS),
@@ -88,6 +94,9 @@ SIGNATURES = {
     'dq_cnn_forward': [ctypes.POINTER(CnnParams), _I32, _P, ctypes.POINTER(CnnActs), _P, _P],
     'dq_cnn_backward': [ctypes.POINTER(CnnParams), ctypes.POINTER(CnnParams), _I32, _P,
                         ctypes.POINTER(CnnActs), _P, ctypes.POINTER(CnnActs), _P, _P],
+    'dq_cnn_backward_adam': [ctypes.POINTER(CnnParams), ctypes.POINTER(CnnParams), _I32, _P,
+                             ctypes.POINTER(CnnActs), _P, ctypes.POINTER(CnnActs), _P,
+                             ctypes.POINTER(AdamArgs), _P],
     'dq_cnn_backward_layer': [ctypes.POINTER(CnnParams), ctypes.POINTER(CnnParams), _I32, _P,
                               ctypes.POINTER(CnnActs), _P, ctypes.POINTER(CnnActs), _P, _I32, _I32,
                               _P],

@@ -83,6 +83,7 @@ class DQNAgent(object):
                use_hip_graph=True,
                pipeline=True,
                use_hip_cnn=True,
+               fuse_optimizer=False,
                device=None,
                seed=0,
                process_group=None):
@@ -117,6 +118,7 @@ class DQNAgent(object):
     self.use_hip_graph = use_hip_graph
     self.pipeline = pipeline
     self.use_hip_cnn = use_hip_cnn
+    self.fuse_optimizer = fuse_optimizer
     self._graphs = None
     self._graphs_opt = None
     self._eager_steps = 0
@@ -205,9 +207,22 @@ class DQNAgent(object):
                              self.cumulative_gamma, out=self._loss_out)
     return q, out['grad']
 
-  def _backward(self, y, g):
+  def _fused_opt(self):
+    """fuse_optimizer + single replica + HIP CNN + TF1 Adam: the optimizer step
+    runs inside the backward's gradient epilogues (dq_cnn_backward_adam).
+    Bitwise identical to the separate step, but measured slower on MI355X (4628
+    vs 5289 steps/s): the epilogue's scalar read-modify-write of 4M fc1
+    parameters runs at ~2.8 TB/s against k_adam's float4 stream at ~6.4 TB/s,
+    and it contends with the concurrently running target forward."""
+    return (self.fuse_optimizer and self._hip is not None and self._pg is None and
+            isinstance(self._opt, ops.TF1Adam))
+
+  def _backward(self, y, g, k=0):
     if self._hip is not None:       # all gradients stored into the flat buffer
-      self._hip['online'].backward(g)
+      if self._fused_opt():
+        self._hip['online'].backward(g, adam=self._opt, slot=k)
+      else:
+        self._hip['online'].backward(g)
       return
     # Fresh per-parameter gradients (no flat-buffer zeroing + accumulate kernels);
     # the multi-tensor TF1 Adam reads them in place.
@@ -242,7 +257,7 @@ class DQNAgent(object):
     for k, v in tg.items():
       self._ptgt[i][k].copy_(v)
 
-  def _grad_step(self, c):
+  def _grad_step(self, c, k=0):
     if not self.pipeline:
       self._prefetch(c)
     y, g = self._online_loss(self._pbuf[c], self._ptgt[c])
@@ -254,17 +269,19 @@ class DQNAgent(object):
       with torch.cuda.stream(self._side):
         self._post_loss(self._pbuf[c])
         self._prefetch(1 - c)
-      self._backward(y, g)
+      self._backward(y, g, k)
       main.wait_stream(self._side)
     else:
       self._post_loss(self._pbuf[c])
-      self._backward(y, g)
+      self._backward(y, g, k)
 
   def _post_loss(self, t):
     """Work that needs the loss but not the gradient (PER priority write-back)."""
 
   def _device_opt_step(self, k):
     """Optimizer step k (k = gradient-step parity: TF1 Adam's beta-power slot)."""
+    if self._fused_opt():
+      return                          # applied inside the backward
     if self._needs_flat_grad():
       self._opt.step(self.online_convnet.fp.grad, slot=k)
     else:
@@ -297,7 +314,7 @@ class DQNAgent(object):
         self._allreduce_grads()
         self._graphs_opt[k].replay()
     else:
-      self._grad_step(c)
+      self._grad_step(c, k)
       self._allreduce_grads()
       self._device_opt_step(k)
       self._eager_steps += 1
@@ -321,7 +338,7 @@ class DQNAgent(object):
       c = k if self.pipeline else 0
       g = torch.cuda.CUDAGraph()
       with torch.cuda.graph(g, pool=pool):
-        self._grad_step(c)
+        self._grad_step(c, k)
         if self._pg is None:
           self._device_opt_step(k)
       pool = g.pool()

@@ -75,8 +75,13 @@ class HipNatureCNN(object):
                'dq_cnn_forward')
     return self.acts['out']
 
-  def backward(self, dout, parallel=False):
+  def backward(self, dout, parallel=False, adam=None, slot=0):
     """dout: (B, n_out).  Writes all parameter gradients into net.fp.grad.
+
+    adam: an ops.TF1Adam over net.fp.flat -- its step (beta-power slot ``slot``)
+    is applied inside the gradient epilogues (dq_cnn_backward_adam), so no
+    separate optimizer launch is needed.  Single replica only: N > 1 GPUs must
+    all-reduce the gradient before the optimizer.
 
     parallel: the weight gradients run on a second stream, each forked after
     the input gradient it needs and joined before returning (stream-ordered,
@@ -86,6 +91,16 @@ class HipNatureCNN(object):
     with the other stream's.  Kept for experimentation; off by default."""
     dout = dout.reshape(self.B, self.n_out)
     assert dout.is_contiguous() and self._x is not None
+    if adam is not None:
+      assert adam.params.data_ptr() == self.net.fp.flat.data_ptr(), 'adam must own net.fp.flat'
+      args = _lib.AdamArgs(var=adam.params.data_ptr(), m=adam.m.data_ptr(), v=adam.v.data_ptr(),
+                           state=adam.state.data_ptr(), slot=int(slot), lr=adam.lr,
+                           beta1=adam.b1, beta2=adam.b2, epsilon=adam.eps)
+      _lib.check(_lib.lib.dq_cnn_backward_adam(
+          ctypes.byref(self._p), ctypes.byref(self._g), self.B, self._x.data_ptr(),
+          ctypes.byref(self._a), dout.data_ptr(), ctypes.byref(self._d), self.ws.data_ptr(),
+          ctypes.byref(args), self._stream(dout)), 'dq_cnn_backward_adam')
+      return self.net.fp.grad
     if not parallel:
       _lib.check(_lib.lib.dq_cnn_backward(ctypes.byref(self._p), ctypes.byref(self._g), self.B,
                                           self._x.data_ptr(), ctypes.byref(self._a),

@@ -58,4 +58,26 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// ---- TF1 ApplyAdam, shared by the optimizer kernels and the fused CNN epilogues.
+// state = {beta1^t, beta2^t} x 2 slots: step t reads slot t % 2 and writes the
+// next powers into the other slot (one thread per step does that).
+__device__ __forceinline__ float adam_alpha_of(const float* state, int slot, float lr) {
+  const float b1p = state[2 * slot], b2p = state[2 * slot + 1];
+  // alpha = lr * sqrt(1 - beta2^t) / (1 - beta1^t)
+  return __fdiv_rn(__fmul_rn(lr, __fsqrt_rn(__fsub_rn(1.0f, b2p))), __fsub_rn(1.0f, b1p));
+}
+
+__device__ __forceinline__ void adam_bump(float* state, int slot, float b1, float b2) {
+  float* nxt = state + 2 * (slot ^ 1);
+  nxt[0] = __fmul_rn(state[2 * slot], b1);
+  nxt[1] = __fmul_rn(state[2 * slot + 1], b2);
+}
+
+__device__ __forceinline__ void adam1(float& var, float g, float& m, float& v, float alpha,
+                                      float omb1, float omb2, float eps) {
+  m = __fadd_rn(m, __fmul_rn(__fsub_rn(g, m), omb1));
+  v = __fadd_rn(v, __fmul_rn(__fsub_rn(__fmul_rn(g, g), v), omb2));
+  var = __fsub_rn(var, __fdiv_rn(__fmul_rn(m, alpha), __fadd_rn(__fsqrt_rn(v), eps)));
+}
+
 }  // namespace dq

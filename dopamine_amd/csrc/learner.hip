@@ -251,21 +251,8 @@ __global__ __launch_bounds__(64) void k_mean(const float* x, int n, float* out) 
 // "prepare" launch and no intra-launch race.
 __device__ __forceinline__ float adam_alpha(const float* state, int slot, float lr, float b1,
                                             float b2) {
-  const float b1p = state[2 * slot], b2p = state[2 * slot + 1];
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    float* nxt = const_cast<float*>(state) + 2 * (slot ^ 1);
-    nxt[0] = __fmul_rn(b1p, b1);
-    nxt[1] = __fmul_rn(b2p, b2);
-  }
-  // alpha = lr * sqrt(1 - beta2^t) / (1 - beta1^t)  (TF1 ApplyAdam)
-  return __fdiv_rn(__fmul_rn(lr, __fsqrt_rn(__fsub_rn(1.0f, b2p))), __fsub_rn(1.0f, b1p));
-}
-
-__device__ __forceinline__ void adam1(float& var, float g, float& m, float& v, float alpha,
-                                      float omb1, float omb2, float eps) {
-  m = __fadd_rn(m, __fmul_rn(__fsub_rn(g, m), omb1));
-  v = __fadd_rn(v, __fmul_rn(__fsub_rn(__fmul_rn(g, g), v), omb2));
-  var = __fsub_rn(var, __fdiv_rn(__fmul_rn(m, alpha), __fadd_rn(__fsqrt_rn(v), eps)));
+  if (blockIdx.x == 0 && threadIdx.x == 0) adam_bump(const_cast<float*>(state), slot, b1, b2);
+  return adam_alpha_of(state, slot, lr);
 }
 
 __device__ __forceinline__ void adam_range(float* __restrict__ var, const float* __restrict__ grad,

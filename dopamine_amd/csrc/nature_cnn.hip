@@ -242,6 +242,90 @@ struct EpiGrad {             // n < nw: dW[m][n]; n == nw: db[m]
   }
 };
 
+// gradient + TF1 Adam in one pass: the element's gradient is final here, so the
+// optimizer update (same arithmetic as dq_adam_tf1) is applied where it is made.
+struct AdamDev {
+  float* state;
+  int slot;
+  float lr, b1, b2, eps;
+};
+struct EpiGradAdam {
+  float* gw;
+  float* gb;
+  int nw;
+  float *w, *mw, *vw;      // parameter / moment slices at the same offsets as gw
+  float *b, *mb, *vb;      // ... and as gb
+  AdamDev o;
+  int bump;                // this epilogue advances the beta powers (one per step)
+  // two-phase form: pre() issues the element's loads, commit() updates and stores,
+  // so a thread's loads for ALL its elements are in flight before the first store
+  // (the stores may alias later loads as far as the compiler knows)
+  static constexpr bool kPre = true;
+  struct Pre {
+    float w, m, v;
+  };
+  __device__ __forceinline__ Pre pre(int m, int n) const {
+    if (n < nw) {
+      const int64_t i = (int64_t)m * nw + n;
+      return Pre{w[i], mw[i], vw[i]};
+    }
+    return Pre{b[m], mb[m], vb[m]};
+  }
+  __device__ __forceinline__ void commit(int m, int n, float g, Pre q) const {
+    const float alpha = adam_alpha_of(o.state, o.slot, o.lr);
+    const float omb1 = __fsub_rn(1.0f, o.b1), omb2 = __fsub_rn(1.0f, o.b2);
+    adam1(q.w, g, q.m, q.v, alpha, omb1, omb2, o.eps);
+    if (n < nw) {
+      const int64_t i = (int64_t)m * nw + n;
+      gw[i] = g;
+      w[i] = q.w;
+      mw[i] = q.m;
+      vw[i] = q.v;
+    } else {
+      gb[m] = g;
+      b[m] = q.w;
+      mb[m] = q.m;
+      vb[m] = q.v;
+    }
+    if (bump && m == 0 && n == 0) adam_bump(o.state, o.slot, o.b1, o.b2);
+  }
+  __device__ __forceinline__ void operator()(int m, int n, float g, int) const {
+    commit(m, n, g, pre(m, n));
+  }
+};
+
+template <class EP, class = void>
+struct HasPre {
+  static constexpr bool value = false;
+};
+template <class EP>
+struct HasPre<EP, decltype((void)EP::kPre)> {
+  static constexpr bool value = EP::kPre;
+};
+
+// host-side: EpiGrad, or EpiGradAdam with the moment slices of the same parameter
+struct AdamHost {
+  const dq_adam_args* a;
+};
+template <bool kAdam>
+struct GradEpi;
+template <>
+struct GradEpi<false> {
+  static EpiGrad make(float* gw, float* gb, int nw, float*, float*, const AdamHost&, int) {
+    return EpiGrad{gw, gb, nw};
+  }
+};
+template <>
+struct GradEpi<true> {
+  static EpiGradAdam make(float* gw, float* gb, int nw, float* w, float* b, const AdamHost& h,
+                          int bump) {
+    const dq_adam_args* a = h.a;
+    const ptrdiff_t ow = w - a->var, ob = b - a->var;
+    return EpiGradAdam{gw, gb, nw, w, a->m + ow, a->v + ow, b, a->m + ob, a->v + ob,
+                       AdamDev{a->state, a->slot, a->lr, a->beta1, a->beta2, a->epsilon}, bump};
+  }
+};
+
 // ------------------------------------------------------------- tile kernel
 // 16-byte group g of an R x BKT operand slice -> (row rr, k offset kk).
 // kFast: 8 consecutive lanes cover 128 contiguous bytes of one row, then rows,
@@ -356,11 +440,25 @@ __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& 
   }
   // C/D layout of the 32x32 f32 MFMA: col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5)
   if (WK == 1) {
+    const int n = n0 + wn * 32 + (lane & 31);
+    if constexpr (HasPre<EP>::value) {      // all loads first, then updates + stores
+      typename EP::Pre q[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      const int n = n0 + wn * 32 + (lane & 31);
-      if (m < M && n < N) E(m, n, acc[r], bz);
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        q[r] = E.pre(min(m, M - 1), min(n, N - 1));     // clamped: loads never branch
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (m < M && n < N) E.commit(m, n, acc[r], q[r]);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (m < M && n < N) E(m, n, acc[r], bz);
+      }
     }
     return;
   }
@@ -667,7 +765,10 @@ bool backward_layer(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int 
   }
 }
 
-// Backward in 7 grouped launches (13 kernels' worth of work):
+// Backward in 7 grouped launches (13 kernels' worth of work; with kAdam also the
+// optimizer: each weight gradient's epilogue applies TF1 Adam, which is safe
+// because every layer's weights have had their last backward use (its input
+// gradient) in an EARLIER launch than the one that finalises its gradient):
 //   1: dh                      (fc2 input grad)
 //   2: dW fc2     | da3        (fc1 input grad)
 //   3: dW fc1     | da2        (conv3 input grad)
@@ -677,9 +778,12 @@ bool backward_layer(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int 
 //   7: sum conv1 slabs
 // Each GEMM writes its gradient/activation exactly as the per-layer form does
 // (same tiles, same summation order), so the two are bitwise identical.
+template <bool kAdam>
 void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int B,
-                      const float* x, const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d) {
+                      const float* x, const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d,
+                      const AdamHost& opt) {
   const int NO = p->n_out;
+  using GE = GradEpi<kAdam>;
   using W16 = Tile<1, 1, 16>;
   // workspace regions (ops of one launch never share one)
   const int K3 = B * 121, K1 = B * 441;
@@ -694,28 +798,33 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
   auto dX_fc2 = gemm_op<1, 1, 16>(RowKScalar{dout, NO}, ColK{p->fc2_w, kHidden},
                                   EpiMask{d->h, a->h, kHidden}, B, kHidden, NO, NO);
   auto dW_fc2 = gemm_op<4, 4, 1>(ColKScalar{dout, NO}, ColKOnes{a->h, kHidden},
-                                 EpiGrad{g->fc2_w, g->fc2_b, kHidden}, NO, kHidden + 1, B, B);
+                                 GE::make(g->fc2_w, g->fc2_b, kHidden, p->fc2_w, p->fc2_b, opt, 0),
+                                 NO, kHidden + 1, B, B);
   auto dX_fc1 = gemm_op<1, 1, 16>(RowK{d->h, kHidden}, ColK{p->fc1_w, kFlat},
                                   EpiMask{d->a3, a->a3, kFlat}, B, kFlat, kHidden, kHidden);
   auto dW_fc1 = gemm_op<4, 4, 1>(ColK{d->h, kHidden}, ColKOnes{a->a3, kFlat},
-                                 EpiGrad{g->fc1_w, g->fc1_b, kFlat}, kHidden, kFlat + 1, B, B);
+                                 GE::make(g->fc1_w, g->fc1_b, kFlat, p->fc1_w, p->fc1_b, opt, 0),
+                                 kHidden, kFlat + 1, B, B);
   auto dX_c3 = gemm_op<1, 1, 16>(Col2im<Conv3>{d->a3}, WeightT<Conv3>{p->conv3_w},
                                  EpiMask{d->a2, a->a2, 64}, K3, 64, Conv3::K, Conv3::K);
   auto dW_c3 = gemm_op<1, 1, 16>(DyT<64>{d->a3}, Im2colT<Conv3>{a->a2},
                                  EpiPartial{ws + o3, 64, Conv3::K + 1}, 64, Conv3::K + 1, K3, ch3);
   auto dcol = gemm_op<4, 4, 1>(RowK{d->a2, 64}, ColK{p->conv2_w, Conv2::K},
                                EpiStore{ws + od, Conv2::K}, K3, Conv2::K, 64, 64);
-  auto sum_c3 = ReduceOp<EpiGrad>{ws + o3, nz3, 64, Conv3::K + 1,
-                                  EpiGrad{g->conv3_w, g->conv3_b, Conv3::K}};
+  auto sum_c3 = ReduceOp<decltype(GE::make(0, 0, 0, 0, 0, opt, 0))>{
+      ws + o3, nz3, 64, Conv3::K + 1,
+      GE::make(g->conv3_w, g->conv3_b, Conv3::K, p->conv3_w, p->conv3_b, opt, 0)};
   auto dW_c2 = gemm_op<1, 1, 16>(DyT<64>{d->a2}, Im2colT<Conv2>{a->a1},
                                  EpiPartial{ws + o2, 64, Conv2::K + 1}, 64, Conv2::K + 1, K3, ch3);
   auto da1 = Col2imOp<Conv2>{ws + od, a->a1, d->a1, B * 441 * 32 / 4};
-  auto sum_c2 = ReduceOp<EpiGrad>{ws + o2, nz3, 64, Conv2::K + 1,
-                                  EpiGrad{g->conv2_w, g->conv2_b, Conv2::K}};
+  auto sum_c2 = ReduceOp<decltype(GE::make(0, 0, 0, 0, 0, opt, 0))>{
+      ws + o2, nz3, 64, Conv2::K + 1,
+      GE::make(g->conv2_w, g->conv2_b, Conv2::K, p->conv2_w, p->conv2_b, opt, 0)};
   auto dW_c1 = gemm_op<1, 1, 16>(DyT<32>{d->a1}, Im2colT<Conv1>{x},
                                  EpiPartial{ws + o1, 32, Conv1::K + 1}, 32, Conv1::K + 1, K1, ch1);
-  auto sum_c1 = ReduceOp<EpiGrad>{ws + o1, nz1, 32, Conv1::K + 1,
-                                  EpiGrad{g->conv1_w, g->conv1_b, Conv1::K}};
+  auto sum_c1 = ReduceOp<decltype(GE::make(0, 0, 0, 0, 0, opt, 0))>{
+      ws + o1, nz1, 32, Conv1::K + 1,
+      GE::make(g->conv1_w, g->conv1_b, Conv1::K, p->conv1_w, p->conv1_b, opt, 1)};
   group(c, dX_fc2);
   group(c, dW_fc2, dX_fc1);
   group(c, dW_fc1, dX_c3);
@@ -749,8 +858,25 @@ int dq_cnn_backward(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batc
   DQ_CHECK_ARG(p && g && a && d && x && dout && ws && batch >= 1, "null argument");
   DQ_CHECK_ARG(p->in_channels == 4 && p->n_out >= 1, "the Nature CNN takes 84x84x4 NHWC input");
   Ctx c{(hipStream_t)stream, ws, false, 0};
-  backward_grouped(c, p, g, batch, x, a, dout, d);
+  backward_grouped<false>(c, p, g, batch, x, a, dout, d, AdamHost{nullptr});
   DQ_CHECK_LAUNCH("dq_cnn_backward");
+  return DQ_OK;
+}
+
+int dq_cnn_backward_adam(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch,
+                         const float* x, const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d,
+                         float* ws, const dq_adam_args* opt, void* stream) {
+  DQ_CHECK_ARG(p && g && a && d && x && dout && ws && opt && batch >= 1, "null argument");
+  DQ_CHECK_ARG(p->in_channels == 4 && p->n_out >= 1, "the Nature CNN takes 84x84x4 NHWC input");
+  DQ_CHECK_ARG(opt->var && opt->m && opt->v && opt->state && (opt->slot == 0 || opt->slot == 1),
+               "adam args: var, m, v, state and slot 0/1 required");
+  const float* w[10] = {p->conv1_w, p->conv1_b, p->conv2_w, p->conv2_b, p->conv3_w,
+                        p->conv3_b, p->fc1_w,  p->fc1_b,  p->fc2_w,  p->fc2_b};
+  for (const float* q : w)
+    DQ_CHECK_ARG(q >= opt->var, "parameters must live in the flat buffer opt->var");
+  Ctx c{(hipStream_t)stream, ws, false, 0};
+  backward_grouped<true>(c, p, g, batch, x, a, dout, d, AdamHost{opt});
+  DQ_CHECK_LAUNCH("dq_cnn_backward_adam");
   return DQ_OK;
 }
 
@@ -783,7 +909,7 @@ size_t dq_cnn_workspace_floats(int32_t batch, int32_t n_out) {
       need = l.need > need ? l.need : need;
     }
   Ctx g{nullptr, nullptr, true, 0};
-  backward_grouped(g, &p, &p, batch, nullptr, &a, nullptr, &a);
+  backward_grouped<false>(g, &p, &p, batch, nullptr, &a, nullptr, &a, AdamHost{nullptr});
   return g.need > need ? g.need : need;
 }
 

@@ -222,6 +222,20 @@ int dq_cnn_forward(const dq_cnn_params* p, int32_t batch, const float* x, dq_cnn
 int dq_cnn_backward(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch, const float* x,
                     const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d, float* ws,
                     void* stream);
+/* TF1 Adam (as dq_adam_tf1) applied inside the backward's gradient epilogues. */
+typedef struct dq_adam_args {
+  float* var;        /* flat parameter buffer the dq_cnn_params pointers point into */
+  float* m;          /* moments, same layout as var */
+  float* v;
+  float* state;      /* {beta1^t, beta2^t} x 2 slots, as dq_adam_tf1 */
+  int32_t slot;      /* step parity: reads state slot, writes the other */
+  float lr, beta1, beta2, epsilon;
+} dq_adam_args;
+/* backward + optimizer step in one pass (single-replica training: no gradient
+   all-reduce between them).  Gradients are still written to g. */
+int dq_cnn_backward_adam(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch,
+                         const float* x, const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d,
+                         float* ws, const dq_adam_args* opt, void* stream);
 /* one layer of the backward: layer 0..4 = fc2, fc1, conv3, conv2, conv1; part 1 = weight and
    bias gradient, part 0 = input gradient (not for conv1).  dW(L) depends only on dX(L-1),
    so the weight gradients may run on a second stream, each with its own ws. */

@@ -35,9 +35,10 @@ def test_struct_layouts_match_c():
 #include <stddef.h>
 #include "dopamine_amd.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(dq_replay_meta), sizeof(dq_replay_config),
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(dq_replay_meta), sizeof(dq_replay_config),
          sizeof(dq_replay_storage), offsetof(dq_replay_meta, status),
-         offsetof(dq_replay_config, gamma), offsetof(dq_replay_storage, discount));
+         offsetof(dq_replay_config, gamma), offsetof(dq_replay_storage, discount),
+         sizeof(dq_adam_args), offsetof(dq_adam_args, epsilon));
   return 0;
 }
 '''
@@ -48,7 +49,8 @@ int main(void) {
     subprocess.run(['gcc', '-I', os.path.join(ROOT, 'include'), '-o', exe, c], check=True)
     got = [int(x) for x in subprocess.check_output([exe]).split()]
   exp = [ctypes.sizeof(_lib.Meta), ctypes.sizeof(_lib.Config), ctypes.sizeof(_lib.Storage),
-         _lib.Meta.status.offset, _lib.Config.gamma.offset, _lib.Storage.discount.offset]
+         _lib.Meta.status.offset, _lib.Config.gamma.offset, _lib.Storage.discount.offset,
+         ctypes.sizeof(_lib.AdamArgs), _lib.AdamArgs.epsilon.offset]
   assert got == exp
 
 

@@ -73,3 +73,28 @@ def test_hip_cnn_graph_capturable_and_deterministic():
   torch.cuda.synchronize()
   assert torch.equal(hip.acts['out'], ref_y)
   assert torch.equal(net.fp.grad, ref_g)     # split-K reduced in fixed order: bitwise stable
+
+
+def test_fused_adam_backward_equals_backward_then_adam():
+  """dq_cnn_backward_adam == dq_cnn_backward + dq_adam_tf1, bitwise, over two
+  steps (both beta-power slots): same gradient, same ApplyAdam arithmetic."""
+  from dopamine_amd import ops
+  from dopamine_amd.agents.networks import RainbowNetwork
+  from dopamine_amd.cnn import HipNatureCNN
+  nets = [RainbowNetwork(9, device='cuda', seed=5) for _ in range(2)]
+  hips = [HipNatureCNN(n, 32) for n in nets]
+  opts = [ops.TF1Adam(n.fp.flat, learning_rate=6.25e-5, epsilon=1.5e-4) for n in nets]
+  torch.manual_seed(1)
+  for step in range(2):
+    x = torch.rand(32, 84, 84, 4, device='cuda')
+    gout = torch.randn(32, 459, device='cuda')
+    for h in hips:
+      h.forward(x)
+    hips[0].backward(gout, adam=opts[0], slot=step % 2)
+    hips[1].backward(gout)
+    opts[1].step(nets[1].fp.grad, slot=step % 2)
+    torch.cuda.synchronize()
+    for a, b in zip(nets[0].fp.grad_views, nets[1].fp.grad_views):
+      assert torch.equal(a, b)
+    for n in ('params', 'm', 'v', 'state'):
+      assert torch.equal(getattr(opts[0], n), getattr(opts[1], n)), (step, n)
