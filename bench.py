@@ -96,6 +96,40 @@ def time_gather(agent, iters):
   return graph_us, eager_us, algo_bytes, name
 
 
+def time_gather_large(agent, batch=1024, iters=50):
+  """Supplementary: the same gather kernel at batch 1024 (distinct random valid
+  indices), where it is no longer launch/latency bound -- what the kernel design
+  reaches on HBM.  Not the bench workload; reported beside ``roofline``."""
+  mem = agent._replay.memory
+  layout = agent._replay._layout
+  C = mem._replay_capacity
+  gen = torch.Generator(device='cpu').manual_seed(7)
+  idx = torch.randint(mem._stack_size, C - mem._update_horizon - 1, (batch,), generator=gen,
+                      dtype=torch.int32).to(torch.cuda.current_device())
+  out = mem._alloc_batch(batch, layout)
+  stream = torch.cuda.current_stream()
+  for _ in range(3):
+    mem._gather(idx, batch, layout, out)
+  g = torch.cuda.CUDAGraph()
+  with torch.cuda.graph(g):
+    for _ in range(iters):
+      mem._gather(idx, batch, layout, out)
+  g.replay()
+  torch.cuda.synchronize()
+  e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+  e0.record(stream)
+  g.replay()
+  e1.record(stream)
+  e1.synchronize()
+  us = e0.elapsed_time(e1) * 1e3 / iters
+  S, obs = mem._stack_size, mem._obs_bytes
+  algo = batch * (2 * S * obs + 2 * S * obs * 4)
+  del out
+  return {'batch': batch, 'avg_launch_us': round(us, 3), 'algo_bytes_per_launch': algo,
+          'achieved_GBs': round(algo / (us * 1e-6) / 1e9, 1),
+          'frac': round(algo / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+
+
 def cpu_baseline(seconds, A, batch):
   from oracle.cpu_step import CpuRainbowStep
   threads = min(16, os.cpu_count() or 1)
@@ -161,6 +195,7 @@ def main():
   assert np.isfinite(loss), 'non-finite loss'
 
   graph_us, eager_us, algo_bytes, gname = time_gather(agent, args.gather_iters)
+  large = time_gather_large(agent)
   achieved = algo_bytes / (graph_us * 1e-6) / 1e9
 
   cpu = None
@@ -184,7 +219,8 @@ def main():
                      'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
                      'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4),
                      'traffic': None, 'algo_bytes_per_launch': algo_bytes,
-                     'avg_launch_us': round(graph_us, 3), 'avg_launch_us_eager': round(eager_us, 3)},
+                     'avg_launch_us': round(graph_us, 3), 'avg_launch_us_eager': round(eager_us, 3),
+                     'same_kernel_batch_1024': large},
         'cpu_baseline': cpu,
         'final_mean_loss': round(loss, 5),
     }

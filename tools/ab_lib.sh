@@ -1,0 +1,10 @@
+#!/bin/bash
+# A/B the bench between the in-tree library and alternate builds (same box, one
+# process per run, alternating):   bash tools/ab_lib.sh ab/A/libdopamine_amd.so ...
+for rep in 1 2; do
+  for lib in "" "$@"; do
+    line=$(DOPAMINE_AMD_LIB=$lib timeout -k 10 240 python bench.py --steps 400 2>/dev/null | tail -1)
+    v=$(echo "$line" | python3 -c 'import sys,json; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])' 2>/dev/null)
+    echo "[${lib:-in-tree}] -> $v"
+  done
+done
