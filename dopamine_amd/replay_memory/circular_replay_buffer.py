@@ -11,7 +11,10 @@ uses ``sample_device`` which stays on the device and never synchronises.
 """
 import collections
 import ctypes
+import gzip
 import math
+import os
+import pickle
 
 import numpy as np
 import torch
@@ -23,6 +26,15 @@ ReplayElement = collections.namedtuple('shape_type', ['name', 'shape', 'type'])
 
 STORE_FILENAME_PREFIX = '$store$_'
 CHECKPOINT_DURATION = 4
+
+
+class NotFoundError(IOError):
+  """Stands in for ``tf.errors.NotFoundError`` (same constructor), raised by
+  ``load`` when a checkpoint file is missing (crb:671-673)."""
+
+  def __init__(self, node_def, op, message):
+    super().__init__(message)
+    self.node_def, self.op, self.message = node_def, op, message
 
 
 def invalid_range(cursor, replay_capacity, stack_size, update_horizon):
@@ -487,13 +499,108 @@ class OutOfGraphReplayBuffer(object):
     _lib.call('dq_replay_set_meta', self._h, int(add_count), maxrec, self._stream)
 
   # --------------------------------------------------------- checkpointing
-  def _return_checkpointable_elements(self):
-    elems = {STORE_FILENAME_PREFIX + n: None for n in ('observation', 'action', 'reward', 'terminal')}
+  # crb:593-687: one gzip file per element, '<name>_ckpt.<iteration>.gz'; the store
+  # arrays as '$store$_<name>' via np.save (no pickle), other ndarray attributes
+  # via np.save, anything else pickled; the file CHECKPOINT_DURATION iterations
+  # old is removed after each write; load() first checks that every file exists.
+  # The arrays live in HBM: save is one D2H copy per array, load one H2D copy
+  # into the existing device tensors (so shapes/dtypes must match the buffer).
+  def _store_tensors(self):
+    """Device views of the storage with the reference's ``_store`` names,
+    shapes and dtypes (crb:160-171)."""
+    C = self._replay_capacity
+    obs = self._frames.view(_torch_dtype(self._observation_dtype)).reshape(
+        (C,) + tuple(self._observation_shape))
+    st = collections.OrderedDict([('observation', obs), ('action', self._actions),
+                                  ('reward', self._rewards), ('terminal', self._terminals)])
     for e in self._extra_storage_types:
-      elems[STORE_FILENAME_PREFIX + e.name] = None
-    elems['add_count'] = self.add_count
-    elems['invalid_range'] = self.invalid_range
+      st[e.name] = self._extras[e.name]
+    return st
+
+  @property
+  def _store(self):
+    """Host copies of the storage arrays, keyed as the reference's ``_store``."""
+    return {k: v.cpu().numpy() for k, v in self._store_tensors().items()}
+
+  def _return_checkpointable_elements(self):
+    """crb:596-610: every public member + every store array."""
+    elems = collections.OrderedDict()
+    for name, t in self._store_tensors().items():
+      elems[STORE_FILENAME_PREFIX + name] = t
+    for member_name, member in self.__dict__.items():
+      if not member_name.startswith('_'):
+        elems[member_name] = member
     return elems
+
+  def _generate_filename(self, checkpoint_dir, name, suffix):
+    return os.path.join(checkpoint_dir, '{}_ckpt.{}.gz'.format(name, suffix))
+
+  def _checkpoint_value(self, attr, value):
+    """What gets pickled for a non-array public member (PER overrides sum_tree)."""
+    return value
+
+  def _restore_value(self, attr, value):
+    return value
+
+  def save(self, checkpoint_dir, iteration_number):
+    """crb:612-657."""
+    if not os.path.exists(checkpoint_dir):
+      return
+    elems = self._return_checkpointable_elements()
+    for attr, value in elems.items():
+      filename = self._generate_filename(checkpoint_dir, attr, iteration_number)
+      with open(filename, 'wb') as f:
+        with gzip.GzipFile(fileobj=f, mode='wb') as outfile:
+          if attr.startswith(STORE_FILENAME_PREFIX):
+            np.save(outfile, value.cpu().numpy(), allow_pickle=False)
+          elif isinstance(value, np.ndarray):
+            np.save(outfile, value, allow_pickle=False)
+          else:
+            pickle.dump(self._checkpoint_value(attr, value), outfile)
+      stale = iteration_number - CHECKPOINT_DURATION
+      if stale >= 0:
+        try:
+          os.remove(self._generate_filename(checkpoint_dir, attr, stale))
+        except FileNotFoundError:
+          pass
+
+  def load(self, checkpoint_dir, suffix):
+    """crb:659-687.  Raises NotFoundError (nothing loaded) if any file is missing.
+    Pickled members are unpickled: load only checkpoints this code wrote."""
+    elems = self._return_checkpointable_elements()
+    for attr in elems:
+      filename = self._generate_filename(checkpoint_dir, attr, suffix)
+      if not os.path.exists(filename):
+        raise NotFoundError(None, None, 'Missing file: {}'.format(filename))
+    arrays = {}
+    for attr, cur in elems.items():
+      filename = self._generate_filename(checkpoint_dir, attr, suffix)
+      with open(filename, 'rb') as f:
+        with gzip.GzipFile(fileobj=f, mode='rb') as infile:
+          if attr.startswith(STORE_FILENAME_PREFIX):
+            arr = np.load(infile, allow_pickle=False)
+            if tuple(arr.shape) != tuple(cur.shape):
+              raise ValueError('{}: checkpoint array has shape {}, the buffer stores {}'.format(
+                  filename, arr.shape, tuple(cur.shape)))
+            arrays[attr] = arr
+          elif isinstance(cur, np.ndarray):
+            self.__dict__[attr] = np.load(infile, allow_pickle=False)
+          else:
+            self.__dict__[attr] = self._restore_value(attr, pickle.load(infile))
+    for attr, arr in arrays.items():
+      t = elems[attr]
+      t.copy_(torch.from_numpy(np.ascontiguousarray(arr)).to(dtype=t.dtype))
+    self._after_load()
+
+  def _after_load(self):
+    """Re-derive the device control block from the loaded host state."""
+    C = self._replay_capacity
+    self._last_terminal = int(self._terminals[(self.cursor() - 1) % C].item())
+    _lib.call('dq_replay_set_meta', self._h, int(self.add_count), self._max_recorded_after_load(),
+              self._stream)
+
+  def _max_recorded_after_load(self):
+    return 1.0
 
 
 def _torch_dtype(np_dtype):

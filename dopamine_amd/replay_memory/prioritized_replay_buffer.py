@@ -12,7 +12,7 @@ import torch
 from dopamine_amd import _lib
 from dopamine_amd.replay_memory import circular_replay_buffer
 from dopamine_amd.replay_memory.circular_replay_buffer import ReplayElement
-from dopamine_amd.replay_memory.sum_tree import DeviceSumTree
+from dopamine_amd.replay_memory.sum_tree import DeviceSumTree, SumTreeState
 
 
 class OutOfGraphPrioritizedReplayBuffer(circular_replay_buffer.OutOfGraphReplayBuffer):
@@ -84,6 +84,30 @@ class OutOfGraphPrioritizedReplayBuffer(circular_replay_buffer.OutOfGraphReplayB
     p = torch.as_tensor(priorities, dtype=torch.float64, device=self._device).reshape(-1)
     self._tree[leaves - 1:leaves - 1 + p.numel()] = p
     _lib.call('dq_sumtree_rebuild', self._h, self._stream)
+
+  # checkpoint: the reference pickles its SumTree object (prb:98 is a public member);
+  # here the member is a device view, so a SumTreeState with the reference SumTree's
+  # fields (per-level ``nodes`` arrays, ``max_recorded_priority``) is pickled instead.
+  def _checkpoint_value(self, attr, value):
+    if attr == 'sum_tree' and isinstance(value, DeviceSumTree):
+      return SumTreeState(value.nodes, value.max_recorded_priority)
+    return value
+
+  def _restore_value(self, attr, value):
+    if attr == 'sum_tree':
+      if not isinstance(value, SumTreeState):
+        raise ValueError('sum_tree checkpoint holds {}, expected SumTreeState'.format(type(value)))
+      flat = np.concatenate([np.asarray(n, np.float64) for n in value.nodes])
+      if flat.shape[0] != self._tree.numel():
+        raise ValueError('sum_tree checkpoint has {} nodes, the buffer {}'.format(
+            flat.shape[0], self._tree.numel()))
+      self._tree.copy_(torch.from_numpy(flat))
+      self._loaded_maxrec = float(value.max_recorded_priority)
+      return DeviceSumTree(self)
+    return value
+
+  def _max_recorded_after_load(self):
+    return getattr(self, '_loaded_maxrec', self.sum_tree.max_recorded_priority)
 
   def load_tree_nodes(self, nodes, max_recorded_priority):
     """Install a complete heap (e.g. an oracle-built tree) verbatim."""

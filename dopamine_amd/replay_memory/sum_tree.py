@@ -42,6 +42,16 @@ class DeviceSumTree(object):
     self._buf.set_priority(np.array([node_index], np.int32), np.array([value], np.float32))
 
 
+class SumTreeState(object):
+  """Host snapshot of a sum tree with the reference SumTree's fields (st:80-89),
+  the pickled ``sum_tree`` member of a prioritized buffer checkpoint."""
+
+  def __init__(self, nodes, max_recorded_priority):
+    self.nodes = [np.asarray(n, np.float64) for n in nodes]
+    self.depth = len(self.nodes) - 1
+    self.max_recorded_priority = float(max_recorded_priority)
+
+
 def SumTree(capacity):  # noqa: N802 -- reference class name
   """A standalone device sum tree (sum_tree.py:65-89): a prioritized buffer
   with 1-byte observations whose tree is the object of interest."""

@@ -169,11 +169,42 @@ def gen_replay(m, prioritized):
   np.savez_compressed(os.path.join(OUT, fname), **out)
 
 
+def gen_checkpoint(m):
+  """A checkpoint WRITTEN BY THE REFERENCE's OutOfGraphReplayBuffer.save
+  (crb:612-657) for a small wrapped uniform buffer -- its members are all numpy
+  arrays, so every file is np.save data (no pickle) -- plus what the reference
+  samples after loading it (np.random.seed(13))."""
+  import shutil
+  crb = m['circular_replay_buffer']
+  tf = sys.modules['tensorflow']
+  tf.gfile = types.SimpleNamespace(Exists=os.path.exists, Open=open, Remove=os.remove)
+  tf.errors = types.SimpleNamespace(NotFoundError=FileNotFoundError)
+  kw = dict(observation_shape=(6, 6), stack_size=4, replay_capacity=40, batch_size=4,
+            update_horizon=2, gamma=0.9)
+  mem = crb.OutOfGraphReplayBuffer(**kw)
+  rs = np.random.RandomState(5)
+  for i in range(57):
+    mem.add(rs.randint(0, 256, (6, 6)).astype(np.uint8), int(rs.randint(0, 5)),
+            float(rs.randn()), bool(i % 13 == 12))
+  d = os.path.join(OUT, 'ckpt_uniform')
+  shutil.rmtree(d, ignore_errors=True)
+  os.makedirs(d)
+  mem.save(d, 7)
+  fresh = crb.OutOfGraphReplayBuffer(**kw)
+  fresh.load(d, 7)
+  np.random.seed(13)
+  batch = fresh.sample_transition_batch(batch_size=4)
+  names = [e.name for e in fresh.get_transition_elements(4)]
+  np.savez_compressed(os.path.join(OUT, 'ckpt_uniform_expected.npz'),
+                      **{n: np.asarray(v) for n, v in zip(names, batch)})
+
+
 if __name__ == '__main__':
   mods = _load_reference()
   gen_sumtree(mods)
   gen_replay(mods, prioritized=False)
   gen_replay(mods, prioritized=True)
+  gen_checkpoint(mods)
   for f in sorted(os.listdir(OUT)):
     if f.endswith('.npz'):
       print(f, os.path.getsize(os.path.join(OUT, f)))

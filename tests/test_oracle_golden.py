@@ -82,3 +82,18 @@ def test_replay_golden(golden, prioritized):
     fb = mem.sample_transition_batch(batch_size=len(fixed), indices=fixed)
     for k, v in zip(keys, fb):
       np.testing.assert_array_equal(v, z[name + '_fixed_' + k])
+
+
+def test_reference_checkpoint_fixture_is_plain_npy():
+  """The reference-written uniform checkpoint holds only np.save data (loadable
+  with allow_pickle=False), in the '<name>_ckpt.<iteration>.gz' layout of crb:593-594."""
+  import gzip
+  import os
+  d = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden', 'ckpt_uniform')
+  names = sorted(f for f in os.listdir(d))
+  assert names == sorted('{}_ckpt.7.gz'.format(a) for a in (
+      '$store$_observation', '$store$_action', '$store$_reward', '$store$_terminal',
+      'add_count', 'invalid_range'))
+  for f in names:
+    with gzip.open(os.path.join(d, f), 'rb') as fh:
+      np.load(fh, allow_pickle=False)
