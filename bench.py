@@ -42,6 +42,8 @@ def parse():
   ap.add_argument('--cpu-seconds', type=float, default=12.0)
   ap.add_argument('--skip-cpu-baseline', action='store_true')
   ap.add_argument('--gather-iters', type=int, default=400)
+  ap.add_argument('--fuse-opt', type=int, default=None,
+                  help='override the agent default fuse_optimizer (0/1)')
   return ap.parse_args()
 
 
@@ -163,7 +165,8 @@ def main():
                        optimizer=AdamOptimizer(learning_rate=0.0000625, epsilon=0.00015),
                        replay_capacity=args.capacity, batch_size=args.batch,
                        use_hip_graph=not args.no_graph, device=dev, seed=1000 * rank,
-                       process_group=pg)
+                       process_group=pg,
+                       **({} if args.fuse_opt is None else {'fuse_optimizer': bool(args.fuse_opt)}))
   import random
   random.seed(0 + rank)
   fill_synthetic(agent._replay.memory, args.actions, seed=1 + rank)

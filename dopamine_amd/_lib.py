@@ -92,6 +92,8 @@ SIGNATURES = {
     'dq_rmsprop_tf1': [_P, _P, _P, _P, _P, _I64, _F, _F, _F, _F, _I32, _P],
     'dq_sync_copy': [_P, _P, _I64, _P],
     'dq_cnn_forward': [ctypes.POINTER(CnnParams), _I32, _P, ctypes.POINTER(CnnActs), _P, _P],
+    'dq_cnn_forward_pair': [ctypes.POINTER(CnnParams), _P, ctypes.POINTER(CnnActs), _P,
+                            ctypes.POINTER(CnnParams), _P, ctypes.POINTER(CnnActs), _P, _I32, _P],
     'dq_cnn_backward': [ctypes.POINTER(CnnParams), ctypes.POINTER(CnnParams), _I32, _P,
                         ctypes.POINTER(CnnActs), _P, ctypes.POINTER(CnnActs), _P, _P],
     'dq_cnn_backward_adam': [ctypes.POINTER(CnnParams), ctypes.POINTER(CnnParams), _I32, _P,

@@ -84,6 +84,7 @@ class DQNAgent(object):
                pipeline=True,
                use_hip_cnn=True,
                fuse_optimizer=False,
+               pair_forward=False,
                device=None,
                seed=0,
                process_group=None):
@@ -119,6 +120,7 @@ class DQNAgent(object):
     self.pipeline = pipeline
     self.use_hip_cnn = use_hip_cnn
     self.fuse_optimizer = fuse_optimizer
+    self.pair_forward = pair_forward
     self._graphs = None
     self._graphs_opt = None
     self._eager_steps = 0
@@ -128,6 +130,7 @@ class DQNAgent(object):
     self._ptgt = [None, None]
     self._has_prefetch = False
     self._prefetch_add_count = -1
+    self._online_ready = None
     self._sess = sess
 
     state_shape = (1,) + self.observation_shape + (stack_size,)
@@ -172,6 +175,9 @@ class DQNAgent(object):
   def _online_forward(self, x):
     """Online network output for the loss (keeps what the backward needs)."""
     if self._hip is not None:
+      ready, self._online_ready = self._online_ready, None
+      if ready is not None:             # already computed by _forward_pair
+        return ready
       return self._hip['online'].forward(x)
     return self.online_convnet(self._state_input(x))
 
@@ -209,11 +215,12 @@ class DQNAgent(object):
 
   def _fused_opt(self):
     """fuse_optimizer + single replica + HIP CNN + TF1 Adam: the optimizer step
-    runs inside the backward's gradient epilogues (dq_cnn_backward_adam).
-    Bitwise identical to the separate step, but measured slower on MI355X (4628
-    vs 5289 steps/s): the epilogue's scalar read-modify-write of 4M fc1
-    parameters runs at ~2.8 TB/s against k_adam's float4 stream at ~6.4 TB/s,
-    and it contends with the concurrently running target forward."""
+    rides in the backward's last grouped launch (dq_cnn_backward_adam: conv1's
+    split-K sum applies Adam in its epilogue, a float4 Adam op streams the rest).
+    Bitwise identical to the separate k_adam step but measured ~1.5% slower on
+    MI355X (5,196 vs 5,292 steps/s), so it is off by default.  (A first form that
+    applied Adam in every gradient epilogue was 12% slower: scalar RMW of 4M fc1
+    parameters at 2.8 TB/s against k_adam's 6.4 TB/s.)"""
     return (self.fuse_optimizer and self._hip is not None and self._pg is None and
             isinstance(self._opt, ops.TF1Adam))
 
@@ -243,11 +250,32 @@ class DQNAgent(object):
   # Step t+1's sample still follows step t's set_priority, so draws and indices
   # are exactly the reference's; a prefetch made stale by add() or host RNG use
   # is rewound (dq_replay_rewind_last_sample) and redrawn.
+  def _target_dict(self, out):
+    """The target network's raw output as the loss kernel's inputs."""
+    return {'q': out}
+
+  def _pairs(self):
+    return self.pair_forward and self._hip is not None
+
+  def _forward_pair(self, c):
+    """pair_forward: the online net on s and the target net on s' of slot c in ONE
+    pass (dq_cnn_forward_pair, 6 grouped launches) at the start of the step,
+    instead of the target forward riding on the prefetch stream.  Measured slower
+    (4938 vs 5260 steps/s): the prefetch-stream target forward is mostly hidden
+    under the backward, while the pair lengthens the critical path."""
+    from dopamine_amd.cnn import forward_pair
+    t = self._pbuf[c]
+    on, tg = forward_pair(self._hip['online'], t['state'], self._hip['target'][c], t['next_state'])
+    self._online_ready = on
+    self._ptgt[c] = self._target_dict(tg)
+
   def _prefetch(self, i):
     mem = self._replay.memory
     t = mem.sample_device(self._batch_size, layout=self._replay._layout, out=self._pbuf[i],
                           reserve=False)
     self._pbuf[i] = t
+    if self._pairs():               # the target forward runs with the online one (_forward_pair)
+      return
     tg = self._target_forward(t, i)
     if self._hip is not None:       # persistent per-slot output buffers: no copy
       self._ptgt[i] = tg
@@ -260,6 +288,8 @@ class DQNAgent(object):
   def _grad_step(self, c, k=0):
     if not self.pipeline:
       self._prefetch(c)
+    if self._pairs():
+      self._forward_pair(c)
     y, g = self._online_loss(self._pbuf[c], self._ptgt[c])
     if self.pipeline:
       main = torch.cuda.current_stream(self._device)
@@ -353,7 +383,7 @@ class DQNAgent(object):
 
   def _sync_target(self):
     ops.sync_copy(self.target_convnet.fp.flat, self.online_convnet.fp.flat)
-    if self.pipeline and self._has_prefetch:   # the prefetched target outputs are stale
+    if self.pipeline and self._has_prefetch and not self._pairs():   # prefetched target outputs are stale
       tg = self._target_forward(self._pbuf[self._slot], self._slot)
       for k, v in tg.items():
         if v.data_ptr() != self._ptgt[self._slot][k].data_ptr():

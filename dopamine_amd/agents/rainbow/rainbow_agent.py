@@ -113,9 +113,11 @@ class RainbowAgent(dqn_agent.DQNAgent):
     logits = self.online_convnet(x)
     return (torch.softmax(logits, -1) * self._support).sum(-1)
 
+  def _target_dict(self, out):
+    return {'logits': out.view(-1, self.num_actions, self._num_atoms)}
+
   def _target_forward(self, t, slot):
-    return {'logits': self._target_net(t['next_state'], slot).view(-1, self.num_actions,
-                                                                   self._num_atoms)}
+    return self._target_dict(self._target_net(t['next_state'], slot))
 
   def _online_loss(self, t, tgt):
     """rainbow_agent.py:200-305."""

@@ -63,12 +63,16 @@ class HipNatureCNN(object):
   def _stream(t):
     return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
 
-  def forward(self, x):
-    """x: (B, 84, 84, 4) NHWC float32, or its (B, 4, 84, 84) channels_last view.
-    Returns the (B, n_out) output buffer (overwritten by the next call)."""
+  def _nhwc(self, x):
     if x.dim() == 4 and x.shape[1] == self.in_ch and x.shape[-1] != self.in_ch:
       x = x.permute(0, 2, 3, 1)              # channels_last NCHW view -> NHWC
     assert x.shape == (self.B, 84, 84, 4) and x.is_contiguous() and x.dtype == torch.float32
+    return x
+
+  def forward(self, x):
+    """x: (B, 84, 84, 4) NHWC float32, or its (B, 4, 84, 84) channels_last view.
+    Returns the (B, n_out) output buffer (overwritten by the next call)."""
+    x = self._nhwc(x)
     self._x = x
     _lib.check(_lib.lib.dq_cnn_forward(ctypes.byref(self._p), self.B, x.data_ptr(),
                                        ctypes.byref(self._a), self.ws.data_ptr(), self._stream(x)),
@@ -132,3 +136,17 @@ class HipNatureCNN(object):
     ev[4].record(side)
     main.wait_event(ev[4])
     return self.net.fp.grad
+
+
+def forward_pair(a, xa, b, xb):
+  """``a.forward(xa)`` and ``b.forward(xb)`` (e.g. the online net on s and the
+  target net on s') in one pass: 6 grouped launches instead of 12, bitwise the
+  same outputs.  Returns the two output buffers."""
+  assert a.B == b.B and a is not b
+  xa, xb = a._nhwc(xa), b._nhwc(xb)
+  a._x, b._x = xa, xb
+  _lib.check(_lib.lib.dq_cnn_forward_pair(
+      ctypes.byref(a._p), xa.data_ptr(), ctypes.byref(a._a), a.ws.data_ptr(),
+      ctypes.byref(b._p), xb.data_ptr(), ctypes.byref(b._a), b.ws.data_ptr(), a.B,
+      a._stream(xa)), 'dq_cnn_forward_pair')
+  return a.acts['out'], b.acts['out']

@@ -24,6 +24,8 @@
 //
 // Activations are NHWC fp32; weights live in the flat parameter buffer as
 // conv (out, kh, kw, in) and FC (out, in) -- the GEMM's natural [M][K] layouts.
+#include <algorithm>
+
 #include "common.h"
 
 namespace dq {
@@ -561,7 +563,7 @@ constexpr int kGroupT = 1024;
 
 template <int WM, int WN, int WK, class AL, class BL, class EP>
 struct GemmOp {
-  static_assert(64 * WM * WN * WK == kGroupT, "grouped GEMMs use 16-wave blocks");
+  static constexpr int kT = 64 * WM * WN * WK;
   static constexpr int kLds = Tile<WM, WN, WK>::template lds<AL, BL>();
   AL a;
   BL b;
@@ -574,20 +576,22 @@ struct GemmOp {
   int blocks() const { return gx * gy * gz; }
 };
 
-template <class EP>
+template <class EP, int T = kGroupT>
 struct ReduceOp {                 // ordered split-K sum of nz slabs + epilogue
+  static constexpr int kT = T;
   static constexpr int kLds = 0;
   const float* ws;
   int nz, M, N;
   EP e;
   __device__ __forceinline__ void run(int blk, float*) const {
-    splitk_sum(ws, nz, M, N, e, (int64_t)blk * kGroupT + threadIdx.x);
+    splitk_sum(ws, nz, M, N, e, (int64_t)blk * T + threadIdx.x);
   }
-  int blocks() const { return (int)(((int64_t)M * N + kGroupT - 1) / kGroupT); }
+  int blocks() const { return (int)(((int64_t)M * N + T - 1) / T); }
 };
 
 template <class G>
 struct Col2imOp {
+  static constexpr int kT = kGroupT;
   static constexpr int kLds = 0;
   const float* dcol;
   const float* act;
@@ -597,6 +601,43 @@ struct Col2imOp {
     col2im_group<G>(dcol, act, dx, blk * kGroupT + threadIdx.x, total4);
   }
   int blocks() const { return (total4 + kGroupT - 1) / kGroupT; }
+};
+
+// TF1 Adam (the arithmetic of dq_adam_tf1) over a contiguous range of the flat
+// parameter buffer, float4 grid-stride: the optimizer rides in the backward's last
+// launch for every parameter whose gradient is final by then.
+struct AdamOp {
+  static constexpr int kT = kGroupT;
+  static constexpr int kLds = 0;
+  float* var;
+  const float* grad;
+  float* m;
+  float* v;
+  int64_t n;
+  AdamDev o;
+  int nb;
+  __device__ __forceinline__ void run(int blk, float*) const {
+    const float alpha = adam_alpha_of(o.state, o.slot, o.lr);
+    const float omb1 = __fsub_rn(1.0f, o.b1), omb2 = __fsub_rn(1.0f, o.b2);
+    const int64_t n4 = n >> 2, stride = (int64_t)nb * kT;
+    for (int64_t i = (int64_t)blk * kT + threadIdx.x; i < n4; i += stride) {
+      float4 p = reinterpret_cast<float4*>(var)[i];
+      const float4 g = reinterpret_cast<const float4*>(grad)[i];
+      float4 mm = reinterpret_cast<float4*>(m)[i], vv = reinterpret_cast<float4*>(v)[i];
+      adam1(p.x, g.x, mm.x, vv.x, alpha, omb1, omb2, o.eps);
+      adam1(p.y, g.y, mm.y, vv.y, alpha, omb1, omb2, o.eps);
+      adam1(p.z, g.z, mm.z, vv.z, alpha, omb1, omb2, o.eps);
+      adam1(p.w, g.w, mm.w, vv.w, alpha, omb1, omb2, o.eps);
+      reinterpret_cast<float4*>(var)[i] = p;
+      reinterpret_cast<float4*>(m)[i] = mm;
+      reinterpret_cast<float4*>(v)[i] = vv;
+    }
+    if (blk == 0 && threadIdx.x < (n & 3)) {
+      const int64_t i = (n4 << 2) + threadIdx.x;
+      adam1(var[i], grad[i], m[i], v[i], alpha, omb1, omb2, o.eps);
+    }
+  }
+  int blocks() const { return nb; }
 };
 
 template <class... Ops>
@@ -621,8 +662,8 @@ struct GroupArgs {
   int nblocks[sizeof...(Ops)];
 };
 
-template <class... Ops>
-__global__ __launch_bounds__(kGroupT) void k_grouped(GroupArgs<Ops...> g, Ops... ops) {
+template <int T, class... Ops>
+__global__ __launch_bounds__(T) void k_grouped(GroupArgs<Ops...> g, Ops... ops) {
   __shared__ __attribute__((aligned(16))) float smem[max_lds<Ops...>()];
   int blk = blockIdx.x, i = 0;
   ((dispatch(ops, g.nblocks[i++], blk, smem)) || ...);
@@ -679,13 +720,17 @@ GemmOp<WM, WN, WK, AL, BL, EP> gemm_op(AL a, BL b, EP e, int M, int N, int K, in
   return op;
 }
 
-template <class... Ops>
-void group(Ctx& c, Ops... ops) {
+template <class Op0, class... Ops>
+void group(Ctx& c, Op0 op0, Ops... ops) {
+  constexpr int T = Op0::kT;
+  static_assert(((Ops::kT == T) && ...), "grouped ops share one block size");
   if (c.dry) return;
-  GroupArgs<Ops...> g;
+  GroupArgs<Op0, Ops...> g;
   int i = 0, total = 0;
+  g.nblocks[i++] = op0.blocks();
+  total += op0.blocks();
   ((g.nblocks[i++] = ops.blocks(), total += ops.blocks()), ...);
-  hipLaunchKernelGGL((k_grouped<Ops...>), dim3(total), dim3(kGroupT), 0, c.s, g, ops...);
+  hipLaunchKernelGGL((k_grouped<T, Op0, Ops...>), dim3(total), dim3(T), 0, c.s, g, op0, ops...);
 }
 
 // Tile shapes: WM = WN = 1 with WK k-bands sized so K takes one or two slices
@@ -707,6 +752,57 @@ void forward(Ctx& c, const dq_cnn_params* p, int B, const float* x, dq_cnn_acts*
   // fc2 (512 -> n_out), no activation
   gemm<1, 1, 16>(c, RowK{a->h, kHidden}, RowK{p->fc2_w, kHidden},
                  EpiBiasAct{a->out, p->fc2_b, p->n_out, false}, B, p->n_out, kHidden);
+}
+
+// The online and target networks' forwards together: the same tiles and split
+// order as forward() (bitwise identical outputs), one grouped launch per layer
+// holding both nets' ops -- 6 launches instead of 12.
+void forward_pair(Ctx& c0, Ctx& c1, const dq_cnn_params* p0, const float* x0, dq_cnn_acts* a0,
+                  const dq_cnn_params* p1, const float* x1, dq_cnn_acts* a1, int B) {
+  constexpr int BK16 = 32 * 16;
+  const int ch = split_chunk(kFlat, kSplitFc1, BK16), nz = (kFlat + ch - 1) / ch;
+  const size_t need = (size_t)nz * B * kHidden;
+  c0.need = need > c0.need ? need : c0.need;
+  c1.need = need > c1.need ? need : c1.need;
+  if (c0.dry) return;
+  const dq_cnn_params* p[2] = {p0, p1};
+  const float* x[2] = {x0, x1};
+  dq_cnn_acts* a[2] = {a0, a1};
+  float* ws[2] = {c0.ws, c1.ws};
+  auto conv1 = [&](int i) {
+    return gemm_op<1, 1, 8>(Im2col<Conv1>{x[i]}, RowK{p[i]->conv1_w, Conv1::K},
+                            EpiBiasAct{a[i]->a1, p[i]->conv1_b, 32, true}, B * 441, 32, Conv1::K,
+                            Conv1::K);
+  };
+  auto conv2 = [&](int i) {
+    return gemm_op<1, 1, 16>(Im2col<Conv2>{a[i]->a1}, RowK{p[i]->conv2_w, Conv2::K},
+                             EpiBiasAct{a[i]->a2, p[i]->conv2_b, 64, true}, B * 121, 64, Conv2::K,
+                             Conv2::K);
+  };
+  auto conv3 = [&](int i) {
+    return gemm_op<1, 1, 9>(Im2col<Conv3>{a[i]->a2}, RowK{p[i]->conv3_w, Conv3::K},
+                            EpiBiasAct{a[i]->a3, p[i]->conv3_b, 64, true}, B * 121, 64, Conv3::K,
+                            Conv3::K);
+  };
+  auto fc1 = [&](int i) {
+    return gemm_op<1, 1, 16>(RowK{a[i]->a3, kFlat}, RowK{p[i]->fc1_w, kFlat},
+                             EpiPartial{ws[i], B, kHidden}, B, kHidden, kFlat, ch);
+  };
+  auto fc1_sum = [&](int i) {
+    return ReduceOp<EpiBiasAct, 256>{ws[i], nz, B, kHidden,
+                                     EpiBiasAct{a[i]->h, p[i]->fc1_b, kHidden, true}};
+  };
+  auto fc2 = [&](int i) {
+    return gemm_op<1, 1, 16>(RowK{a[i]->h, kHidden}, RowK{p[i]->fc2_w, kHidden},
+                             EpiBiasAct{a[i]->out, p[i]->fc2_b, p[i]->n_out, false}, B,
+                             p[i]->n_out, kHidden, kHidden);
+  };
+  group(c0, conv1(0), conv1(1));
+  group(c0, conv2(0), conv2(1));
+  group(c0, conv3(0), conv3(1));
+  group(c0, fc1(0), fc1(1));
+  group(c0, fc1_sum(0), fc1_sum(1));
+  group(c0, fc2(0), fc2(1));
 }
 
 // Backward of one layer: part 1 = weight/bias gradient, part 0 = input gradient.
@@ -766,9 +862,9 @@ bool backward_layer(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int 
 }
 
 // Backward in 7 grouped launches (13 kernels' worth of work; with kAdam also the
-// optimizer: each weight gradient's epilogue applies TF1 Adam, which is safe
-// because every layer's weights have had their last backward use (its input
-// gradient) in an EARLIER launch than the one that finalises its gradient):
+// optimizer, in the last launch: the conv1 split-K sum applies TF1 Adam in its
+// epilogue, and an AdamOp streams the contiguous conv2..fc2 range, whose
+// gradients are all final and whose weights have had their last use by then):
 //   1: dh                      (fc2 input grad)
 //   2: dW fc2     | da3        (fc1 input grad)
 //   3: dW fc1     | da2        (conv3 input grad)
@@ -798,12 +894,12 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
   auto dX_fc2 = gemm_op<1, 1, 16>(RowKScalar{dout, NO}, ColK{p->fc2_w, kHidden},
                                   EpiMask{d->h, a->h, kHidden}, B, kHidden, NO, NO);
   auto dW_fc2 = gemm_op<4, 4, 1>(ColKScalar{dout, NO}, ColKOnes{a->h, kHidden},
-                                 GE::make(g->fc2_w, g->fc2_b, kHidden, p->fc2_w, p->fc2_b, opt, 0),
+                                 EpiGrad{g->fc2_w, g->fc2_b, kHidden},
                                  NO, kHidden + 1, B, B);
   auto dX_fc1 = gemm_op<1, 1, 16>(RowK{d->h, kHidden}, ColK{p->fc1_w, kFlat},
                                   EpiMask{d->a3, a->a3, kFlat}, B, kFlat, kHidden, kHidden);
   auto dW_fc1 = gemm_op<4, 4, 1>(ColK{d->h, kHidden}, ColKOnes{a->a3, kFlat},
-                                 GE::make(g->fc1_w, g->fc1_b, kFlat, p->fc1_w, p->fc1_b, opt, 0),
+                                 EpiGrad{g->fc1_w, g->fc1_b, kFlat},
                                  kHidden, kFlat + 1, B, B);
   auto dX_c3 = gemm_op<1, 1, 16>(Col2im<Conv3>{d->a3}, WeightT<Conv3>{p->conv3_w},
                                  EpiMask{d->a2, a->a2, 64}, K3, 64, Conv3::K, Conv3::K);
@@ -811,15 +907,13 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
                                  EpiPartial{ws + o3, 64, Conv3::K + 1}, 64, Conv3::K + 1, K3, ch3);
   auto dcol = gemm_op<4, 4, 1>(RowK{d->a2, 64}, ColK{p->conv2_w, Conv2::K},
                                EpiStore{ws + od, Conv2::K}, K3, Conv2::K, 64, 64);
-  auto sum_c3 = ReduceOp<decltype(GE::make(0, 0, 0, 0, 0, opt, 0))>{
-      ws + o3, nz3, 64, Conv3::K + 1,
-      GE::make(g->conv3_w, g->conv3_b, Conv3::K, p->conv3_w, p->conv3_b, opt, 0)};
+  auto sum_c3 = ReduceOp<EpiGrad>{ws + o3, nz3, 64, Conv3::K + 1,
+                                  EpiGrad{g->conv3_w, g->conv3_b, Conv3::K}};
   auto dW_c2 = gemm_op<1, 1, 16>(DyT<64>{d->a2}, Im2colT<Conv2>{a->a1},
                                  EpiPartial{ws + o2, 64, Conv2::K + 1}, 64, Conv2::K + 1, K3, ch3);
   auto da1 = Col2imOp<Conv2>{ws + od, a->a1, d->a1, B * 441 * 32 / 4};
-  auto sum_c2 = ReduceOp<decltype(GE::make(0, 0, 0, 0, 0, opt, 0))>{
-      ws + o2, nz3, 64, Conv2::K + 1,
-      GE::make(g->conv2_w, g->conv2_b, Conv2::K, p->conv2_w, p->conv2_b, opt, 0)};
+  auto sum_c2 = ReduceOp<EpiGrad>{ws + o2, nz3, 64, Conv2::K + 1,
+                                  EpiGrad{g->conv2_w, g->conv2_b, Conv2::K}};
   auto dW_c1 = gemm_op<1, 1, 16>(DyT<32>{d->a1}, Im2colT<Conv1>{x},
                                  EpiPartial{ws + o1, 32, Conv1::K + 1}, 32, Conv1::K + 1, K1, ch1);
   auto sum_c1 = ReduceOp<decltype(GE::make(0, 0, 0, 0, 0, opt, 0))>{
@@ -831,7 +925,18 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
   group(c, dW_c3, dcol);
   group(c, sum_c3, dW_c2, da1);
   group(c, sum_c2, dW_c1);
-  group(c, sum_c1);
+  if constexpr (kAdam) {
+    const dq_adam_args* o = opt.a;
+    float* w0 = p->conv2_w;
+    const ptrdiff_t off = w0 - o->var;
+    const int64_t n = (int64_t)((p->fc2_b + NO) - w0);
+    const int nb = (int)std::max<int64_t>(1, ((n >> 2) + kGroupT - 1) / kGroupT);  // 1 float4 / thread
+    AdamOp rest{w0, g->conv2_w, o->m + off, o->v + off, n,
+                AdamDev{o->state, o->slot, o->lr, o->beta1, o->beta2, o->epsilon}, nb};
+    group(c, sum_c1, rest);
+  } else {
+    group(c, sum_c1);
+  }
 }
 
 }  // namespace cnn
@@ -849,6 +954,19 @@ int dq_cnn_forward(const dq_cnn_params* p, int32_t batch, const float* x, dq_cnn
   Ctx c{(hipStream_t)stream, ws, false, 0};
   forward(c, p, batch, x, a);
   DQ_CHECK_LAUNCH("dq_cnn_forward");
+  return DQ_OK;
+}
+
+int dq_cnn_forward_pair(const dq_cnn_params* p0, const float* x0, dq_cnn_acts* a0, float* ws0,
+                        const dq_cnn_params* p1, const float* x1, dq_cnn_acts* a1, float* ws1,
+                        int32_t batch, void* stream) {
+  DQ_CHECK_ARG(p0 && a0 && x0 && ws0 && p1 && a1 && x1 && ws1 && batch >= 1, "null argument");
+  DQ_CHECK_ARG(p0->in_channels == 4 && p1->in_channels == 4 && p0->n_out >= 1 && p1->n_out >= 1,
+               "the Nature CNN takes 84x84x4 NHWC input");
+  DQ_CHECK_ARG(ws0 != ws1, "the two networks need separate workspaces");
+  Ctx c0{(hipStream_t)stream, ws0, false, 0}, c1{(hipStream_t)stream, ws1, false, 0};
+  forward_pair(c0, c1, p0, x0, a0, p1, x1, a1, batch);
+  DQ_CHECK_LAUNCH("dq_cnn_forward_pair");
   return DQ_OK;
 }
 
@@ -872,8 +990,16 @@ int dq_cnn_backward_adam(const dq_cnn_params* p, const dq_cnn_params* g, int32_t
                "adam args: var, m, v, state and slot 0/1 required");
   const float* w[10] = {p->conv1_w, p->conv1_b, p->conv2_w, p->conv2_b, p->conv3_w,
                         p->conv3_b, p->fc1_w,  p->fc1_b,  p->fc2_w,  p->fc2_b};
-  for (const float* q : w)
-    DQ_CHECK_ARG(q >= opt->var, "parameters must live in the flat buffer opt->var");
+  const float* gw[10] = {g->conv1_w, g->conv1_b, g->conv2_w, g->conv2_b, g->conv3_w,
+                         g->conv3_b, g->fc1_w,  g->fc1_b,  g->fc2_w,  g->fc2_b};
+  for (int i = 0; i < 10; ++i) {
+    DQ_CHECK_ARG(w[i] >= opt->var && (i == 0 || w[i] > w[i - 1]),
+                 "parameters must live in the flat buffer opt->var in conv1..fc2 order");
+    DQ_CHECK_ARG(gw[i] - g->conv1_w == w[i] - p->conv1_w,
+                 "gradients must have the parameters' flat layout");
+  }
+  DQ_CHECK_ARG(((p->conv2_w - opt->var) & 3) == 0 && ((g->conv2_w - g->conv1_w) & 3) == 0,
+               "16-byte aligned parameter views required");
   Ctx c{(hipStream_t)stream, ws, false, 0};
   backward_grouped<true>(c, p, g, batch, x, a, dout, d, AdamHost{opt});
   DQ_CHECK_LAUNCH("dq_cnn_backward_adam");

@@ -219,6 +219,11 @@ int dq_cnn_forward(const dq_cnn_params* p, int32_t batch, const float* x, dq_cnn
                    float* ws, void* stream);
 /* backward from d out (B, n_out): writes EVERY weight/bias gradient into g (plain stores,
  * no accumulation); d holds the intermediate activation gradients. */
+/* two forwards in one pass (the online net on s and the target net on s', say): the same
+   results as two dq_cnn_forward calls, bit for bit, in half the launches. */
+int dq_cnn_forward_pair(const dq_cnn_params* p0, const float* x0, dq_cnn_acts* a0, float* ws0,
+                        const dq_cnn_params* p1, const float* x1, dq_cnn_acts* a1, float* ws1,
+                        int32_t batch, void* stream);
 int dq_cnn_backward(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch, const float* x,
                     const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d, float* ws,
                     void* stream);

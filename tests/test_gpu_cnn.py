@@ -98,3 +98,18 @@ def test_fused_adam_backward_equals_backward_then_adam():
       assert torch.equal(a, b)
     for n in ('params', 'm', 'v', 'state'):
       assert torch.equal(getattr(opts[0], n), getattr(opts[1], n)), (step, n)
+
+
+@pytest.mark.parametrize('B', [32, 7])
+def test_forward_pair_equals_two_forwards(B):
+  from dopamine_amd.agents.networks import RainbowNetwork
+  from dopamine_amd.cnn import HipNatureCNN, forward_pair
+  on, tg = RainbowNetwork(9, device='cuda', seed=1), RainbowNetwork(9, device='cuda', seed=2)
+  ho, ht = HipNatureCNN(on, B), HipNatureCNN(tg, B)
+  x, nx = torch.rand(B, 84, 84, 4, device='cuda'), torch.rand(B, 84, 84, 4, device='cuda')
+  ref_o, ref_t = ho.forward(x).clone(), ht.forward(nx).clone()
+  ho.acts['out'].zero_()
+  ht.acts['out'].zero_()
+  yo, yt = forward_pair(ho, x, ht, nx)
+  torch.cuda.synchronize()
+  assert torch.equal(yo, ref_o) and torch.equal(yt, ref_t)
