@@ -132,6 +132,18 @@ def time_gather_large(agent, batch=1024, iters=50):
           'frac': round(algo / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
+def gather_traffic(batch):
+  """HBM bytes per gather launch from the committed PMC passes (rocprofv3 --pmc
+  FETCH_SIZE / WRITE_SIZE, calibrated as MI355X_MICROARCH.md prescribes;
+  tools/gather_traffic.py, profiles/r1_gather_traffic.json), or None."""
+  path = os.path.join(ROOT, 'profiles', 'r1_gather_traffic.json')
+  try:
+    d = json.load(open(path))
+    return round(float(d['traffic_bytes_per_launch'][str(batch)])), os.path.relpath(path, ROOT)
+  except (OSError, KeyError, ValueError):
+    return None, None
+
+
 def cpu_baseline(seconds, A, batch):
   from oracle.cpu_step import CpuRainbowStep
   threads = min(16, os.cpu_count() or 1)
@@ -199,6 +211,7 @@ def main():
 
   graph_us, eager_us, algo_bytes, gname = time_gather(agent, args.gather_iters)
   large = time_gather_large(agent)
+  traffic, traffic_src = gather_traffic(args.batch)
   achieved = algo_bytes / (graph_us * 1e-6) / 1e9
 
   cpu = None
@@ -221,7 +234,8 @@ def main():
         'roofline': {'kernel': gname + ' (frame-stack gather + /255, state+next_state)',
                      'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
                      'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4),
-                     'traffic': None, 'algo_bytes_per_launch': algo_bytes,
+                     'traffic': traffic, 'traffic_source': traffic_src,
+                     'algo_bytes_per_launch': algo_bytes,
                      'avg_launch_us': round(graph_us, 3), 'avg_launch_us_eager': round(eager_us, 3),
                      'same_kernel_batch_1024': large},
         'cpu_baseline': cpu,
