@@ -1,0 +1,97 @@
+"""The agent's multi-learner path end to end (BASELINE config 4's schedule:
+graph replays around the gradient all-reduce), exercised on ONE GPU with two
+ranks sharing cuda:0 over gloo (which all-reduces CUDA tensors).
+
+* identical seeds on both ranks: the mean gradient equals each rank's own
+  ((g + g) / 2 is exact in fp32), so after K steps the parameters must equal a
+  single-process agent's BIT FOR BIT -- this pins the whole N > 1 schedule;
+* different seeds: the replicas stay bit-identical (checksum broadcast)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+STEPS = 12
+CAP = 30000
+
+
+def _agent(pg, seed):
+  from dopamine_amd.agents.optimizers import AdamOptimizer
+  from dopamine_amd.agents.rainbow.rainbow_agent import RainbowAgent
+  import bench
+  import random
+  agent = RainbowAgent(num_actions=9, update_horizon=3, gamma=0.99, replay_scheme='prioritized',
+                       min_replay_history=100, update_period=4, target_update_period=40,
+                       optimizer=AdamOptimizer(learning_rate=6.25e-5, epsilon=1.5e-4),
+                       replay_capacity=CAP, batch_size=32, device=torch.device('cuda', 0),
+                       seed=0, process_group=pg)
+  random.seed(seed)
+  bench.fill_synthetic(agent._replay.memory, 9, seed=1 + seed)
+  return agent
+
+
+def _run(agent):
+  for _ in range(STEPS):
+    for _ in range(agent.update_period):
+      agent._train_step()
+  torch.cuda.synchronize()
+  return agent.online_convnet.fp.flat.detach().cpu().clone()
+
+
+def _worker(rank, world, port, same_seed, q):
+  import sys
+  sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+  import torch.distributed as dist
+  os.environ['MASTER_ADDR'] = '127.0.0.1'
+  os.environ['MASTER_PORT'] = str(port)
+  torch.cuda.set_device(0)
+  dist.init_process_group('gloo', rank=rank, world_size=world)
+  from dopamine_amd import parallel
+  agent = _agent(dist.group.WORLD, 0 if same_seed else rank)
+  flat = _run(agent)
+  ok = parallel.replicas_in_sync(agent.online_convnet.fp.flat)
+  if rank == 0:
+    q.put((ok, flat.numpy()))
+  dist.barrier()
+  dist.destroy_process_group()
+
+
+def _free_port():
+  s = socket.socket()
+  s.bind(('127.0.0.1', 0))
+  p = s.getsockname()[1]
+  s.close()
+  return p
+
+
+def _two_ranks(same_seed):
+  ctx = mp.get_context('spawn')
+  q = ctx.Queue()
+  port = _free_port()
+  procs = [ctx.Process(target=_worker, args=(r, 2, port, same_seed, q)) for r in range(2)]
+  for p in procs:
+    p.start()
+  ok, flat = q.get(timeout=400)
+  for p in procs:
+    p.join(timeout=120)
+    assert p.exitcode == 0
+  return ok, flat
+
+
+@pytest.mark.timeout(600)
+def test_two_ranks_same_seed_equal_single_learner_bitwise():
+  ok, flat = _two_ranks(same_seed=True)
+  assert ok
+  single = _run(_agent(None, 0)).numpy()
+  assert np.array_equal(flat, single)
+
+
+@pytest.mark.timeout(600)
+def test_two_ranks_different_seeds_stay_in_sync():
+  ok, _ = _two_ranks(same_seed=False)
+  assert ok
