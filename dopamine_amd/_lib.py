@@ -99,6 +99,9 @@ SIGNATURES = {
     'dq_cnn_backward_adam': [ctypes.POINTER(CnnParams), ctypes.POINTER(CnnParams), _I32, _P,
                              ctypes.POINTER(CnnActs), _P, ctypes.POINTER(CnnActs), _P,
                              ctypes.POINTER(AdamArgs), _P],
+    'dq_cnn_backward_groups': [ctypes.POINTER(CnnParams), ctypes.POINTER(CnnParams), _I32, _P,
+                               ctypes.POINTER(CnnActs), _P, ctypes.POINTER(CnnActs), _P, _I32,
+                               _I32, _P],
     'dq_cnn_backward_layer': [ctypes.POINTER(CnnParams), ctypes.POINTER(CnnParams), _I32, _P,
                               ctypes.POINTER(CnnActs), _P, ctypes.POINTER(CnnActs), _P, _I32, _I32,
                               _P],

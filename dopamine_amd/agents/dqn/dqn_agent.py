@@ -142,6 +142,7 @@ class DQNAgent(object):
       self._opt = self.optimizer.build(self.online_convnet.fp.flat,
                                        segments=self.online_convnet.fp.segments())
       self._side = torch.cuda.Stream(self._device)
+      self._comm = torch.cuda.Stream(self._device)
     self._observation = None
     self._last_observation = None
     self.last_loss = None
@@ -305,6 +306,61 @@ class DQNAgent(object):
       self._post_loss(self._pbuf[c])
       self._backward(y, g, k)
 
+  # Data-parallel learners (N > 1) with the HIP CNN: the gradient all-reduce is
+  # bucketed and overlapped.  The backward's first _SPLIT grouped launches leave
+  # fc1/fc2's gradients final (93% of the 17.1 MB); their all-reduce runs on a
+  # comm stream while the prefetch branch and the remaining launches run, then
+  # the conv bucket is all-reduced and the optimizer applied.  Three graphs per
+  # step parity: head | tail | optimizer, the collectives between them.
+  _SPLIT = 3
+
+  def _split_allreduce(self):
+    return self._pg is not None and self._hip is not None and not self._fused_opt()
+
+  def _grad_step_head(self, c, k):
+    if not self.pipeline:
+      self._prefetch(c)
+    if self._pairs():
+      self._forward_pair(c)
+    y, g = self._online_loss(self._pbuf[c], self._ptgt[c])
+    self._hip['online'].backward(g, groups=(0, self._SPLIT))
+    self._dout = g
+
+  def _grad_step_tail(self, c, k):
+    g = self._dout
+    if self.pipeline:
+      main = torch.cuda.current_stream(self._device)
+      ev = torch.cuda.Event()
+      ev.record(main)
+      self._side.wait_event(ev)
+      with torch.cuda.stream(self._side):
+        self._post_loss(self._pbuf[c])
+        self._prefetch(1 - c)
+      self._hip['online'].backward(g, groups=(self._SPLIT, 7))
+      main.wait_stream(self._side)
+    else:
+      self._post_loss(self._pbuf[c])
+      self._hip['online'].backward(g, groups=(self._SPLIT, 7))
+
+  def _grad_buckets(self):
+    fp = self.online_convnet.fp
+    o = fp.offsets['fc1_w'][0]
+    return fp.grad[o:], fp.grad[:o]           # fc1 + fc2 (final after the head), convs
+
+  def _split_step(self, head, tail, opt):
+    main = torch.cuda.current_stream(self._device)
+    fc, conv = self._grad_buckets()
+    head()
+    ev = torch.cuda.Event()
+    ev.record(main)
+    self._comm.wait_event(ev)
+    with torch.cuda.stream(self._comm):
+      parallel.allreduce_mean_(fc, self._pg)
+    tail()
+    parallel.allreduce_mean_(conv, self._pg)
+    main.wait_stream(self._comm)
+    opt()
+
   def _post_loss(self, t):
     """Work that needs the loss but not the gradient (PER priority write-back)."""
 
@@ -338,7 +394,14 @@ class DQNAgent(object):
         mem.reserve_rng(self._batch_size)
         self._prefetch(c)
     mem.reserve_rng(self._batch_size)
-    if self._graphs is not None:
+    if self._split_allreduce():
+      if self._graphs is not None:
+        self._split_step(*[g.replay for g in self._graphs[k]])
+      else:
+        self._split_step(lambda: self._grad_step_head(c, k), lambda: self._grad_step_tail(c, k),
+                         lambda: self._device_opt_step(k))
+        self._eager_steps += 1
+    elif self._graphs is not None:
       self._graphs[k].replay()
       if self._pg is not None:
         self._allreduce_grads()
@@ -364,6 +427,19 @@ class DQNAgent(object):
     same graph, with N GPUs it is a second graph after the RCCL all-reduce."""
     torch.cuda.synchronize(self._device)
     graphs, graphs_opt, pool = [], [], None
+    if self._split_allreduce():
+      for k in (0, 1):
+        c = k if self.pipeline else 0
+        parts = [torch.cuda.CUDAGraph() for _ in range(3)]
+        fns = (lambda: self._grad_step_head(c, k), lambda: self._grad_step_tail(c, k),
+               lambda: self._device_opt_step(k))
+        for gr, fn in zip(parts, fns):
+          with torch.cuda.graph(gr, pool=pool):
+            fn()
+          pool = gr.pool()
+        graphs.append(parts)
+      self._graphs, self._graphs_opt = graphs, []
+      return
     for k in (0, 1):
       c = k if self.pipeline else 0
       g = torch.cuda.CUDAGraph()

@@ -79,8 +79,11 @@ class HipNatureCNN(object):
                'dq_cnn_forward')
     return self.acts['out']
 
-  def backward(self, dout, parallel=False, adam=None, slot=0):
+  def backward(self, dout, parallel=False, adam=None, slot=0, groups=None):
     """dout: (B, n_out).  Writes all parameter gradients into net.fp.grad.
+
+    groups=(first, last): only launches [first, last) of the 7 grouped launches
+    (a data-parallel learner all-reduces fc1/fc2's gradients after launch 3).
 
     adam: an ops.TF1Adam over net.fp.flat -- its step (beta-power slot ``slot``)
     is applied inside the gradient epilogues (dq_cnn_backward_adam), so no
@@ -95,6 +98,12 @@ class HipNatureCNN(object):
     with the other stream's.  Kept for experimentation; off by default."""
     dout = dout.reshape(self.B, self.n_out)
     assert dout.is_contiguous() and self._x is not None
+    if groups is not None:          # a sub-range of the 7 grouped launches
+      _lib.check(_lib.lib.dq_cnn_backward_groups(
+          ctypes.byref(self._p), ctypes.byref(self._g), self.B, self._x.data_ptr(),
+          ctypes.byref(self._a), dout.data_ptr(), ctypes.byref(self._d), self.ws.data_ptr(),
+          int(groups[0]), int(groups[1]), self._stream(dout)), 'dq_cnn_backward_groups')
+      return self.net.fp.grad
     if adam is not None:
       assert adam.params.data_ptr() == self.net.fp.flat.data_ptr(), 'adam must own net.fp.flat'
       args = _lib.AdamArgs(var=adam.params.data_ptr(), m=adam.m.data_ptr(), v=adam.v.data_ptr(),

@@ -877,7 +877,7 @@ bool backward_layer(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int 
 template <bool kAdam>
 void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int B,
                       const float* x, const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d,
-                      const AdamHost& opt) {
+                      const AdamHost& opt, int first = 0, int last = 7) {
   const int NO = p->n_out;
   using GE = GradEpi<kAdam>;
   using W16 = Tile<1, 1, 16>;
@@ -919,12 +919,14 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
   auto sum_c1 = ReduceOp<decltype(GE::make(0, 0, 0, 0, 0, opt, 0))>{
       ws + o1, nz1, 32, Conv1::K + 1,
       GE::make(g->conv1_w, g->conv1_b, Conv1::K, p->conv1_w, p->conv1_b, opt, 1)};
-  group(c, dX_fc2);
-  group(c, dW_fc2, dX_fc1);
-  group(c, dW_fc1, dX_c3);
-  group(c, dW_c3, dcol);
-  group(c, sum_c3, dW_c2, da1);
-  group(c, sum_c2, dW_c1);
+  auto in = [&](int i) { return first <= i && i < last; };
+  if (in(0)) group(c, dX_fc2);
+  if (in(1)) group(c, dW_fc2, dX_fc1);
+  if (in(2)) group(c, dW_fc1, dX_c3);
+  if (in(3)) group(c, dW_c3, dcol);
+  if (in(4)) group(c, sum_c3, dW_c2, da1);
+  if (in(5)) group(c, sum_c2, dW_c1);
+  if (!in(6)) return;
   if constexpr (kAdam) {
     const dq_adam_args* o = opt.a;
     float* w0 = p->conv2_w;
@@ -1003,6 +1005,18 @@ int dq_cnn_backward_adam(const dq_cnn_params* p, const dq_cnn_params* g, int32_t
   Ctx c{(hipStream_t)stream, ws, false, 0};
   backward_grouped<true>(c, p, g, batch, x, a, dout, d, AdamHost{opt});
   DQ_CHECK_LAUNCH("dq_cnn_backward_adam");
+  return DQ_OK;
+}
+
+int dq_cnn_backward_groups(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch,
+                           const float* x, const dq_cnn_acts* a, const float* dout,
+                           dq_cnn_acts* d, float* ws, int32_t first, int32_t last, void* stream) {
+  DQ_CHECK_ARG(p && g && a && d && x && dout && ws && batch >= 1, "null argument");
+  DQ_CHECK_ARG(p->in_channels == 4 && p->n_out >= 1, "the Nature CNN takes 84x84x4 NHWC input");
+  DQ_CHECK_ARG(0 <= first && first <= last && last <= 7, "groups must satisfy 0 <= first <= last <= 7");
+  Ctx c{(hipStream_t)stream, ws, false, 0};
+  backward_grouped<false>(c, p, g, batch, x, a, dout, d, AdamHost{nullptr}, first, last);
+  DQ_CHECK_LAUNCH("dq_cnn_backward_groups");
   return DQ_OK;
 }
 

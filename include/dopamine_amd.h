@@ -241,6 +241,12 @@ typedef struct dq_adam_args {
 int dq_cnn_backward_adam(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch,
                          const float* x, const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d,
                          float* ws, const dq_adam_args* opt, void* stream);
+/* launches [first, last) of dq_cnn_backward's 7 grouped launches (the full call is [0, 7)):
+   after launch 3 the fc1 / fc2 weight gradients are final, so a data-parallel learner can
+   start their all-reduce while launches 3..6 run.  Bitwise the same results. */
+int dq_cnn_backward_groups(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch,
+                           const float* x, const dq_cnn_acts* a, const float* dout,
+                           dq_cnn_acts* d, float* ws, int32_t first, int32_t last, void* stream);
 /* one layer of the backward: layer 0..4 = fc2, fc1, conv3, conv2, conv1; part 1 = weight and
    bias gradient, part 0 = input gradient (not for conv1).  dW(L) depends only on dX(L-1),
    so the weight gradients may run on a second stream, each with its own ws. */
