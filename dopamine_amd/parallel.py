@@ -18,6 +18,9 @@ def allreduce_mean_(flat_grad, group=None):
   world = dist.get_world_size(group)
   if world == 1:
     return flat_grad
+  if dist.get_backend(group) == 'nccl':     # RCCL averages in the collective (no extra kernel)
+    dist.all_reduce(flat_grad, op=dist.ReduceOp.AVG, group=group)
+    return flat_grad
   dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, group=group)
   flat_grad.mul_(1.0 / world)
   return flat_grad
