@@ -26,6 +26,7 @@
 // conv (out, kh, kw, in) and FC (out, in) -- the GEMM's natural [M][K] layouts.
 #include <algorithm>
 
+
 #include "common.h"
 
 namespace dq {
