@@ -51,6 +51,11 @@ class ImplicitQuantileAgent(rainbow_agent.RainbowAgent):
     self._loss_out = dict(grad=torch.empty((self.num_tau_samples * B, A), device=dev),
                           loss=torch.empty(B, device=dev), mean_loss=torch.empty(1, device=dev))
 
+  def _post_loss(self, t):
+    """No priority write-back: the reference IQN's train op never calls
+    set_priority (iqn:314, "TODO: Add prioritized replay functionality"), so with
+    replay_scheme='prioritized' the stored priorities are the insert-time ones."""
+
   def _online_q(self, x):
     qv, _ = self.online_convnet(x, self.num_quantile_samples)
     return qv.view(self.num_quantile_samples, x.shape[0], -1).mean(0)

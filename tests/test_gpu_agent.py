@@ -119,3 +119,21 @@ def test_pipelined_prefetch_is_invalidated_by_adds_and_host_draws():
   np.testing.assert_array_equal(res[0][0], res[1][0])
   assert res[0][1] == res[1][1]
   np.testing.assert_allclose(res[0][2], res[1][2], rtol=1e-5, atol=1e-7)
+
+
+def test_iqn_with_prioritized_replay_keeps_insert_priorities():
+  """IQN inherits Rainbow's replay_scheme default ('prioritized'); its train op
+  never writes priorities back (iqn:314), so training must run and leave the
+  sum tree's leaves untouched."""
+  from dopamine_amd.agents.implicit_quantile.implicit_quantile_agent import ImplicitQuantileAgent
+  random.seed(2); np.random.seed(2); torch.manual_seed(2)
+  a = ImplicitQuantileAgent(num_actions=4, replay_capacity=3000, batch_size=16, num_tau_samples=8,
+                            num_tau_prime_samples=8, num_quantile_samples=4, min_replay_history=100,
+                            update_horizon=3)
+  _fill(a._replay.memory, a.num_actions, 3)
+  before = a._replay.memory.sum_tree.nodes[-1].copy()
+  for _ in range(6):
+    a._run_train_op()
+  a._replay.memory.sync_rng()
+  np.testing.assert_array_equal(a._replay.memory.sum_tree.nodes[-1], before)
+  assert np.isfinite(a.mean_loss())

@@ -1,0 +1,70 @@
+"""Gradient-steps/s for the other single-GPU BASELINE configs, measured like
+bench.py (synthetic full 1M-transition buffer in HBM, HIP graph, the reference's
+_train_step cadence), for DESIGN.md -- not the bench line:
+
+  config 2: DQN / Pong   -- 6 actions, uniform replay, n = 1, TF1 centered RMSProp, B = 32
+  config 5: IQN / Breakout -- 4 actions, n = 3, Adam, B = 64 (quantile-Huber kernel)
+
+    python tools/bench_configs.py [steps]
+"""
+import gc
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault('HIP_FORCE_DEV_KERNARG', '1')
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+
+
+def measure(make, actions, steps, warmup=20):
+  agent = make()
+  import random
+  random.seed(0)
+  bench.fill_synthetic(agent._replay.memory, actions, seed=1)
+  torch.cuda.synchronize()
+
+  def grad_step():
+    for _ in range(agent.update_period):
+      agent._train_step()
+
+  for _ in range(warmup):
+    grad_step()
+  torch.cuda.synchronize()
+  t0 = time.perf_counter()
+  for _ in range(steps):
+    grad_step()
+  torch.cuda.synchronize()
+  dt = time.perf_counter() - t0
+  agent._replay.memory.sync_rng()
+  out = {'steps_per_s': round(steps / dt, 1), 'ms_per_step': round(1e3 * dt / steps, 4),
+         'batch': agent._batch_size, 'hip_cnn': agent._hip is not None}
+  del agent
+  gc.collect()
+  torch.cuda.empty_cache()
+  return out
+
+
+def main():
+  steps = int(sys.argv[1]) if len(sys.argv) > 1 else 300
+  dev = torch.device('cuda', 0)
+  from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
+  from dopamine_amd.agents.implicit_quantile.implicit_quantile_agent import ImplicitQuantileAgent
+  res = {}
+  res['dqn_pong'] = measure(lambda: DQNAgent(num_actions=6, min_replay_history=20000,
+                                             update_period=4, target_update_period=8000,
+                                             replay_capacity=1_000_000, batch_size=32,
+                                             device=dev), 6, steps)
+  res['iqn_breakout'] = measure(lambda: ImplicitQuantileAgent(
+      num_actions=4, update_horizon=3, replay_scheme='uniform',   # implicit_quantile.gin:24
+      min_replay_history=20000, update_period=4,
+      target_update_period=8000, replay_capacity=1_000_000, batch_size=64, device=dev), 4,
+      max(steps // 3, 50))
+  print(json.dumps(res))
+
+
+if __name__ == '__main__':
+  main()
