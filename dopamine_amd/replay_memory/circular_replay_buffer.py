@@ -28,7 +28,7 @@ STORE_FILENAME_PREFIX = '$store$_'
 CHECKPOINT_DURATION = 4
 
 
-class NotFoundError(IOError):
+class NotFoundError(FileNotFoundError):
   """Stands in for ``tf.errors.NotFoundError`` (same constructor), raised by
   ``load`` when a checkpoint file is missing (crb:671-673)."""
 
@@ -409,7 +409,11 @@ class OutOfGraphReplayBuffer(object):
       if layout == _lib.LAYOUT_F32_NHWC:   # (B, H, W, S) memory viewed as channels_last NCHW
         nhwc = torch.empty((B,) + tuple(self._observation_shape) + (S,), dtype=torch.float32, device=dev)
         return nhwc.permute(0, 3, 1, 2)
-      return torch.empty((B, S, self._obs_bytes), dtype=torch.uint8, device=dev)
+      raw = torch.empty((B, S, self._obs_bytes), dtype=torch.uint8, device=dev)
+      if np.dtype(self._observation_dtype) != np.uint8:   # typed view of the gathered bytes
+        return raw.view(_torch_dtype(self._observation_dtype)).reshape(
+            (B, S) + tuple(self._observation_shape))
+      return raw
 
     out = {'state': states(),
            'next_state': states(),
