@@ -121,9 +121,11 @@ class DQNAgent(object):
     self.use_hip_cnn = use_hip_cnn
     self.fuse_optimizer = fuse_optimizer
     self.pair_forward = pair_forward
-    self._graphs = None
-    self._graphs_opt = None
-    self._eager_steps = 0
+    self._graph_sets = {}          # pipe -> (graphs per parity, optimizer graphs per parity)
+    self._graph_pool = None
+    self._eager_steps = {True: 0, False: 0}
+    self._last_train_add_count = -1
+    self._selects_since_train = 0
     self._opt_steps = 0
     self._slot = 0
     self._pbuf = [None, None]
@@ -286,13 +288,14 @@ class DQNAgent(object):
     for k, v in tg.items():
       self._ptgt[i][k].copy_(v)
 
-  def _grad_step(self, c, k=0):
-    if not self.pipeline:
+  def _grad_step(self, c, k=0, pipe=None):
+    pipe = self.pipeline if pipe is None else pipe
+    if not pipe:
       self._prefetch(c)
     if self._pairs():
       self._forward_pair(c)
     y, g = self._online_loss(self._pbuf[c], self._ptgt[c])
-    if self.pipeline:
+    if pipe:
       main = torch.cuda.current_stream(self._device)
       ev = torch.cuda.Event()
       ev.record(main)
@@ -317,8 +320,9 @@ class DQNAgent(object):
   def _split_allreduce(self):
     return self._pg is not None and self._hip is not None and not self._fused_opt()
 
-  def _grad_step_head(self, c, k):
-    if not self.pipeline:
+  def _grad_step_head(self, c, k, pipe=None):
+    pipe = self.pipeline if pipe is None else pipe
+    if not pipe:
       self._prefetch(c)
     if self._pairs():
       self._forward_pair(c)
@@ -326,9 +330,10 @@ class DQNAgent(object):
     self._hip['online'].backward(g, groups=(0, self._SPLIT))
     self._dout = g
 
-  def _grad_step_tail(self, c, k):
+  def _grad_step_tail(self, c, k, pipe=None):
+    pipe = self.pipeline if pipe is None else pipe
     g = self._dout
-    if self.pipeline:
+    if pipe:
       main = torch.cuda.current_stream(self._device)
       ev = torch.cuda.Event()
       ev.record(main)
@@ -383,68 +388,91 @@ class DQNAgent(object):
       self._replay.memory.rewind_last_sample()
       self._has_prefetch = False
 
+  # The prefetch of step t+1 (drawn right after step t's priority write-back) is
+  # only usable if nothing touches the replay RNG stream or the buffer before
+  # step t+1 -- true for a learner-only loop (the benchmark), never for an agent
+  # acting in an environment, where add() and (with PER) epsilon-greedy draws
+  # come between steps.  Such steps use a second, non-pipelined graph family
+  # instead of prefetching work that would be thrown away.
+  def _interleaved(self):
+    mem = self._replay.memory
+    if int(mem.add_count) != self._last_train_add_count:
+      return True
+    return self._selects_since_train > 0 and mem._rng.stream is random
+
   def _run_train_op(self):
     """One gradient step (the body of sess.run(self._train_op))."""
     mem = self._replay.memory
-    c, k = self._slot, self._opt_steps % 2
-    if self.pipeline:
-      if self._has_prefetch and self._prefetch_add_count != int(mem.add_count):
-        self._discard_prefetch()          # transitions were added after the prefetch
-      if not self._has_prefetch:
-        mem.reserve_rng(self._batch_size)
-        self._prefetch(c)
+    k = self._opt_steps % 2
+    c = k                                 # pipeline slot == step parity (graphs bake it in)
+    pipe = self.pipeline and not self._interleaved()
+    if self._has_prefetch and (not pipe or self._prefetch_add_count != int(mem.add_count)):
+      self._discard_prefetch()            # transitions were added after the prefetch
+    if pipe and not self._has_prefetch:
+      mem.reserve_rng(self._batch_size)
+      self._prefetch(c)
     mem.reserve_rng(self._batch_size)
+    graphs = self._graph_sets.get(pipe)
     if self._split_allreduce():
-      if self._graphs is not None:
-        self._split_step(*[g.replay for g in self._graphs[k]])
+      if graphs is not None:
+        self._split_step(*[g.replay for g in graphs[0][k]])
       else:
-        self._split_step(lambda: self._grad_step_head(c, k), lambda: self._grad_step_tail(c, k),
+        self._split_step(lambda: self._grad_step_head(c, k, pipe),
+                         lambda: self._grad_step_tail(c, k, pipe),
                          lambda: self._device_opt_step(k))
-        self._eager_steps += 1
-    elif self._graphs is not None:
-      self._graphs[k].replay()
+        self._eager_steps[pipe] += 1
+    elif graphs is not None:
+      graphs[0][k].replay()
       if self._pg is not None:
         self._allreduce_grads()
-        self._graphs_opt[k].replay()
+        graphs[1][k].replay()
     else:
-      self._grad_step(c, k)
+      self._grad_step(c, k, pipe)
       self._allreduce_grads()
       self._device_opt_step(k)
-      self._eager_steps += 1
+      self._eager_steps[pipe] += 1
     self._opt_steps += 1
     self._replay._out = self._pbuf[c]
     self._replay.unpack_transition(self._pbuf[c])
-    if self.pipeline:
-      self._slot = 1 - c
-      self._has_prefetch = True
-      self._prefetch_add_count = int(mem.add_count)
-    if self._graphs is None and self.use_hip_graph and self._eager_steps >= 3:
-      self._capture()
+    self._slot = 1 - c
+    self._has_prefetch = pipe
+    self._prefetch_add_count = int(mem.add_count)
+    self._last_train_add_count = int(mem.add_count)
+    self._selects_since_train = 0
+    if graphs is None and self.use_hip_graph and self._eager_steps[pipe] >= 3:
+      self._capture(pipe)
 
-  def _capture(self):
+  @property
+  def _graphs(self):
+    g = self._graph_sets.get(self.pipeline)
+    return None if g is None else g[0]
+
+  def _capture(self, pipe=None):
     """Two graphs, one per gradient-step parity k (pipeline slot and Adam
     beta-power slot both alternate with k); with one GPU the optimizer is in the
     same graph, with N GPUs it is a second graph after the RCCL all-reduce."""
+    pipe = self.pipeline if pipe is None else pipe
     torch.cuda.synchronize(self._device)
-    graphs, graphs_opt, pool = [], [], None
+    graphs, graphs_opt, pool = [], [], self._graph_pool
     if self._split_allreduce():
       for k in (0, 1):
-        c = k if self.pipeline else 0
+        c = k
         parts = [torch.cuda.CUDAGraph() for _ in range(3)]
-        fns = (lambda: self._grad_step_head(c, k), lambda: self._grad_step_tail(c, k),
+        fns = (lambda: self._grad_step_head(c, k, pipe), lambda: self._grad_step_tail(c, k, pipe),
                lambda: self._device_opt_step(k))
         for gr, fn in zip(parts, fns):
           with torch.cuda.graph(gr, pool=pool):
             fn()
           pool = gr.pool()
         graphs.append(parts)
-      self._graphs, self._graphs_opt = graphs, []
+      self._graph_pool = pool
+      self._graph_sets[pipe] = (graphs, [])
       return
     for k in (0, 1):
-      c = k if self.pipeline else 0
+      c = k
       g = torch.cuda.CUDAGraph()
       with torch.cuda.graph(g, pool=pool):
-        self._grad_step(c, k)
+        self._grad_step(c, k, pipe)
         if self._pg is None:
           self._device_opt_step(k)
       pool = g.pool()
@@ -455,7 +483,8 @@ class DQNAgent(object):
           self._device_opt_step(k)
         graphs_opt.append(go)
     # capture records without executing: tape cursor and buffers are unchanged
-    self._graphs, self._graphs_opt = graphs, graphs_opt
+    self._graph_pool = pool
+    self._graph_sets[pipe] = (graphs, graphs_opt)
 
   def _sync_target(self):
     ops.sync_copy(self.target_convnet.fp.flat, self.online_convnet.fp.flat)
@@ -501,8 +530,11 @@ class DQNAgent(object):
   def _select_action(self):
     """dqn_agent.py:394-416.  The replay's RNG tape is brought in step first so
     Python's `random` stream is consumed exactly as by the reference."""
-    self._discard_prefetch()      # its draws would precede ours: give them back first
-    self._replay.memory.sync_rng()
+    mem = self._replay.memory
+    if mem._rng.stream is random:   # PER samples from Python's `random`, as epsilon-greedy does
+      self._selects_since_train += 1
+      self._discard_prefetch()      # its draws would precede ours: give them back first
+      mem.sync_rng()
     if self.eval_mode:
       epsilon = self.epsilon_eval
     else:

@@ -52,6 +52,7 @@ class RNGTape:
     self._base = None              # full host state the tape starts from
     self._len = 0
     self._budget = 0               # words guaranteed left (host-side worst-case accounting)
+    self._host_synced = False      # last invalidation came from a host-side sync
 
   @property
   def valid(self):
@@ -89,7 +90,16 @@ class RNGTape:
     if self.valid:
       self.sync(stream_handle)
       synced = True
-    self.rebuild(max(worst_case, self.capacity), stream_handle)
+      size = self.capacity               # drained: a full tape (≈ hundreds of steps)
+    elif self._host_synced:
+      # the host drew from the stream (e.g. epsilon-greedy between steps): it will
+      # again before long, so a short tape -- generating a full one per action
+      # would cost milliseconds of host time each time
+      size = 8 * worst_case
+    else:
+      size = self.capacity
+    self._host_synced = False
+    self.rebuild(max(worst_case, min(size, self.capacity)), stream_handle)
     self._budget -= worst_case
     return synced
 
@@ -113,6 +123,7 @@ class RNGTape:
     st = rs.get_state()
     _set_stream(self.stream, base, np.asarray(st[1], np.uint32), int(st[2]))
     self._base = None
+    self._host_synced = True
     return meta
 
 
