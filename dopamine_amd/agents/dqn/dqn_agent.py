@@ -126,6 +126,7 @@ class DQNAgent(object):
     self._eager_steps = {True: 0, False: 0}
     self._last_train_add_count = -1
     self._selects_since_train = 0
+    self._act = None
     self._opt_steps = 0
     self._slot = 0
     self._pbuf = [None, None]
@@ -517,6 +518,8 @@ class DQNAgent(object):
       self._store_transition(self._observation, self.action, reward, True)
 
   def _q_values(self, state_np):
+    if self._hip is not None and self.use_hip_graph:
+      return self._act_q(state_np)
     x = torch.as_tensor(state_np, dtype=torch.float32, device=self._device)
     x = x.permute(0, 3, 1, 2) if x.dim() == 4 else x          # NHWC -> NCHW
     if np.dtype(self.observation_dtype) == np.uint8:
@@ -524,8 +527,38 @@ class DQNAgent(object):
     with torch.no_grad():
       return self._online_q(self._state_input(x.contiguous()))
 
+  def _q_from_output(self, out):
+    """Network output -> Q-values (B, A)."""
+    return out
+
   def _online_q(self, x):
-    return self.online_convnet(x)
+    return self._q_from_output(self.online_convnet(x))
+
+  def _act_q(self, state_np):
+    """Q-values for action selection on the HIP CNN at batch 1: the forward and
+    the Q reduction are one captured graph; the state goes up through a pinned
+    staging buffer.  The executor reads the online parameters in place."""
+    if self._act is None:
+      from dopamine_amd.cnn import HipNatureCNN
+      exe = HipNatureCNN(self.online_convnet, 1)
+      x = torch.zeros((1, 84, 84, self.stack_size), dtype=torch.float32, device=self._device)
+      pin = torch.empty(x.shape, dtype=torch.float32).pin_memory()
+      main = torch.cuda.current_stream(self._device)
+      warm = torch.cuda.Stream(self._device)
+      warm.wait_stream(main)
+      with torch.cuda.stream(warm):
+        self._q_from_output(exe.forward(x))
+      main.wait_stream(warm)
+      g = torch.cuda.CUDAGraph()
+      with torch.cuda.graph(g):
+        q = self._q_from_output(exe.forward(x))
+      self._act = (exe, x, pin, g, q)
+    exe, x, pin, g, q = self._act
+    scale = 1.0 / 255.0 if np.dtype(self.observation_dtype) == np.uint8 else 1.0
+    np.multiply(state_np, scale, out=pin.numpy(), casting='unsafe')
+    x.copy_(pin, non_blocking=True)
+    g.replay()
+    return q
 
   def _select_action(self):
     """dqn_agent.py:394-416.  The replay's RNG tape is brought in step first so

@@ -109,8 +109,8 @@ class RainbowAgent(dqn_agent.DQNAgent):
       loss = loss * (w / w.max())
     return float(loss.mean().item())
 
-  def _online_q(self, x):
-    logits = self.online_convnet(x)
+  def _q_from_output(self, out):
+    logits = out.reshape(out.shape[0], self.num_actions, self._num_atoms)
     return (torch.softmax(logits, -1) * self._support).sum(-1)
 
   def _target_dict(self, out):

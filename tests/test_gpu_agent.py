@@ -137,3 +137,25 @@ def test_iqn_with_prioritized_replay_keeps_insert_priorities():
   a._replay.memory.sync_rng()
   np.testing.assert_array_equal(a._replay.memory.sum_tree.nodes[-1], before)
   assert np.isfinite(a.mean_loss())
+
+
+@pytest.mark.parametrize('kind', ['dqn', 'rainbow'])
+def test_action_q_values_on_the_hip_cnn_match_torch(kind):
+  """_select_action's Q-values (batch-1 HIP CNN graph) vs the PyTorch network on
+  the same parameters, before and after an in-place parameter update."""
+  from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
+  torch.manual_seed(3)
+  a = (_rainbow(use_hip_graph=True) if kind == 'rainbow' else
+       DQNAgent(num_actions=6, replay_capacity=3000, batch_size=32, min_replay_history=100))
+  rs = np.random.RandomState(4)
+  for _ in range(2):
+    st = rs.randint(0, 256, (1, 84, 84, 4)).astype(np.float64)
+    q_hip = a._q_values(st).clone()
+    with torch.no_grad():
+      x = torch.as_tensor(st, dtype=torch.float32, device='cuda').permute(0, 3, 1, 2) / 255.0
+      q_ref = a._online_q(x.contiguous())
+    torch.cuda.synchronize()
+    scale = q_ref.abs().max().item() + 1e-30
+    assert (q_hip - q_ref).abs().max().item() <= 2e-5 * scale
+    with torch.no_grad():
+      a.online_convnet.fp.flat.mul_(1.1)        # the graph reads the parameters in place
