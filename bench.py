@@ -44,6 +44,8 @@ def parse():
   ap.add_argument('--gather-iters', type=int, default=400)
   ap.add_argument('--fuse-opt', type=int, default=None,
                   help='override the agent default fuse_optimizer (0/1)')
+  ap.add_argument('--ride', type=int, default=None,
+                  help='override the agent default ride_replay (0/1)')
   return ap.parse_args()
 
 
@@ -178,7 +180,8 @@ def main():
                        replay_capacity=args.capacity, batch_size=args.batch,
                        use_hip_graph=not args.no_graph, device=dev, seed=1000 * rank,
                        process_group=pg,
-                       **({} if args.fuse_opt is None else {'fuse_optimizer': bool(args.fuse_opt)}))
+                       **({} if args.fuse_opt is None else {'fuse_optimizer': bool(args.fuse_opt)}),
+                       **({} if args.ride is None else {'ride_replay': bool(args.ride)}))
   import random
   random.seed(0 + rank)
   fill_synthetic(agent._replay.memory, args.actions, seed=1 + rank)

@@ -61,6 +61,11 @@ class CnnActs(ctypes.Structure):
   _fields_ = [(n, ctypes.c_void_p) for n in ('a1', 'a2', 'a3', 'h', 'out')]
 
 
+class Rider(ctypes.Structure):
+  """dq_rider: a recorded replay operation (opaque)."""
+  _fields_ = [('words', ctypes.c_int64 * 40)]
+
+
 _P = ctypes.c_void_p
 _I32 = ctypes.c_int32
 _I64 = ctypes.c_int64
@@ -84,6 +89,10 @@ SIGNATURES = {
     'dq_replay_set_tape': [_P, _I64, _P],
     'dq_replay_read_meta': [_P, ctypes.POINTER(Meta), _P],
     'dq_replay_rewind_last_sample': [_P, _P],
+    'dq_replay_record_sumtree_set': [_P, _P, _P, _I64, ctypes.POINTER(Rider)],
+    'dq_replay_record_sample': [_P, _I32, _P, ctypes.POINTER(Rider)],
+    'dq_replay_record_gather_nhwc': [_P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                                     ctypes.POINTER(Rider)],
     'dq_c51_loss': [_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _F, _P, _P, _P, _P, _P],
     'dq_dqn_huber_loss': [_P, _P, _P, _P, _P, _I32, _I32, _F, _P, _P, _P, _P],
     'dq_iqn_loss': [_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _F, _F, _P, _P, _P, _P],
@@ -102,6 +111,9 @@ SIGNATURES = {
     'dq_cnn_backward_groups': [ctypes.POINTER(CnnParams), ctypes.POINTER(CnnParams), _I32, _P,
                                ctypes.POINTER(CnnActs), _P, ctypes.POINTER(CnnActs), _P, _I32,
                                _I32, _P],
+    'dq_cnn_backward_riders': [ctypes.POINTER(CnnParams), ctypes.POINTER(CnnParams), _I32, _P,
+                               ctypes.POINTER(CnnActs), _P, ctypes.POINTER(CnnActs), _P,
+                               ctypes.POINTER(Rider), _I32, ctypes.POINTER(AdamArgs), _P],
     'dq_cnn_backward_layer': [ctypes.POINTER(CnnParams), ctypes.POINTER(CnnParams), _I32, _P,
                               ctypes.POINTER(CnnActs), _P, ctypes.POINTER(CnnActs), _P, _I32, _I32,
                               _P],

@@ -85,6 +85,7 @@ class DQNAgent(object):
                use_hip_cnn=True,
                fuse_optimizer=False,
                pair_forward=False,
+               ride_replay=True,
                device=None,
                seed=0,
                process_group=None):
@@ -121,6 +122,7 @@ class DQNAgent(object):
     self.use_hip_cnn = use_hip_cnn
     self.fuse_optimizer = fuse_optimizer
     self.pair_forward = pair_forward
+    self.ride_replay = ride_replay
     self._graph_sets = {}          # pipe -> (graphs per parity, optimizer graphs per parity)
     self._graph_pool = None
     self._eager_steps = {True: 0, False: 0}
@@ -258,8 +260,16 @@ class DQNAgent(object):
     """The target network's raw output as the loss kernel's inputs."""
     return {'q': out}
 
+  def _rides(self):
+    """ride_replay: single-replica HIP-CNN steps run on ONE stream -- the online and
+    target forwards paired at the start, and the next batch's priority write-back
+    -> sample -> gather recorded as riders of the backward's first grouped launches
+    (dq_cnn_backward_riders) instead of a second stream: the graph then has no
+    cross-queue fork/join edges, which cost ~28 us of a ~190 us step on MI355X."""
+    return self.ride_replay and self._hip is not None and self._pg is None
+
   def _pairs(self):
-    return self.pair_forward and self._hip is not None
+    return (self.pair_forward or self._rides()) and self._hip is not None
 
   def _forward_pair(self, c):
     """pair_forward: the online net on s and the target net on s' of slot c in ONE
@@ -296,7 +306,13 @@ class DQNAgent(object):
     if self._pairs():
       self._forward_pair(c)
     y, g = self._online_loss(self._pbuf[c], self._ptgt[c])
-    if pipe:
+    if pipe and self._rides():
+      with self._replay.memory.recording() as riders:
+        self._post_loss(self._pbuf[c])
+        self._prefetch(1 - c)
+      adam = self._opt if self._fused_opt() else None
+      self._hip['online'].backward(g, riders=riders, adam=adam, slot=k)
+    elif pipe:
       main = torch.cuda.current_stream(self._device)
       ev = torch.cuda.Event()
       ev.record(main)

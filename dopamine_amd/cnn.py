@@ -79,8 +79,19 @@ class HipNatureCNN(object):
                'dq_cnn_forward')
     return self.acts['out']
 
-  def backward(self, dout, parallel=False, adam=None, slot=0, groups=None):
+  def _adam_args(self, adam, slot):
+    assert adam.params.data_ptr() == self.net.fp.flat.data_ptr(), 'adam must own net.fp.flat'
+    return _lib.AdamArgs(var=adam.params.data_ptr(), m=adam.m.data_ptr(), v=adam.v.data_ptr(),
+                         state=adam.state.data_ptr(), slot=int(slot), lr=adam.lr,
+                         beta1=adam.b1, beta2=adam.b2, epsilon=adam.eps)
+
+  def backward(self, dout, parallel=False, adam=None, slot=0, groups=None, riders=None):
     """dout: (B, n_out).  Writes all parameter gradients into net.fp.grad.
+
+    riders: replay operations recorded with ``ReplayBuffer.recording()`` (the
+    next batch's priority write-back, sample and gather); rider i runs as extra
+    blocks of grouped launch i (dq_cnn_backward_riders), in order, on this
+    stream.  Combines with ``adam``.
 
     groups=(first, last): only launches [first, last) of the 7 grouped launches
     (a data-parallel learner all-reduces fc1/fc2's gradients after launch 3).
@@ -98,6 +109,14 @@ class HipNatureCNN(object):
     with the other stream's.  Kept for experimentation; off by default."""
     dout = dout.reshape(self.B, self.n_out)
     assert dout.is_contiguous() and self._x is not None
+    if riders:
+      args = None if adam is None else ctypes.byref(self._adam_args(adam, slot))
+      arr = (_lib.Rider * len(riders))(*riders)
+      _lib.check(_lib.lib.dq_cnn_backward_riders(
+          ctypes.byref(self._p), ctypes.byref(self._g), self.B, self._x.data_ptr(),
+          ctypes.byref(self._a), dout.data_ptr(), ctypes.byref(self._d), self.ws.data_ptr(),
+          arr, len(riders), args, self._stream(dout)), 'dq_cnn_backward_riders')
+      return self.net.fp.grad
     if groups is not None:          # a sub-range of the 7 grouped launches
       _lib.check(_lib.lib.dq_cnn_backward_groups(
           ctypes.byref(self._p), ctypes.byref(self._g), self.B, self._x.data_ptr(),
@@ -105,10 +124,7 @@ class HipNatureCNN(object):
           int(groups[0]), int(groups[1]), self._stream(dout)), 'dq_cnn_backward_groups')
       return self.net.fp.grad
     if adam is not None:
-      assert adam.params.data_ptr() == self.net.fp.flat.data_ptr(), 'adam must own net.fp.flat'
-      args = _lib.AdamArgs(var=adam.params.data_ptr(), m=adam.m.data_ptr(), v=adam.v.data_ptr(),
-                           state=adam.state.data_ptr(), slot=int(slot), lr=adam.lr,
-                           beta1=adam.b1, beta2=adam.b2, epsilon=adam.eps)
+      args = self._adam_args(adam, slot)
       _lib.check(_lib.lib.dq_cnn_backward_adam(
           ctypes.byref(self._p), ctypes.byref(self._g), self.B, self._x.data_ptr(),
           ctypes.byref(self._a), dout.data_ptr(), ctypes.byref(self._d), self.ws.data_ptr(),

@@ -28,6 +28,9 @@
 
 
 #include "common.h"
+#include "replay_dev.h"
+
+#include <cstring>
 
 namespace dq {
 namespace cnn {
@@ -353,13 +356,21 @@ __device__ __forceinline__ void group_coord(int g, int& rr, int& kk) {
 // accumulators are then summed through LDS by all threads, each output element
 // in wave order (deterministic), and handed to the epilogue with consecutive
 // threads on consecutive columns.
+// compile with -DDQ_SHARED_STAGING=1 for the block-shared operand staging (A/B builds)
+#ifndef DQ_SHARED_STAGING
+#define DQ_SHARED_STAGING 0
+#endif
+
 template <int WM, int WN, int WK>
 struct Tile {
   static constexpr int T = 64 * WM * WN * WK;
   static constexpr int BM = 32 * WM, BN = 32 * WN, BKT = 32 * WK;
+  // one wave per k band (WM = WN = 1): each wave stages only its own band, 16 k at a time
+  static constexpr bool kPrivate = WM == 1 && WN == 1 && WK > 1 && !DQ_SHARED_STAGING;
   template <class AL, class BL>
   static constexpr int lds() {      // operand slices, or the WK > 1 reduction scratch
-    const int tile = BKT * (BM + (AL::kFast ? 1 : 4)) + BKT * (BN + (BL::kFast ? 1 : 4));
+    const int sa = BM + (AL::kFast ? 1 : 4), sb = BN + (BL::kFast ? 1 : 4);
+    const int tile = kPrivate ? WK * 16 * (sa + sb) : BKT * sa + BKT * sb;
     const int red = WK > 1 ? WK * WM * WN * 1024 : 0;
     return tile > red ? tile : red;
   }
@@ -427,6 +438,59 @@ __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& 
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+  if constexpr (TL::kPrivate) {
+    // Wave-private staging: wave wk fetches its own 32-wide k band (the same
+    // coalesced 128-byte row segments as the shared layout) and transposes it
+    // through its own 16-k LDS window in two halves -- no block barrier until
+    // the reduction, and ~half the LDS, so two 1024-thread blocks share a CU.
+    // Same MFMA sequence as the shared path: bitwise identical results.
+    float* Aw = smem + wave * 16 * (SA + SB);
+    float* Bw = Aw + 16 * SA;
+    float4 pa4[4], pb4[4];
+    auto fetch = [&](int k0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int rr, kk;
+        group_coord<AL::kFast, BM, BKT>(256 * wk + 64 * i + lane, rr, kk);
+        pa4[i] = A.get(m0 + rr, k0 + kk, M, kend);
+        group_coord<BL::kFast, BN, BKT>(256 * wk + 64 * i + lane, rr, kk);
+        pb4[i] = B.get(n0 + rr, k0 + kk, N, kend);
+      }
+    };
+    auto stage = [&](int h) {       // k rows [16h, 16h + 16) of this wave's band
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int rr, kk;
+        group_coord<AL::kFast, BM, BKT>(256 * wk + 64 * i + lane, rr, kk);
+        kk -= 32 * wk + 16 * h;
+        if (kk >= 0 && kk < 16) put(Aw, SA, AL::kFast, rr, kk, pa4[i]);
+        group_coord<BL::kFast, BN, BKT>(256 * wk + 64 * i + lane, rr, kk);
+        kk -= 32 * wk + 16 * h;
+        if (kk >= 0 && kk < 16) put(Bw, SB, BL::kFast, rr, kk, pb4[i]);
+      }
+    };
+    const float* qa = Aw + (lane >> 5) * SA + (lane & 31);
+    const float* qb = Bw + (lane >> 5) * SB + (lane & 31);
+    fetch(kbeg);
+    for (int k0 = kbeg; k0 < kend; k0 += BKT) {
+      const bool live = k0 + wk * 32 < kend;   // wave-uniform: bands past the end are all zero
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        stage(h);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (h == 1 && k0 + BKT < kend) fetch(k0 + BKT);
+        if (live) {
+#pragma unroll
+          for (int s = 0; s < 16; s += 2)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(qa[s * SA], qb[s * SB], acc, 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();                 // staging windows are reused as reduction scratch
+  } else {
   load(kbeg);
   const float* pa = As + (wk * 32 + (lane >> 5)) * SA + wm * 32 + (lane & 31);
   const float* pb = Bs + (wk * 32 + (lane >> 5)) * SB + wn * 32 + (lane & 31);
@@ -440,6 +504,7 @@ __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& 
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(pa[s * SA], pb[s * SB], acc, 0, 0, 0);
     }
     __syncthreads();
+  }
   }
   // C/D layout of the 32x32 f32 MFMA: col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5)
   if (WK == 1) {
@@ -641,6 +706,17 @@ struct AdamOp {
   int blocks() const { return nb; }
 };
 
+// A recorded replay operation (replay_dev.h) riding in a grouped launch: its
+// blocks come first in the launch so the single-wave sum-tree update / sampler
+// chains start before the GEMM blocks fill the machine.
+struct RiderOp {
+  static constexpr int kT = kGroupT;
+  static constexpr int kLds = (kRiderLds + 3) / 4;
+  RiderDesc r;
+  __device__ __forceinline__ void run(int blk, float* smem) const { run_rider<kT>(r, blk, smem); }
+  int blocks() const { return rider_blocks<kT>(r); }
+};
+
 template <class... Ops>
 constexpr int max_lds() {
   int m = 1;
@@ -732,6 +808,15 @@ void group(Ctx& c, Op0 op0, Ops... ops) {
   total += op0.blocks();
   ((g.nblocks[i++] = ops.blocks(), total += ops.blocks()), ...);
   hipLaunchKernelGGL((k_grouped<T, Op0, Ops...>), dim3(total), dim3(T), 0, c.s, g, op0, ops...);
+}
+
+// group() with rider r (if any) in front
+template <class... Ops>
+void group_r(Ctx& c, const RiderDesc* r, Ops... ops) {
+  if (r && r->kind != kRiderNone)
+    group(c, RiderOp{*r}, ops...);
+  else
+    group(c, ops...);
 }
 
 // Tile shapes: WM = WN = 1 with WK k-bands sized so K takes one or two slices
@@ -878,7 +963,8 @@ bool backward_layer(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int 
 template <bool kAdam>
 void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int B,
                       const float* x, const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d,
-                      const AdamHost& opt, int first = 0, int last = 7) {
+                      const AdamHost& opt, int first = 0, int last = 7,
+                      const RiderDesc* riders = nullptr, int n_riders = 0) {
   const int NO = p->n_out;
   using GE = GradEpi<kAdam>;
   using W16 = Tile<1, 1, 16>;
@@ -921,12 +1007,13 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
       ws + o1, nz1, 32, Conv1::K + 1,
       GE::make(g->conv1_w, g->conv1_b, Conv1::K, p->conv1_w, p->conv1_b, opt, 1)};
   auto in = [&](int i) { return first <= i && i < last; };
-  if (in(0)) group(c, dX_fc2);
-  if (in(1)) group(c, dW_fc2, dX_fc1);
-  if (in(2)) group(c, dW_fc1, dX_c3);
-  if (in(3)) group(c, dW_c3, dcol);
-  if (in(4)) group(c, sum_c3, dW_c2, da1);
-  if (in(5)) group(c, sum_c2, dW_c1);
+  auto rd = [&](int i) { return i < n_riders ? riders + i : nullptr; };   // rider of launch i
+  if (in(0)) group_r(c, rd(0), dX_fc2);
+  if (in(1)) group_r(c, rd(1), dW_fc2, dX_fc1);
+  if (in(2)) group_r(c, rd(2), dW_fc1, dX_c3);
+  if (in(3)) group_r(c, rd(3), dW_c3, dcol);
+  if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, da1);
+  if (in(5)) group_r(c, rd(5), sum_c2, dW_c1);
   if (!in(6)) return;
   if constexpr (kAdam) {
     const dq_adam_args* o = opt.a;
@@ -936,9 +1023,9 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
     const int nb = (int)std::max<int64_t>(1, ((n >> 2) + kGroupT - 1) / kGroupT);  // 1 float4 / thread
     AdamOp rest{w0, g->conv2_w, o->m + off, o->v + off, n,
                 AdamDev{o->state, o->slot, o->lr, o->beta1, o->beta2, o->epsilon}, nb};
-    group(c, sum_c1, rest);
+    group_r(c, rd(6), sum_c1, rest);
   } else {
-    group(c, sum_c1);
+    group_r(c, rd(6), sum_c1);
   }
 }
 
@@ -947,6 +1034,26 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
 
 using namespace dq;
 using namespace dq::cnn;
+
+// the fused optimizer needs the parameters (and gradients) in one flat buffer, in
+// conv1..fc2 order, with the float4 Adam range 16-byte aligned
+static int check_adam(const dq_cnn_params* p, const dq_cnn_params* g, const dq_adam_args* opt) {
+  DQ_CHECK_ARG(opt->var && opt->m && opt->v && opt->state && (opt->slot == 0 || opt->slot == 1),
+               "adam args: var, m, v, state and slot 0/1 required");
+  const float* w[10] = {p->conv1_w, p->conv1_b, p->conv2_w, p->conv2_b, p->conv3_w,
+                        p->conv3_b, p->fc1_w,  p->fc1_b,  p->fc2_w,  p->fc2_b};
+  const float* gw[10] = {g->conv1_w, g->conv1_b, g->conv2_w, g->conv2_b, g->conv3_w,
+                         g->conv3_b, g->fc1_w,  g->fc1_b,  g->fc2_w,  g->fc2_b};
+  for (int i = 0; i < 10; ++i) {
+    DQ_CHECK_ARG(w[i] >= opt->var && (i == 0 || w[i] > w[i - 1]),
+                 "parameters must live in the flat buffer opt->var in conv1..fc2 order");
+    DQ_CHECK_ARG(gw[i] - g->conv1_w == w[i] - p->conv1_w,
+                 "gradients must have the parameters' flat layout");
+  }
+  DQ_CHECK_ARG(((p->conv2_w - opt->var) & 3) == 0 && ((g->conv2_w - g->conv1_w) & 3) == 0,
+               "16-byte aligned parameter views required");
+  return DQ_OK;
+}
 
 extern "C" {
 
@@ -989,20 +1096,8 @@ int dq_cnn_backward_adam(const dq_cnn_params* p, const dq_cnn_params* g, int32_t
                          float* ws, const dq_adam_args* opt, void* stream) {
   DQ_CHECK_ARG(p && g && a && d && x && dout && ws && opt && batch >= 1, "null argument");
   DQ_CHECK_ARG(p->in_channels == 4 && p->n_out >= 1, "the Nature CNN takes 84x84x4 NHWC input");
-  DQ_CHECK_ARG(opt->var && opt->m && opt->v && opt->state && (opt->slot == 0 || opt->slot == 1),
-               "adam args: var, m, v, state and slot 0/1 required");
-  const float* w[10] = {p->conv1_w, p->conv1_b, p->conv2_w, p->conv2_b, p->conv3_w,
-                        p->conv3_b, p->fc1_w,  p->fc1_b,  p->fc2_w,  p->fc2_b};
-  const float* gw[10] = {g->conv1_w, g->conv1_b, g->conv2_w, g->conv2_b, g->conv3_w,
-                         g->conv3_b, g->fc1_w,  g->fc1_b,  g->fc2_w,  g->fc2_b};
-  for (int i = 0; i < 10; ++i) {
-    DQ_CHECK_ARG(w[i] >= opt->var && (i == 0 || w[i] > w[i - 1]),
-                 "parameters must live in the flat buffer opt->var in conv1..fc2 order");
-    DQ_CHECK_ARG(gw[i] - g->conv1_w == w[i] - p->conv1_w,
-                 "gradients must have the parameters' flat layout");
-  }
-  DQ_CHECK_ARG(((p->conv2_w - opt->var) & 3) == 0 && ((g->conv2_w - g->conv1_w) & 3) == 0,
-               "16-byte aligned parameter views required");
+  const int rc = check_adam(p, g, opt);
+  if (rc != DQ_OK) return rc;
   Ctx c{(hipStream_t)stream, ws, false, 0};
   backward_grouped<true>(c, p, g, batch, x, a, dout, d, AdamHost{opt});
   DQ_CHECK_LAUNCH("dq_cnn_backward_adam");
@@ -1018,6 +1113,31 @@ int dq_cnn_backward_groups(const dq_cnn_params* p, const dq_cnn_params* g, int32
   Ctx c{(hipStream_t)stream, ws, false, 0};
   backward_grouped<false>(c, p, g, batch, x, a, dout, d, AdamHost{nullptr}, first, last);
   DQ_CHECK_LAUNCH("dq_cnn_backward_groups");
+  return DQ_OK;
+}
+
+int dq_cnn_backward_riders(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch,
+                           const float* x, const dq_cnn_acts* a, const float* dout,
+                           dq_cnn_acts* d, float* ws, const dq_rider* riders, int32_t n_riders,
+                           const dq_adam_args* opt, void* stream) {
+  DQ_CHECK_ARG(p && g && a && d && x && dout && ws && batch >= 1, "null argument");
+  DQ_CHECK_ARG(p->in_channels == 4 && p->n_out >= 1, "the Nature CNN takes 84x84x4 NHWC input");
+  DQ_CHECK_ARG(0 <= n_riders && n_riders <= 7 && (riders || n_riders == 0),
+               "at most one rider per grouped launch (7)");
+  RiderDesc r[7];
+  for (int i = 0; i < n_riders; ++i) {
+    memcpy(&r[i], &riders[i], sizeof(RiderDesc));
+    DQ_CHECK_ARG(r[i].kind >= kRiderNone && r[i].kind <= kRiderGatherNhwc, "corrupt rider");
+  }
+  Ctx c{(hipStream_t)stream, ws, false, 0};
+  if (opt) {
+    const int rc = check_adam(p, g, opt);
+    if (rc != DQ_OK) return rc;
+    backward_grouped<true>(c, p, g, batch, x, a, dout, d, AdamHost{opt}, 0, 7, r, n_riders);
+  } else {
+    backward_grouped<false>(c, p, g, batch, x, a, dout, d, AdamHost{nullptr}, 0, 7, r, n_riders);
+  }
+  DQ_CHECK_LAUNCH("dq_cnn_backward_riders");
   return DQ_OK;
 }
 

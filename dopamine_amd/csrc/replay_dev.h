@@ -1,0 +1,559 @@
+// Device bodies of the replay kernels, shared by replay.hip (their own launches)
+// and nature_cnn.hip (the same code riding as extra blocks in the backward's
+// grouped launches, see RiderOp).  Restates the reference's numpy code:
+// circular_replay_buffer.py:381-555, prioritized_replay_buffer.py:152-170,
+// sum_tree.py:128-139 and :178-205.
+//
+// Numerics: every float64 step of the sampler (stratum edges, uniform(), the
+// q * total scaling, the descent's compare/subtract) and the float32 n-step
+// reward are written with explicit _rn intrinsics and compiled with
+// -ffp-contract=off, so results are bit-identical to the reference.
+#pragma once
+#include "common.h"
+
+namespace dq {
+
+struct ReplayView {
+  int64_t C;
+  int64_t obs_bytes;
+  int32_t S;
+  int32_t n;
+  int32_t depth;
+  int32_t max_attempts;
+  const uint8_t* frames;
+  const int32_t* actions;
+  const float* rewards;
+  const uint8_t* terminals;
+  double* tree;
+  dq_replay_meta* meta;
+  const uint32_t* tape;
+  const float* discount;
+};
+
+__device__ __forceinline__ void latch(dq_replay_meta* m, int code, int arg, double val) {
+  if (atomicCAS(&m->status, 0, code) == 0) {
+    m->status_arg = arg;
+    m->status_value = val;
+  }
+}
+
+// Python's random.random(): genrand_res53 from two consecutive 32-bit words.
+__device__ __forceinline__ double res53(uint32_t w0, uint32_t w1) {
+  const double a = (double)(w0 >> 5), b = (double)(w1 >> 6);
+  return __dmul_rn(__dadd_rn(__dmul_rn(a, 67108864.0), b), 1.0 / 9007199254740992.0);
+}
+
+// SumTree.sample descent (sum_tree.py:128-139) on the flat heap; q already
+// scaled by the root total.
+__device__ __forceinline__ int64_t descend(const double* tree, int depth, double q) {
+  int64_t node = 0;
+  for (int d = 1; d <= depth; ++d) {
+    const double left = tree[((int64_t)1 << d) - 1 + 2 * node];
+    if (q < left) {
+      node = 2 * node;
+    } else {
+      node = 2 * node + 1;
+      q = __dsub_rn(q, left);
+    }
+  }
+  return node;
+}
+
+// OutOfGraphReplayBuffer.is_valid_transition (circular_replay_buffer.py:381-414).
+__device__ inline bool is_valid(const ReplayView& v, int64_t idx, int64_t add_count) {
+  if (idx < 0 || idx >= v.C) return false;
+  const int64_t cursor = add_count % v.C;
+  if (add_count < v.C) {
+    if (idx >= cursor - v.n) return false;
+    if (idx < v.S - 1) return false;
+  }
+  // invalid_range(cursor) = {(cursor - n + k) mod C : 0 <= k < n + S}
+  if (pymod(idx - (cursor - v.n), v.C) < (int64_t)(v.n + v.S)) return false;
+  // a terminal in any but the last frame of the stack
+  for (int k = 0; k < v.S - 1; ++k)
+    if (v.terminals[pymod(idx - v.S + 1 + k, v.C)]) return false;
+  return true;
+}
+
+// trajectory length L (circular_replay_buffer.py:517-526).
+__device__ __forceinline__ int traj_len(const ReplayView& v, int64_t idx, bool* term) {
+  for (int j = 0; j < v.n; ++j) {
+    if (v.terminals[pymod(idx + j, v.C)]) {
+      *term = true;
+      return j + 1;
+    }
+  }
+  *term = false;
+  return v.n;
+}
+
+constexpr int kMaxBatch = 1024;
+
+// ---------------------------------------------------------------------------
+// Prioritized index sampling: stratified descent (one lane per stratum), then
+// the reference's sequential retry loop (prioritized_replay_buffer.py:152-170).
+// One wave (threads 0..63 of the block; any others have returned).
+// ---------------------------------------------------------------------------
+constexpr int kPerSampleLds = kMaxBatch * 8 + kMaxBatch;   // bytes
+
+__device__ inline void per_sample_body(const ReplayView& v, int B, int32_t* out, void* lds) {
+  int64_t* s_idx = (int64_t*)lds;
+  uint8_t* s_ok = (uint8_t*)(s_idx + kMaxBatch);
+  const int lane = threadIdx.x;
+  dq_replay_meta* meta = v.meta;
+  const int64_t add_count = meta->add_count;
+  int64_t pos = meta->tape_pos;
+  const int64_t pos0 = pos;
+  const int64_t len = meta->tape_len;
+  const double total = v.tree[0];
+  bool fail = meta->status != 0;
+  if (!fail && total == 0.0) {
+    if (lane == 0) latch(meta, DQ_ST_EMPTY_TREE, 0, 0.0);
+    fail = true;
+  }
+  if (!fail && pos + 2 * (int64_t)B > len) {
+    if (lane == 0) latch(meta, DQ_ST_TAPE_EXHAUSTED, 0, 0.0);
+    fail = true;
+  }
+  if (fail) {
+    if (lane == 0) meta->reserved[0] = pos0;
+    for (int i = lane; i < B; i += kWave) out[i] = 0;
+    return;
+  }
+  // np.linspace(0, 1, B + 1): edge_i = i * (1/B), last edge exactly 1.0
+  const double step = 1.0 / (double)B;
+  for (int i = lane; i < B; i += kWave) {
+    const double u = res53(v.tape[pos + 2 * i], v.tape[pos + 2 * i + 1]);
+    const double lo = __dmul_rn((double)i, step);
+    const double hi = (i + 1 == B) ? 1.0 : __dmul_rn((double)(i + 1), step);
+    const double q = __dadd_rn(lo, __dmul_rn(__dsub_rn(hi, lo), u));  // random.uniform
+    const int64_t node = descend(v.tree, v.depth, __dmul_rn(q, total));
+    s_idx[i] = node;
+    s_ok[i] = is_valid(v, node, add_count);
+  }
+  pos += 2 * (int64_t)B;
+  __syncthreads();
+  if (lane == 0) {
+    int budget = v.max_attempts;
+    for (int i = 0; i < B; ++i) {
+      if (s_ok[i]) continue;
+      if (budget == 0) {
+        latch(meta, DQ_ST_MAX_ATTEMPTS, i, 0.0);
+        break;
+      }
+      int64_t cand = s_idx[i];
+      bool tape_dry = false;
+      while (budget > 0) {
+        if (pos + 2 > len) {
+          tape_dry = true;
+          break;
+        }
+        const double u = res53(v.tape[pos], v.tape[pos + 1]);
+        pos += 2;
+        cand = descend(v.tree, v.depth, __dmul_rn(u, total));
+        --budget;
+        if (is_valid(v, cand, add_count)) break;
+      }
+      s_idx[i] = cand;
+      if (tape_dry) {
+        latch(meta, DQ_ST_TAPE_EXHAUSTED, i, 0.0);
+        break;
+      }
+    }
+    meta->reserved[0] = pos0;   // entry cursor, for dq_replay_rewind_last_sample
+    meta->tape_pos = pos;
+  }
+  __syncthreads();
+  for (int i = lane; i < B; i += kWave) out[i] = (int32_t)s_idx[i];
+}
+
+// ---------------------------------------------------------------------------
+// Uniform index sampling (circular_replay_buffer.py:449-477).  numpy legacy
+// randint(min_id, max_id) = min_id + masked-rejection draw of 32-bit words.
+// The draw/validate chain is evaluated 64 words at a time speculatively; a
+// ballot/prefix-count finds where the reference's loop would have stopped.
+// ---------------------------------------------------------------------------
+__device__ inline void uniform_sample_body(const ReplayView& v, int B, int32_t* out) {
+  const int lane = threadIdx.x;
+  dq_replay_meta* meta = v.meta;
+  int64_t pos = meta->tape_pos;
+  const int64_t pos0 = pos;
+  if (meta->status != 0) {
+    if (lane == 0) meta->reserved[0] = pos0;
+    for (int i = lane; i < B; i += kWave) out[i] = 0;
+    return;
+  }
+  const int64_t add_count = meta->add_count;
+  const int64_t cursor = add_count % v.C;
+  int64_t min_id, max_id;
+  if (add_count >= v.C) {
+    min_id = cursor - v.C + v.S - 1;
+    max_id = cursor - v.n;
+  } else {
+    min_id = v.S - 1;
+    max_id = cursor - v.n;
+    if (max_id <= min_id) {
+      if (lane == 0) {
+        latch(meta, DQ_ST_TOO_FEW, 0, 0.0);
+        meta->reserved[0] = pos0;
+      }
+      for (int i = lane; i < B; i += kWave) out[i] = 0;
+      return;
+    }
+  }
+  const uint64_t rng = (uint64_t)(max_id - min_id - 1);
+  uint64_t mask = rng;
+  mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4;
+  mask |= mask >> 8; mask |= mask >> 16; mask |= mask >> 32;
+  const int64_t len = meta->tape_len;
+  int count = 0, fails = 0;
+  bool tape_dry = false;
+  if (rng == 0) {  // randint consumes no word when high - low == 1
+    const int64_t idx = pymod(min_id, v.C);
+    const bool ok = is_valid(v, idx, add_count);
+    if (ok) {
+      for (int i = lane; i < B; i += kWave) out[i] = (int32_t)idx;
+      count = B;
+    } else {
+      fails = v.max_attempts;
+    }
+  } else {
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    while (count < B && fails < v.max_attempts) {
+      const int64_t avail = len - pos;
+      if (avail <= 0) { tape_dry = true; break; }
+      const bool live = lane < avail;
+      const uint64_t w = live ? (uint64_t)v.tape[pos + lane] : 0ull;
+      const uint64_t val = w & mask;
+      const bool drawn = live && val <= rng;
+      const int64_t idx = pymod(min_id + (int64_t)val, v.C);
+      const bool ok = drawn && is_valid(v, idx, add_count);
+      const bool bad = drawn && !ok;
+      const uint64_t okm = __ballot(ok), badm = __ballot(bad);
+      const int cok = count + __popcll(okm & below) + (ok ? 1 : 0);
+      const int cbad = fails + __popcll(badm & below) + (bad ? 1 : 0);
+      const bool stop = (ok && cok == B) || (bad && cbad == v.max_attempts);
+      const uint64_t stopm = __ballot(stop);
+      if (stopm) {
+        const int s = __ffsll((unsigned long long)stopm) - 1;
+        if (ok && lane <= s) out[cok - 1] = (int32_t)idx;
+        count = __shfl(cok, s);
+        fails = __shfl(cbad, s);
+        pos += s + 1;
+        break;
+      }
+      if (ok) out[cok - 1] = (int32_t)idx;
+      count += __popcll(okm);
+      fails += __popcll(badm);
+      const int64_t used = avail < kWave ? avail : kWave;
+      pos += used;
+      if (used < kWave) { tape_dry = true; break; }
+    }
+  }
+  if (lane == 0) {
+    if (tape_dry) latch(meta, DQ_ST_TAPE_EXHAUSTED, count, 0.0);
+    else if (count != B) latch(meta, DQ_ST_MAX_ATTEMPTS, count, 0.0);
+    meta->reserved[0] = pos0;   // entry cursor, for dq_replay_rewind_last_sample
+    meta->tape_pos = pos;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Frame-stack gather.  grid.y = (sample b, state|next_state, stack slot k);
+// each block copies one 84x84 frame (contiguous obs_bytes) of the stack.  Frames
+// are independent contiguous blocks, so the store is fully coalesced and the
+// stacking axis becomes the channel axis (NCHW) for free.
+// ---------------------------------------------------------------------------
+struct GatherOut {
+  const int32_t* indices;
+  void* state;
+  void* next_state;
+  int32_t* action;
+  float* reward;
+  int32_t* next_action;
+  float* next_reward;
+  uint8_t* terminal;
+  int32_t* indices_out;
+  float* probs;
+};
+
+// n-step trajectory length with every terminal byte of the trajectory loaded up
+// front (independent loads, no serial early exit).  Same result as traj_len.
+__device__ __forceinline__ int traj_len_par(const ReplayView& v, int64_t idx, bool* term) {
+  for (int j0 = 0; j0 < v.n; j0 += 8) {
+    uint8_t t[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) t[q] = (j0 + q < v.n) ? v.terminals[pymod(idx + j0 + q, v.C)] : 0;
+    int first = -1;
+#pragma unroll
+    for (int q = 7; q >= 0; --q)
+      if (t[q]) first = q;
+    if (first >= 0) {
+      *term = true;
+      return j0 + first + 1;
+    }
+  }
+  *term = false;
+  return v.n;
+}
+
+__device__ __forceinline__ int64_t stack_base(const ReplayView& v, const GatherOut& g, int b,
+                                              int which) {
+  int64_t base = pymod((int64_t)g.indices[b], v.C);
+  if (which) {
+    bool term;
+    base = pymod(base + traj_len_par(v, base, &term), v.C);
+  }
+  return base;
+}
+
+// Per-sample scalars (crb:517-555), one wave: lanes load the trajectory's
+// terminal/reward bytes in parallel, the ballot finds L, lane 0 sums the
+// float32 products left to right exactly as numpy's n < 8 reduction does.
+__device__ inline void write_scalars_wave(const ReplayView& v, const GatherOut& g, int b) {
+  const int lane = threadIdx.x & 63;
+  const int64_t idx = pymod((int64_t)g.indices[b], v.C);
+  float p = 0.0f;
+  bool t = false;
+  if (lane < v.n) {
+    const int64_t j = pymod(idx + lane, v.C);
+    t = v.terminals[j] != 0;
+    p = __fmul_rn(v.discount[lane], v.rewards[j]);
+  }
+  // trajectories longer than a wave are finished by lane 0 below (n > 64 is unheard of)
+  const uint64_t tm = __ballot(t);
+  int L = v.n;
+  bool term = false;
+  if (tm) {
+    L = __ffsll((unsigned long long)tm);
+    term = true;
+  }
+  float acc = 0.0f;
+  for (int k = 0; k < L && k < kWave; ++k) acc = __fadd_rn(acc, __shfl(p, k));
+  if (lane == 0) {
+    if (v.n > kWave) {  // generic tail, serial
+      bool tt;
+      L = traj_len(v, idx, &tt);
+      term = tt;
+      acc = 0.0f;
+      for (int k = 0; k < L; ++k)
+        acc = __fadd_rn(acc, __fmul_rn(v.discount[k], v.rewards[pymod(idx + k, v.C)]));
+    }
+    const int64_t nxt = pymod(idx + L, v.C);
+    if (g.action) g.action[b] = v.actions[idx];
+    if (g.reward) g.reward[b] = acc;
+    if (g.next_action) g.next_action[b] = v.actions[nxt];
+    if (g.next_reward) g.next_reward[b] = v.rewards[nxt];
+    if (g.terminal) g.terminal[b] = term ? 1 : 0;
+    if (g.indices_out) g.indices_out[b] = (int32_t)idx;
+    if (g.probs) g.probs[b] = (float)v.tree[((int64_t)1 << v.depth) - 1 + idx];
+  }
+}
+
+__device__ __forceinline__ float4 u8x4_to_f32_255(uint32_t w) {
+  float4 o;  // tf.div(tf.cast(x, f32), 255.) -- correctly rounded division
+  o.x = __fdiv_rn((float)(w & 0xffu), 255.0f);
+  o.y = __fdiv_rn((float)((w >> 8) & 0xffu), 255.0f);
+  o.z = __fdiv_rn((float)((w >> 16) & 0xffu), 255.0f);
+  o.w = __fdiv_rn((float)(w >> 24), 255.0f);
+  return o;
+}
+
+// NHWC float32 (the reference's state layout (B, H, W, stack), stack == 4): one
+// block column per (b, which) stack; each wave takes R chunks of 64 dwords (256
+// pixels) of each of the 4 frames -- all 4R loads in flight together -- and
+// writes 4 pixels x 4 channels = 64 contiguous bytes per lane per store.
+// (bx, slot) = the block's coordinates in the (column blocks, 2B) grid; tid in [0, 256).
+template <int R>
+__device__ __forceinline__ void gather_nhwc4_body(const ReplayView& v, const GatherOut& g, int bx,
+                                                  int slot, int tid) {
+  const int b = slot >> 1, which = slot & 1;
+  if (bx == 0 && which == 0 && tid < 64) write_scalars_wave(v, g, b);
+  float* dst_base = (float*)(which ? g.next_state : g.state);
+  if (!dst_base) return;
+  const int64_t nd = v.obs_bytes >> 2;
+  const int lane = tid & 63;
+  // this wave's R x 64 dwords of each of the 4 frames
+  const int64_t w0 = ((int64_t)bx * 256 + (tid & ~63)) * R;
+  if (w0 >= nd) return;
+  const int64_t base = stack_base(v, g, b, which);
+  const uint32_t* fr[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    fr[k] = (const uint32_t*)(v.frames + pymod(base - 3 + k, v.C) * v.obs_bytes);
+  uint32_t w[R][4];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int64_t d = w0 + 64 * r + lane;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[r][k] = d < nd ? fr[k][d] : 0u;
+  }
+  // store j of chunk r: lane l writes pixel 64j + l of the chunk (its 4 channels =
+  // 16 B), so every store instruction covers 1 KiB contiguous; the bytes come from
+  // lane 16j + l/4.
+  const int sh = 8 * (lane & 3);
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int64_t d0 = w0 + 64 * r;
+    float4* dst = (float4*)(dst_base + (int64_t)b * 4 * v.obs_bytes) + 4 * d0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int src = 16 * j + (lane >> 2);
+      float4 o;
+      o.x = __fdiv_rn((float)((__shfl(w[r][0], src) >> sh) & 0xffu), 255.0f);
+      o.y = __fdiv_rn((float)((__shfl(w[r][1], src) >> sh) & 0xffu), 255.0f);
+      o.z = __fdiv_rn((float)((__shfl(w[r][2], src) >> sh) & 0xffu), 255.0f);
+      o.w = __fdiv_rn((float)((__shfl(w[r][3], src) >> sh) & 0xffu), 255.0f);
+      if (4 * d0 + 64 * j + lane < 4 * nd) dst[64 * j + lane] = o;
+    }
+  }
+}
+
+// R = 1: measured fastest at B = 32 (R = 2 / 4: 5.3 / 6.7 us vs 5.1 us per launch)
+constexpr int kNhwcR = 1;
+
+// ---------------------------------------------------------------------------
+// Sum-tree ordered batch update (sum_tree.py:178-205 called in order by
+// prioritized_replay_buffer.py:213-214 or :139).  One wave; lane L owns tree
+// level L.  For each update i (in order) the leaf lane computes
+// delta_i = value_i - leaf, every level adds delta_i to its node, and the new
+// value is forwarded (through LDS) to the next update hitting the same node, so
+// each node receives exactly the reference's ordered chain of float64 adds.
+// Threads 0..63 of the block (any others have returned).
+// Index source: explicit array, or (add path) consecutive cursor slots.
+// ---------------------------------------------------------------------------
+struct SetArgs {
+  const int32_t* indices;  // NULL => (add_count + i) mod C
+  const float* values;
+  int64_t n;
+};
+
+constexpr int kSumtreeSetLds = kWave * (kWave + 1) * 8 + kWave * 8 + kWave * 4 + kWave * kWave;
+
+__device__ inline void sumtree_set_body(const ReplayView& v, const SetArgs& a, void* lds) {
+  double (*s_cur)[kWave + 1] = (double (*)[kWave + 1])lds;
+  int64_t* s_idx = (int64_t*)(s_cur + kWave);
+  float* s_val = (float*)(s_idx + kWave);
+  int8_t (*s_next)[kWave] = (int8_t (*)[kWave])(s_val + kWave);  // [level][i] -> next update sharing the node
+  const int lane = threadIdx.x;
+  dq_replay_meta* meta = v.meta;
+  if (meta->status != 0) return;
+  const int depth = v.depth;
+  const int64_t base = meta->add_count;
+  double maxrec = meta->max_recorded_priority;
+  bool stop = false;
+  for (int64_t c0 = 0; c0 < a.n && !stop; c0 += kWave) {
+    const int m = (int)((a.n - c0) < kWave ? (a.n - c0) : kWave);
+    if (lane < m) {
+      s_idx[lane] = a.indices ? (int64_t)a.indices[c0 + lane] : pymod(base + c0 + lane, v.C);
+      s_val[lane] = a.values[c0 + lane];
+    }
+    __syncthreads();
+    // the reference raises at the first negative value, after applying the earlier ones
+    const bool badi = lane < m && (s_idx[lane] < 0 || s_idx[lane] >= ((int64_t)1 << depth));
+    const uint64_t negm = __ballot(lane < m && (s_val[lane] < 0.0f || badi));
+    int me = m;
+    if (negm) {
+      me = __ffsll((unsigned long long)negm) - 1;
+      stop = true;
+    }
+    for (int i = 0; i < me; ++i) {  // max(value, max_rec) with Python's argument order
+      const double x = (double)s_val[i];
+      maxrec = (maxrec > x) ? maxrec : x;
+    }
+    // next-same table: levels 0..D(i,j) share a node between updates i < j
+    for (int d = 0; d <= depth; ++d)
+      if (lane < me) s_next[d][lane] = -1;
+    __syncthreads();
+    if (lane < me) {
+      int covered = -1;
+      for (int j = lane + 1; j < me && covered < depth; ++j) {
+        const uint64_t x = (uint64_t)(s_idx[lane] ^ s_idx[j]);
+        const int D = x ? depth - (64 - __clzll(x)) : depth;
+        for (int d = covered + 1; d <= D; ++d) s_next[d][lane] = (int8_t)j;
+        if (D > covered) covered = D;
+      }
+    }
+    __syncthreads();
+    const bool mine = lane <= depth;
+    const int shift = depth - lane;
+    const int64_t loff = ((int64_t)1 << (mine ? lane : 0)) - 1;
+    if (mine)
+      for (int i = 0; i < me; ++i) s_cur[lane][i] = v.tree[loff + (s_idx[i] >> shift)];
+    __syncthreads();
+    for (int i = 0; i < me; ++i) {
+      const double cur = mine ? s_cur[lane][i] : 0.0;
+      const double dl = __dsub_rn((double)s_val[i], cur);  // meaningful on the leaf lane
+      const double delta = __shfl(dl, depth);
+      if (mine) {
+        const double x = __dadd_rn(cur, delta);
+        const int j = s_next[lane][i];
+        if (j >= 0)
+          s_cur[lane][j] = x;
+        else
+          v.tree[loff + (s_idx[i] >> shift)] = x;
+      }
+    }
+    __syncthreads();
+    if (stop && lane == 0) {
+      const bool oob = s_idx[me] < 0 || s_idx[me] >= ((int64_t)1 << depth);
+      latch(meta, oob ? DQ_ST_BAD_INDEX : DQ_ST_NEG_PRIORITY, (int)(c0 + me),
+            oob ? (double)s_idx[me] : (double)s_val[me]);
+    }
+  }
+  if (lane == 0) meta->max_recorded_priority = maxrec;
+}
+
+// A replay operation recorded for a grouped launch instead of launched (the
+// opaque dq_rider of the C ABI): the sum-tree update, an index sample or the
+// NHWC gather, run by RiderOp (nature_cnn.hip) as extra blocks of a launch.
+enum RiderKind : int32_t { kRiderNone = 0, kRiderSet = 1, kRiderPerSample = 2,
+                           kRiderUniformSample = 3, kRiderGatherNhwc = 4 };
+
+struct RiderDesc {
+  int32_t kind;
+  int32_t batch;
+  int32_t gx;        // gather: column blocks of 256 threads per (b, which) stack
+  int32_t pad;
+  ReplayView v;
+  GatherOut g;
+  SetArgs s;
+  int32_t* out;      // sample: indices
+};
+static_assert(sizeof(RiderDesc) <= sizeof(dq_rider), "dq_rider too small");
+
+constexpr int kRiderLds = kSumtreeSetLds > kPerSampleLds ? kSumtreeSetLds : kPerSampleLds;
+
+// Runs rider r as block blk of a launch with T >= 256 threads per block.
+template <int T>
+__device__ __forceinline__ void run_rider(const RiderDesc& r, int blk, void* lds) {
+  static_assert(T % 256 == 0, "rider blocks are whole 256-thread gather sub-blocks");
+  const int t = threadIdx.x;
+  switch (r.kind) {
+    case kRiderSet:
+      if (t < kWave) sumtree_set_body(r.v, r.s, lds);
+      return;
+    case kRiderPerSample:
+      if (t < kWave) per_sample_body(r.v, r.batch, r.out, lds);
+      return;
+    case kRiderUniformSample:
+      if (t < kWave) uniform_sample_body(r.v, r.batch, r.out);
+      return;
+    case kRiderGatherNhwc: {
+      const int sub = blk * (T / 256) + t / 256;
+      const int slot = sub / r.gx;
+      if (slot < 2 * r.batch) gather_nhwc4_body<kNhwcR>(r.v, r.g, sub - slot * r.gx, slot, t & 255);
+      return;
+    }
+    default:
+      return;
+  }
+}
+
+template <int T>
+inline int rider_blocks(const RiderDesc& r) {
+  if (r.kind == kRiderGatherNhwc) return (r.gx * 2 * r.batch + T / 256 - 1) / (T / 256);
+  return r.kind == kRiderNone ? 0 : 1;
+}
+
+}  // namespace dq

@@ -10,6 +10,7 @@ etc.) synchronise and return exactly what the reference returns; the learner
 uses ``sample_device`` which stays on the device and never synchronises.
 """
 import collections
+import contextlib
 import ctypes
 import gzip
 import math
@@ -111,6 +112,7 @@ class OutOfGraphReplayBuffer(object):
         [math.pow(self._gamma, n) for n in range(update_horizon)], dtype=np.float32)
     self._discount_dev = torch.from_numpy(self._cumulative_discount_vector).to(self._device)
     self._last_terminal = 0
+    self._riders = None            # list while recording() is active
     self._rng = RNGTape(self, rng if rng is not None else default_stream(self._prioritized),
                         tape_words, self._device)
     self._create_handle()
@@ -431,6 +433,16 @@ class OutOfGraphReplayBuffer(object):
     if out is None:
       out = self._alloc_batch(batch_size, layout)
     p = _lib.ptr
+    if self._riders is not None:
+      if layout != _lib.LAYOUT_F32_NHWC or self._extra_storage_types:
+        raise ValueError('only the NHWC gather (no extra storage) can be recorded as a rider')
+      r = _lib.Rider()
+      _lib.call('dq_replay_record_gather_nhwc', self._h, p(d_idx), batch_size, p(out['state']),
+                p(out['next_state']), p(out['action']), p(out['reward']), p(out['next_action']),
+                p(out['next_reward']), p(out['terminal']), p(out['indices']),
+                p(out.get('sampling_probabilities')), ctypes.byref(r))
+      self._riders.append(r)
+      return out
     _lib.call('dq_replay_gather', self._h, p(d_idx), batch_size, layout, p(out['state']),
               p(out['next_state']), p(out['action']), p(out['reward']), p(out['next_action']),
               p(out['next_reward']), p(out['terminal']), p(out['indices']),
@@ -467,9 +479,30 @@ class OutOfGraphReplayBuffer(object):
         self.reserve_rng(B)
       if 'sample_indices' not in out:
         out['sample_indices'] = torch.empty((B,), dtype=torch.int32, device=self._device)
-      _lib.call('dq_replay_sample_indices', self._h, B, _lib.ptr(out['sample_indices']), self._stream)
+      if self._riders is not None:
+        r = _lib.Rider()
+        _lib.call('dq_replay_record_sample', self._h, B, _lib.ptr(out['sample_indices']),
+                  ctypes.byref(r))
+        self._riders.append(r)
+      else:
+        _lib.call('dq_replay_sample_indices', self._h, B, _lib.ptr(out['sample_indices']),
+                  self._stream)
       indices = out['sample_indices']
     return self._gather(indices, B, layout, out)
+
+  @contextlib.contextmanager
+  def recording(self):
+    """Inside, the device replay operations (sample_device's sample and NHWC
+    gather, a prioritized buffer's device-tensor set_priority) are recorded as
+    riders -- returned in the yielded list, in issue order -- instead of
+    launched; HipNatureCNN.backward(riders=...) runs them inside its grouped
+    launches.  Host-side bookkeeping (RNG tape reservation) is unchanged."""
+    assert self._riders is None, 'recording() does not nest'
+    self._riders = []
+    try:
+      yield self._riders
+    finally:
+      self._riders = None
 
   def rewind_last_sample(self):
     """Give back the RNG-tape words of the most recent device sample (whose

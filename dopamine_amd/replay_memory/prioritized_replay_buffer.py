@@ -48,6 +48,12 @@ class OutOfGraphPrioritizedReplayBuffer(circular_replay_buffer.OutOfGraphReplayB
     if isinstance(indices, torch.Tensor):
       assert indices.dtype == torch.int32, 'Indices must be integers, given: {}'.format(indices.dtype)
       n = indices.numel()
+      if self._riders is not None:
+        r = _lib.Rider()
+        _lib.call('dq_replay_record_sumtree_set', self._h, _lib.ptr(indices),
+                  _lib.ptr(priorities), n, ctypes.byref(r))
+        self._riders.append(r)
+        return
       _lib.call('dq_sumtree_set', self._h, _lib.ptr(indices), _lib.ptr(priorities), n, self._stream)
       return
     assert indices.dtype == np.int32, ('Indices must be integers, '

@@ -138,6 +138,25 @@ int dq_replay_rewind_last_sample(dq_replay* h, void* stream);
 /* synchronous: copies the control block to host memory. */
 int dq_replay_read_meta(dq_replay* h, dq_replay_meta* out, void* stream);
 
+/* Recorded replay operations ("riders").  Instead of launching, these fill an
+ * opaque descriptor with exactly the work the matching call above would launch
+ * (same device code, same arguments); dq_cnn_backward_riders then runs rider i
+ * as extra blocks of its i-th grouped launch, so the next batch's priority
+ * write-back -> sample -> gather chain rides inside the backward on ONE stream
+ * (kernel boundaries keep the chain ordered).  Same semantics as
+ * dq_sumtree_set / dq_replay_sample_indices / dq_replay_gather(DQ_LAYOUT_F32_NHWC). */
+typedef struct dq_rider {
+  int64_t words[40];              /* opaque */
+} dq_rider;
+int dq_replay_record_sumtree_set(dq_replay* h, const int32_t* indices, const float* priorities,
+                                 int64_t n, dq_rider* out);
+int dq_replay_record_sample(dq_replay* h, int32_t batch, int32_t* indices_out, dq_rider* out);
+int dq_replay_record_gather_nhwc(dq_replay* h, const int32_t* indices, int32_t batch,
+                                 float* state_out, float* next_state_out, int32_t* action_out,
+                                 float* reward_out, int32_t* next_action_out,
+                                 float* next_reward_out, uint8_t* terminal_out,
+                                 int32_t* indices_out, float* probs_out, dq_rider* out);
+
 /* ---------------- learner-side kernels (stateless) ---------------- */
 
 /* Rainbow/C51 target distribution + projection + softmax cross-entropy + PER
@@ -247,6 +266,14 @@ int dq_cnn_backward_adam(const dq_cnn_params* p, const dq_cnn_params* g, int32_t
 int dq_cnn_backward_groups(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch,
                            const float* x, const dq_cnn_acts* a, const float* dout,
                            dq_cnn_acts* d, float* ws, int32_t first, int32_t last, void* stream);
+/* dq_cnn_backward (opt NULL) or dq_cnn_backward_adam (opt set) with riders[i] (recorded by
+   dq_replay_record_*) as extra blocks of grouped launch i, i < n_riders <= 7: a chain of
+   riders runs in order, each after the launches before its own.  Riders must not touch
+   x, a, dout, d, g or ws.  CNN results are bitwise those of the rider-less call. */
+int dq_cnn_backward_riders(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch,
+                           const float* x, const dq_cnn_acts* a, const float* dout,
+                           dq_cnn_acts* d, float* ws, const dq_rider* riders, int32_t n_riders,
+                           const dq_adam_args* opt, void* stream);
 /* one layer of the backward: layer 0..4 = fc2, fc1, conv3, conv2, conv1; part 1 = weight and
    bias gradient, part 0 = input gradient (not for conv1).  dW(L) depends only on dX(L-1),
    so the weight gradients may run on a second stream, each with its own ws. */

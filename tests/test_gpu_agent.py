@@ -159,3 +159,36 @@ def test_action_q_values_on_the_hip_cnn_match_torch(kind):
     assert (q_hip - q_ref).abs().max().item() <= 2e-5 * scale
     with torch.no_grad():
       a.online_convnet.fp.flat.mul_(1.1)        # the graph reads the parameters in place
+
+
+@pytest.mark.parametrize('kind', ['rainbow', 'dqn'])
+@pytest.mark.parametrize('graph', [False, True])
+def test_replay_riders_match_the_two_stream_schedule(kind, graph):
+  """ride_replay (priority write-back -> sample -> gather as riders of the
+  backward's grouped launches, one stream) draws the same batches and produces
+  the same parameters and sum tree, bit for bit, as the two-stream prefetch."""
+  from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
+  res = []
+  for ride in (False, True):
+    random.seed(7); np.random.seed(7); torch.manual_seed(7)
+    if kind == 'rainbow':
+      a = _rainbow(use_hip_graph=graph, ride_replay=ride)
+    else:
+      a = DQNAgent(num_actions=6, replay_capacity=3000, batch_size=32, min_replay_history=100,
+                   use_hip_graph=graph, ride_replay=ride)
+      _fill(a._replay.memory, 6, 3)
+    idx = []
+    for _ in range(9):
+      a._run_train_op()
+      idx.append(a._replay.transition['indices'].cpu().numpy().copy())
+    a._discard_prefetch()
+    a._replay.memory.sync_rng()
+    leaves = a._replay.memory.sum_tree.nodes[-1].copy() if kind == 'rainbow' else None
+    res.append((np.stack(idx), a.online_convnet.fp.flat.cpu().numpy(), leaves,
+                a._replay.transition['state'].cpu().numpy()))
+    assert (a._graphs is not None) == graph
+  np.testing.assert_array_equal(res[0][0], res[1][0])
+  np.testing.assert_array_equal(res[0][1], res[1][1])
+  np.testing.assert_array_equal(res[0][3], res[1][3])
+  if kind == 'rainbow':
+    np.testing.assert_array_equal(res[0][2], res[1][2])
