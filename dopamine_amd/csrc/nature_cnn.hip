@@ -947,17 +947,19 @@ bool backward_layer(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int 
   }
 }
 
-// Backward in 7 grouped launches (13 kernels' worth of work; with kAdam also the
-// optimizer, in the last launch: the conv1 split-K sum applies TF1 Adam in its
-// epilogue, and an AdamOp streams the contiguous conv2..fc2 range, whose
-// gradients are all final and whose weights have had their last use by then):
+// Backward in 7 grouped launches (13 kernels' worth of work):
 //   1: dh                      (fc2 input grad)
 //   2: dW fc2     | da3        (fc1 input grad)
-//   3: dW fc1     | da2        (conv3 input grad)
-//   4: dW conv3 slabs | dcol   (conv2 input grad, dense part)
-//   5: sum conv3 slabs | dW conv2 slabs | da1 = col2im(dcol)
-//   6: sum conv2 slabs | dW conv1 slabs
-//   7: sum conv1 slabs
+//   3: dW fc1     | da2        (conv3 input grad)              [+ Adam fc2]
+//   4: dW conv3 slabs | dcol   (conv2 input grad, dense part)  [+ Adam fc1, 1st third]
+//   5: sum conv3 slabs | dW conv2 slabs | da1 = col2im(dcol)   [+ Adam fc1, 2nd third]
+//   6: sum conv2 slabs | dW conv1 slabs                        [+ Adam fc1, 3rd third]
+//   7: sum conv1 slabs                                         [+ Adam conv2, conv3]
+// With kAdam the TF1 Adam step is spread as bracketed: float4 AdamOps over ranges
+// whose gradients are final and whose weights have had their last read; conv1's
+// split-K sum applies it in its epilogue (and advances the beta powers).  The
+// optimizer's 47 MB of traffic then overlaps the latency-bound GEMM launches
+// instead of running as an 18 us launch of its own.
 // Each GEMM writes its gradient/activation exactly as the per-layer form does
 // (same tiles, same summation order), so the two are bitwise identical.
 template <bool kAdam>
@@ -1008,25 +1010,41 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
       GE::make(g->conv1_w, g->conv1_b, Conv1::K, p->conv1_w, p->conv1_b, opt, 1)};
   auto in = [&](int i) { return first <= i && i < last; };
   auto rd = [&](int i) { return i < n_riders ? riders + i : nullptr; };   // rider of launch i
+  if constexpr (kAdam) {
+    {
+      // The optimizer spread over the launches after each gradient is final (fc2 after
+      // launch 2, fc1 after launch 3) and each weight's last read: fc2 rides in launch 3,
+      // fc1 in thirds in launches 4-6, conv2..conv3 with conv1's epilogue in launch 7.
+      const dq_adam_args* o = opt.a;
+      const AdamDev od{o->state, o->slot, o->lr, o->beta1, o->beta2, o->epsilon};
+      auto part = [&](float* w0, float* w1) {
+        const ptrdiff_t off = w0 - o->var;
+        const int64_t n = (int64_t)(w1 - w0);
+        const int nb = (int)std::max<int64_t>(1, ((n >> 2) + kGroupT - 1) / kGroupT);
+        return AdamOp{w0, g->conv1_w + (w0 - p->conv1_w), o->m + off, o->v + off, n, od, nb};
+      };
+      float* f0 = p->fc1_w;
+      float* f3 = p->fc2_w;                          // fc1_w .. fc1_b (+ pad)
+      const int64_t third = ((f3 - f0) / 3) & ~(int64_t)3;
+      float* f1 = f0 + third;
+      float* f2 = f1 + third;
+      if (in(0)) group_r(c, rd(0), dX_fc2);
+      if (in(1)) group_r(c, rd(1), dW_fc2, dX_fc1);
+      if (in(2)) group_r(c, rd(2), dW_fc1, dX_c3, part(p->fc2_w, p->fc2_b + NO));
+      if (in(3)) group_r(c, rd(3), dW_c3, dcol, part(f0, f1));
+      if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, da1, part(f1, f2));
+      if (in(5)) group_r(c, rd(5), sum_c2, dW_c1, part(f2, f3));
+      if (in(6)) group_r(c, rd(6), sum_c1, part(p->conv2_w, p->fc1_w));
+      return;
+    }
+  }
   if (in(0)) group_r(c, rd(0), dX_fc2);
   if (in(1)) group_r(c, rd(1), dW_fc2, dX_fc1);
   if (in(2)) group_r(c, rd(2), dW_fc1, dX_c3);
   if (in(3)) group_r(c, rd(3), dW_c3, dcol);
   if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, da1);
   if (in(5)) group_r(c, rd(5), sum_c2, dW_c1);
-  if (!in(6)) return;
-  if constexpr (kAdam) {
-    const dq_adam_args* o = opt.a;
-    float* w0 = p->conv2_w;
-    const ptrdiff_t off = w0 - o->var;
-    const int64_t n = (int64_t)((p->fc2_b + NO) - w0);
-    const int nb = (int)std::max<int64_t>(1, ((n >> 2) + kGroupT - 1) / kGroupT);  // 1 float4 / thread
-    AdamOp rest{w0, g->conv2_w, o->m + off, o->v + off, n,
-                AdamDev{o->state, o->slot, o->lr, o->beta1, o->beta2, o->epsilon}, nb};
-    group_r(c, rd(6), sum_c1, rest);
-  } else {
-    group_r(c, rd(6), sum_c1);
-  }
+  if (in(6)) group_r(c, rd(6), sum_c1);
 }
 
 }  // namespace cnn

@@ -1,6 +1,6 @@
 """Rainbow learner steps on synthetic replay; saves the online parameters and the
 sampled indices (np.save) -- run under two DOPAMINE_AMD_LIB builds to check that
-a kernel change is bitwise neutral.   python tools/dump_params.py out.npz [steps] [ride]"""
+a kernel change is bitwise neutral.   python tools/dump_params.py out.npz [steps] [ride] [fuse]"""
 import os
 import random
 import sys
@@ -16,10 +16,13 @@ def main():
   out = sys.argv[1]
   steps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
   ride = bool(int(sys.argv[3])) if len(sys.argv) > 3 else True
+  fuse = bool(int(sys.argv[4])) if len(sys.argv) > 4 else False
   from dopamine_amd.agents.optimizers import AdamOptimizer
   from dopamine_amd.agents.rainbow.rainbow_agent import RainbowAgent
   random.seed(0); np.random.seed(0); torch.manual_seed(0)
-  kw = {} if ride else {'ride_replay': False}
+  kw = {'fuse_optimizer': fuse}
+  if not ride:
+    kw['ride_replay'] = False
   a = RainbowAgent(num_actions=9, update_horizon=3, replay_capacity=100_000, batch_size=32,
                    min_replay_history=100, device=torch.device('cuda', 0),
                    optimizer=AdamOptimizer(learning_rate=6.25e-5, epsilon=1.5e-4), **kw)

@@ -36,6 +36,40 @@ __global__ __launch_bounds__(256) void k_adam_u(float* __restrict__ var, const f
   }
 }
 
+typedef float f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void nt_store(float4 x, float4* p) {
+  f4v v = {x.x, x.y, x.z, x.w};
+  __builtin_nontemporal_store(v, (f4v*)p);
+}
+
+// nontemporal stores for the moments (streamed: next read one step later) and/or the weights
+template <bool NT_MV, bool NT_VAR>
+__global__ __launch_bounds__(256) void k_adam_nt(float* __restrict__ var, const float* __restrict__ grad,
+                                                 float* __restrict__ m, float* __restrict__ v,
+                                                 const float* state, int64_t n4, float lr) {
+  const float alpha = adam_alpha_of(state, 0, lr);
+  const float omb1 = 0.1f, omb2 = 0.001f, eps = 1.5e-4f;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  float4 p = ((float4*)var)[i], g = ((const float4*)grad)[i];
+  float4 mm = ((float4*)m)[i], vv = ((float4*)v)[i];
+  adam1(p.x, g.x, mm.x, vv.x, alpha, omb1, omb2, eps);
+  adam1(p.y, g.y, mm.y, vv.y, alpha, omb1, omb2, eps);
+  adam1(p.z, g.z, mm.z, vv.z, alpha, omb1, omb2, eps);
+  adam1(p.w, g.w, mm.w, vv.w, alpha, omb1, omb2, eps);
+  if (NT_VAR) {
+    nt_store(p, (float4*)var + i);
+  } else {
+    ((float4*)var)[i] = p;
+  }
+  if (NT_MV) {
+    nt_store(mm, (float4*)m + i);
+    nt_store(vv, (float4*)v + i);
+  } else {
+    ((float4*)m)[i] = mm; ((float4*)v)[i] = vv;
+  }
+}
+
 // same traffic, no math
 __global__ __launch_bounds__(256) void k_copy7(float* __restrict__ var, const float* __restrict__ grad,
                                                float* __restrict__ m, float* __restrict__ v, int64_t n4) {
@@ -75,23 +109,22 @@ int main() {
   hipMemcpy(state, st, 16, hipMemcpyHostToDevice);
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
   const double bytes = 7.0 * n * 4;
-  auto run = [&](const char* name, auto launch, bool cold) {
-    float tot = 0; int it = 200;
-    for (int r = 0; r < 20; ++r) launch();
+  auto run = [&](const char* name, auto launch, size_t flush_mb) {
+    float tot = 0; int it = 100;
+    for (int r = 0; r < 10; ++r) launch();
     for (int r = 0; r < it; ++r) {
-      if (cold) hipMemsetAsync(flush, r & 0xff, 512 << 20, 0);
+      if (flush_mb) hipMemsetAsync(flush, r & 0xff, flush_mb << 20, 0);
       hipEventRecord(e0, 0); launch(); hipEventRecord(e1, 0);
       hipEventSynchronize(e1); float ms; hipEventElapsedTime(&ms, e0, e1); tot += ms;
     }
     const double us = 1e3 * tot / it;
-    printf("%-28s %-5s %8.2f us  %7.1f GB/s\n", name, cold ? "cold" : "warm", us, bytes / us * 1e-3);
+    printf("%-28s flush %4zu MB %8.2f us  %7.1f GB/s\n", name, flush_mb, us, bytes / us * 1e-3);
   };
-  for (int cold = 0; cold < 2; ++cold) {
-    run("adam U1 (1660 blk)", [&] { hipLaunchKernelGGL(k_adam_u<1>, dim3((n4 + 255) / 256), dim3(256), 0, 0, var, grad, m, v, state, n4, 1e-4f); }, cold);
-    run("adam U2", [&] { hipLaunchKernelGGL(k_adam_u<2>, dim3((n4 + 511) / 512), dim3(256), 0, 0, var, grad, m, v, state, n4, 1e-4f); }, cold);
-    run("adam U4", [&] { hipLaunchKernelGGL(k_adam_u<4>, dim3((n4 + 1023) / 1024), dim3(256), 0, 0, var, grad, m, v, state, n4, 1e-4f); }, cold);
-    run("adam fast math (inexact)", [&] { hipLaunchKernelGGL(k_adam_fast, dim3((n4 + 255) / 256), dim3(256), 0, 0, var, grad, m, v, state, n4, 1e-4f); }, cold);
-    run("copy 4r3w (ceiling)", [&] { hipLaunchKernelGGL(k_copy7, dim3((n4 + 255) / 256), dim3(256), 0, 0, var, grad, m, v, n4); }, cold);
+  const unsigned g1 = (unsigned)((n4 + 255) / 256);
+  for (size_t mb : {0, 16, 32, 64, 128, 256, 512}) {
+    run("adam U1", [&] { hipLaunchKernelGGL(k_adam_u<1>, dim3(g1), dim3(256), 0, 0, var, grad, m, v, state, n4, 1e-4f); }, mb);
+    run("adam nt m,v", [&] { hipLaunchKernelGGL((k_adam_nt<true, false>), dim3(g1), dim3(256), 0, 0, var, grad, m, v, state, n4, 1e-4f); }, mb);
+    run("adam nt m,v,var", [&] { hipLaunchKernelGGL((k_adam_nt<true, true>), dim3(g1), dim3(256), 0, 0, var, grad, m, v, state, n4, 1e-4f); }, mb);
   }
   return 0;
 }
