@@ -67,6 +67,23 @@ __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast
 
 __device__ __forceinline__ float4 sel4(bool ok, float4 v) { return ok ? v : zero4(); }
 
+// Raw buffer loads: an offset at or past num_records reads as zero in hardware,
+// so an out-of-range group costs one offset select instead of a clamped 64-bit
+// address and four data selects.  Valid byte offsets are < 2 GB here.
+constexpr int kOOB = 0x7ffffff0;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, kOOB, 0x00020000);
+}
+__device__ __forceinline__ float4 bload4(const float* base, int off, bool ok) {   // off in floats
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc(base), ok ? off * 4 : kOOB, 0, 0);
+  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
+                     __uint_as_float(v.w));
+}
+__device__ __forceinline__ float bload1(const float* base, int off, bool ok) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc(base), ok ? off * 4 : kOOB, 0, 0));
+}
+
 // forward im2col of an NHWC input: rows = output pixels, k = (kh, kw, ci).
 // CI % 4 == 0, so a 16-byte group never straddles a (kh, kw) tap.
 template <class G>
@@ -84,8 +101,7 @@ struct Im2col {
   }
   __device__ __forceinline__ float4 get(int m, int k, int mlim, int klim) const {
     const int o = offset(m, k);
-    const bool ok = m < mlim && k < klim && o >= 0;
-    return sel4(ok, ld4(x + (ok ? o : 0)));
+    return bload4(x, o, m < mlim && k < klim && o >= 0);
   }
 };
 
@@ -114,7 +130,7 @@ struct Col2im {
     const int kh = kk / G::KW, kw = kk - kh * G::KW;
     const int oh = ih + G::PT - kh, ow = iw + G::PL - kw;
     const bool ok = m < mlim && k < klim && oh >= 0 && ow >= 0 && oh < G::OH && ow < G::OW;
-    return sel4(ok, ld4(dy + (ok ? ((b * G::OH + oh) * G::OW + ow) * G::CO + co : 0)));
+    return bload4(dy, ((b * G::OH + oh) * G::OW + ow) * G::CO + co, ok);
   }
 };
 
@@ -125,8 +141,7 @@ struct WeightT {
   const float* w;
   __device__ __forceinline__ float4 get(int n, int k, int nlim, int klim) const {
     const int kk = k / G::CO, co = k - kk * G::CO;
-    const bool ok = n < nlim && k < klim;
-    return sel4(ok, ld4(w + (ok ? (co * (G::KH * G::KW) + kk) * G::CI + n : 0)));
+    return bload4(w, (co * (G::KH * G::KW) + kk) * G::CI + n, n < nlim && k < klim);
   }
 };
 
@@ -136,8 +151,7 @@ struct RowK {
   const float* p;
   int ld;
   __device__ __forceinline__ float4 get(int r, int k, int rlim, int klim) const {
-    const bool ok = r < rlim && k < klim;
-    return sel4(ok, ld4(p + (ok ? (int64_t)r * ld + k : 0)));
+    return bload4(p, r * ld + k, r < rlim && k < klim);
   }
 };
 // [k][rows] with rows contiguous: dy^T of FC dW (A), W of FC dX as B(n = in, k = out); ld % 4 == 0
@@ -146,8 +160,7 @@ struct ColK {
   const float* p;
   int ld;
   __device__ __forceinline__ float4 get(int r, int k, int rlim, int klim) const {
-    const bool ok = r < rlim && k < klim;
-    return sel4(ok, ld4(p + (ok ? (int64_t)k * ld + r : 0)));
+    return bload4(p, k * ld + r, r < rlim && k < klim);
   }
 };
 // FC dW's B operand: B(n, k = batch) = x[k][n], with the bias ones-column at n == ld
@@ -156,8 +169,7 @@ struct ColKOnes {
   const float* p;
   int ld;
   __device__ __forceinline__ float4 get(int n, int k, int, int klim) const {
-    const bool ok = n < ld && k < klim;
-    const float4 v = sel4(ok, ld4(p + (ok ? (int64_t)k * ld + n : 0)));
+    const float4 v = bload4(p, k * ld + n, n < ld && k < klim);
     return (n == ld && k < klim) ? make_float4(1.0f, 0.0f, 0.0f, 0.0f) : v;
   }
 };
@@ -167,8 +179,7 @@ struct DyT {
   static constexpr bool kFast = false;
   const float* dy;
   __device__ __forceinline__ float4 get(int m, int k, int mlim, int klim) const {
-    const bool ok = m < mlim && k < klim;
-    return sel4(ok, ld4(dy + (ok ? (int64_t)k * CO + m : 0)));
+    return bload4(dy, k * CO + m, m < mlim && k < klim);
   }
 };
 // scalar forms of RowK / ColK for a leading dimension that is not a multiple of 4
@@ -181,9 +192,7 @@ struct RowKScalar {
     float v[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const bool ok = r < rlim && k + j < klim;
-      const float x = p[ok ? (int64_t)r * ld + k + j : 0];
-      v[j] = ok ? x : 0.0f;
+      v[j] = bload1(p, r * ld + k + j, r < rlim && k + j < klim);
     }
     return make_float4(v[0], v[1], v[2], v[3]);
   }
@@ -196,9 +205,7 @@ struct ColKScalar {
     float v[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const bool ok = r + j < rlim && k < klim;
-      const float x = p[ok ? (int64_t)k * ld + r + j : 0];
-      v[j] = ok ? x : 0.0f;
+      v[j] = bload1(p, k * ld + r + j, r + j < rlim && k < klim);
     }
     return make_float4(v[0], v[1], v[2], v[3]);
   }
@@ -370,7 +377,8 @@ struct Tile {
   template <class AL, class BL>
   static constexpr int lds() {      // operand slices, or the WK > 1 reduction scratch
     const int sa = BM + (AL::kFast ? 1 : 4), sb = BN + (BL::kFast ? 1 : 4);
-    const int tile = kPrivate ? WK * 16 * (sa + sb) : BKT * sa + BKT * sb;
+    const int pa = AL::kFast ? 32 * 16 : 16 * 36, pb = BL::kFast ? 32 * 16 : 16 * 36;
+    const int tile = kPrivate ? WK * (pa + pb) : BKT * sa + BKT * sb;
     const int red = WK > 1 ? WK * WM * WN * 1024 : 0;
     return tile > red ? tile : red;
   }
@@ -441,11 +449,16 @@ __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& 
   if constexpr (TL::kPrivate) {
     // Wave-private staging: wave wk fetches its own 32-wide k band (the same
     // coalesced 128-byte row segments as the shared layout) and transposes it
-    // through its own 16-k LDS window in two halves -- no block barrier until
-    // the reduction, and ~half the LDS, so two 1024-thread blocks share a CU.
-    // Same MFMA sequence as the shared path: bitwise identical results.
-    float* Aw = smem + wave * 16 * (SA + SB);
-    float* Bw = Aw + 16 * SA;
+    // through its own LDS window, 16 k at a time -- no block barrier until the
+    // reduction, and about half the LDS, so two 1024-thread blocks share a CU.
+    // MFMA step s of a half takes k = s from lanes 0-31 and k = 8 + s from lanes
+    // 32-63, so a lane's 8 operands of the half are contiguous in k: a k-contiguous
+    // operand is kept [row][16 k] (float4 slots XOR-swizzled by row, conflict-free
+    // 128-bit writes and reads), a row-contiguous one [k][row] (stride 36: its
+    // 128-bit writes and the two half-waves' scalar reads hit disjoint banks).
+    constexpr int WA = AL::kFast ? 32 * 16 : 16 * 36, WB = BL::kFast ? 32 * 16 : 16 * 36;
+    float* Aw = smem + wave * (WA + WB);
+    float* Bw = Aw + WA;
     float4 pa4[4], pb4[4];
     auto fetch = [&](int k0) {
 #pragma unroll
@@ -457,20 +470,35 @@ __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& 
         pb4[i] = B.get(n0 + rr, k0 + kk, N, kend);
       }
     };
+    auto st = [](float* W, bool kfast, int rr, int kl, float4 v) {   // kl in [0, 16)
+      float* q = kfast ? W + rr * 16 + 4 * ((kl >> 2) ^ ((rr >> 2) & 3)) : W + kl * 36 + rr;
+      *reinterpret_cast<float4*>(q) = v;
+    };
     auto stage = [&](int h) {       // k rows [16h, 16h + 16) of this wave's band
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         int rr, kk;
         group_coord<AL::kFast, BM, BKT>(256 * wk + 64 * i + lane, rr, kk);
         kk -= 32 * wk + 16 * h;
-        if (kk >= 0 && kk < 16) put(Aw, SA, AL::kFast, rr, kk, pa4[i]);
+        if (kk >= 0 && kk < 16) st(Aw, AL::kFast, rr, kk, pa4[i]);
         group_coord<BL::kFast, BN, BKT>(256 * wk + 64 * i + lane, rr, kk);
         kk -= 32 * wk + 16 * h;
-        if (kk >= 0 && kk < 16) put(Bw, SB, BL::kFast, rr, kk, pb4[i]);
+        if (kk >= 0 && kk < 16) st(Bw, BL::kFast, rr, kk, pb4[i]);
       }
     };
-    const float* qa = Aw + (lane >> 5) * SA + (lane & 31);
-    const float* qb = Bw + (lane >> 5) * SB + (lane & 31);
+    const int r = lane & 31, hh = lane >> 5;
+    auto operands = [&](const float* W, bool kfast, float* o) {   // o[s] = element (r, 8 hh + s)
+      if (kfast) {
+        const float4 x0 = *reinterpret_cast<const float4*>(W + r * 16 + 4 * ((2 * hh) ^ ((r >> 2) & 3)));
+        const float4 x1 =
+            *reinterpret_cast<const float4*>(W + r * 16 + 4 * ((2 * hh + 1) ^ ((r >> 2) & 3)));
+        o[0] = x0.x; o[1] = x0.y; o[2] = x0.z; o[3] = x0.w;
+        o[4] = x1.x; o[5] = x1.y; o[6] = x1.z; o[7] = x1.w;
+      } else {
+#pragma unroll
+        for (int s = 0; s < 8; ++s) o[s] = W[(8 * hh + s) * 36 + r];
+      }
+    };
     fetch(kbeg);
     for (int k0 = kbeg; k0 < kend; k0 += BKT) {
       const bool live = k0 + wk * 32 < kend;   // wave-uniform: bands past the end are all zero
@@ -483,9 +511,12 @@ __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& 
         __builtin_amdgcn_wave_barrier();
         if (h == 1 && k0 + BKT < kend) fetch(k0 + BKT);
         if (live) {
+          float av[8], bv[8];
+          operands(Aw, AL::kFast, av);
+          operands(Bw, BL::kFast, bv);
 #pragma unroll
-          for (int s = 0; s < 16; s += 2)
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(qa[s * SA], qb[s * SB], acc, 0, 0, 0);
+          for (int s = 0; s < 8; ++s)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc, 0, 0, 0);
         }
       }
     }
