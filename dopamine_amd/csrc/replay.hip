@@ -43,9 +43,11 @@ struct dq_replay {
 
 namespace dq {
 
-__global__ __launch_bounds__(64) void k_per_sample(ReplayView v, int B, int32_t* out) {
+constexpr int kTreeT = 1024;   // block of the block-parallel sum-tree kernels
+
+__global__ __launch_bounds__(kTreeT) void k_per_sample(ReplayView v, int B, int32_t* out) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kPerSampleLds];
-  per_sample_body(v, B, out, lds);
+  per_sample_par<kTreeT>(v, B, out, lds);
 }
 
 __global__ __launch_bounds__(64) void k_uniform_sample(ReplayView v, int B, int32_t* out) {
@@ -129,9 +131,9 @@ __global__ __launch_bounds__(256) void k_gather_raw(ReplayView v, GatherOut g) {
   }
 }
 
-__global__ __launch_bounds__(64) void k_sumtree_set(ReplayView v, SetArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kSumtreeSetLds];
-  sumtree_set_body(v, a, lds);
+__global__ __launch_bounds__(kTreeT) void k_sumtree_set(ReplayView v, SetArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kSumtreeParLds];
+  sumtree_set_par<kTreeT>(v, a, lds);
 }
 
 __global__ void k_sumtree_get(ReplayView v, const int32_t* idx, int64_t n, float* out) {
@@ -240,7 +242,7 @@ int dq_replay_add(dq_replay* h, int64_t n, const uint8_t* frames, const int32_t*
   ReplayView v = h->view();
   if (h->cfg.prioritized) {  // _add: sum_tree.set(cursor, p) before the write (prb:139)
     SetArgs a{nullptr, priorities, n};
-    hipLaunchKernelGGL(k_sumtree_set, dim3(1), dim3(64), 0, s, v, a);
+    hipLaunchKernelGGL(k_sumtree_set, dim3(1), dim3(kTreeT), 0, s, v, a);
     DQ_CHECK_LAUNCH("k_sumtree_set");
   }
   const int64_t work = std::max<int64_t>(n * h->cfg.obs_bytes, n);
@@ -259,7 +261,7 @@ int dq_replay_sample_indices(dq_replay* h, int32_t batch, int32_t* indices_out, 
   DQ_CHECK_ARG(h->st.tape, "RNG tape not attached");
   hipStream_t s = (hipStream_t)stream;
   if (h->cfg.prioritized)
-    hipLaunchKernelGGL(k_per_sample, dim3(1), dim3(64), 0, s, h->view(), batch, indices_out);
+    hipLaunchKernelGGL(k_per_sample, dim3(1), dim3(kTreeT), 0, s, h->view(), batch, indices_out);
   else
     hipLaunchKernelGGL(k_uniform_sample, dim3(1), dim3(64), 0, s, h->view(), batch, indices_out);
   DQ_CHECK_LAUNCH("sample_indices");
@@ -310,7 +312,7 @@ int dq_sumtree_set(dq_replay* h, const int32_t* indices, const float* priorities
   DQ_CHECK_ARG(h->depth < 63, "tree too deep");
   if (n == 0) return DQ_OK;
   SetArgs a{indices, priorities, n};
-  hipLaunchKernelGGL(k_sumtree_set, dim3(1), dim3(64), 0, (hipStream_t)stream, h->view(), a);
+  hipLaunchKernelGGL(k_sumtree_set, dim3(1), dim3(kTreeT), 0, (hipStream_t)stream, h->view(), a);
   DQ_CHECK_LAUNCH("k_sumtree_set");
   return DQ_OK;
 }

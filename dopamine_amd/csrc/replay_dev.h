@@ -504,6 +504,245 @@ __device__ inline void sumtree_set_body(const ReplayView& v, const SetArgs& a, v
   if (lane == 0) meta->max_recorded_priority = maxrec;
 }
 
+// ---------------------------------------------------------------------------
+// Block-parallel forms of the two single-wave chains above (same float64
+// operations in the same order, so bitwise the same trees and indices), for a
+// block of T threads: the riders get a whole 1024-thread block anyway.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int readlane_i(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
+__device__ __forceinline__ float readlane_f(float x, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
+}
+
+// Ordered chain of float64 adds per tree node: update i (lane i) hits node n_i,
+// prev_i = the latest earlier update on n_i (-1: none).  before_i = the node's value
+// before update i (the tree value, or after_prev), after_i = before_i + delta_i --
+// resolved in rounds along the prev links, each round one shuffle.
+__device__ __forceinline__ double node_chain(bool act, int prev, double tree_val, double& delta,
+                                             bool leaf, float val) {
+  bool done = act && prev < 0;
+  double before = tree_val, after = 0.0;
+  if (done) {
+    if (leaf) delta = __dsub_rn((double)val, before);
+    after = __dadd_rn(before, delta);
+  }
+  while (__ballot(act && !done)) {
+    const int src = prev < 0 ? 0 : prev;
+    const double ap = __shfl(after, src);
+    const int dp = __shfl((int)done, src);
+    if (act && !done && dp) {
+      before = ap;
+      if (leaf) delta = __dsub_rn((double)val, before);
+      after = __dadd_rn(before, delta);
+      done = true;
+    }
+  }
+  return after;
+}
+
+constexpr int kSumtreeParLds = kWave * 8;   // bytes: the chunk's deltas
+
+// sum_tree.py:178-205 called in order for each (index, value) of the batch
+// (prioritized_replay_buffer.py:213-214): wave w owns tree levels w, w + T/64, ...,
+// lane i = update i of a <= 64-update chunk.  Phase 1: the leaf level's chain gives
+// every update's delta (value - the leaf as left by the earlier updates); phase 2:
+// each level's nodes take their updates' deltas in update order, and the last
+// update on a node stores it.
+template <int T>
+__device__ inline void sumtree_set_par(const ReplayView& v, const SetArgs& a, void* lds) {
+  constexpr int NW = T / 64;
+  double* s_delta = (double*)lds;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  dq_replay_meta* meta = v.meta;
+  if (meta->status != 0) return;
+  const int depth = v.depth;
+  const int64_t base = meta->add_count;
+  double maxrec = meta->max_recorded_priority;
+  bool stop = false;
+  for (int64_t c0 = 0; c0 < a.n && !stop; c0 += kWave) {
+    const int m = (int)((a.n - c0) < kWave ? (a.n - c0) : kWave);
+    int64_t idx = 0;
+    float val = 0.0f;
+    if (lane < m) {
+      idx = a.indices ? (int64_t)a.indices[c0 + lane] : pymod(base + c0 + lane, v.C);
+      val = a.values[c0 + lane];
+    }
+    // the reference raises at the first negative value, after applying the earlier ones
+    const bool badi = lane < m && (idx < 0 || idx >= ((int64_t)1 << depth));
+    const uint64_t negm = __ballot(lane < m && (val < 0.0f || badi));
+    int me = m;
+    if (negm) {
+      me = __ffsll((unsigned long long)negm) - 1;
+      stop = true;
+    }
+    const bool act = lane < me;
+    if (wave == 0)
+      for (int i = 0; i < me; ++i) {   // max(value, max_rec) with Python's argument order
+        const double x = (double)readlane_f(val, i);
+        maxrec = (maxrec > x) ? maxrec : x;
+      }
+    const int node_leaf = act ? (int)idx : 0;
+    // same-node links at level L (node = leaf >> (depth - L))
+    auto links = [&](int L, int& prev, bool& last) {
+      const int node = node_leaf >> (depth - L);
+      prev = -1;
+      last = true;
+      for (int j = 0; j < me; ++j) {
+        const int nj = readlane_i(node_leaf, j) >> (depth - L);
+        if (nj == node) {
+          if (j < lane) prev = j;
+          if (j > lane) last = false;
+        }
+      }
+    };
+    // this wave's levels: issue every node load first
+    constexpr int KL = (64 + NW - 1) / NW;   // levels per wave, depth < 63
+    double tv[KL];
+#pragma unroll
+    for (int k = 0; k < KL; ++k) {
+      const int L = wave + NW * k;
+      tv[k] = (act && L <= depth) ? v.tree[((int64_t)1 << L) - 1 + (node_leaf >> (depth - L))] : 0.0;
+    }
+    if (wave == depth % NW) {          // the leaf level's owner: deltas
+      int prev;
+      bool last;
+      links(depth, prev, last);
+      double delta = 0.0;
+      node_chain(act, prev, tv[depth / NW], delta, true, val);
+      if (act) s_delta[lane] = delta;
+    }
+    __syncthreads();
+    double delta = act ? s_delta[lane] : 0.0;
+#pragma unroll
+    for (int k = 0; k < KL; ++k) {
+      const int L = wave + NW * k;
+      if (L > depth) break;
+      int prev;
+      bool last;
+      links(L, prev, last);
+      const double after = node_chain(act, prev, tv[k], delta, false, val);
+      if (act && last) v.tree[((int64_t)1 << L) - 1 + (node_leaf >> (depth - L))] = after;
+    }
+    if (stop) {                        // the first bad update: a bad index, else its value
+      const int64_t bi = (int64_t)readlane_i((int)idx, me);   // indices are int32
+      const float bv = readlane_f(val, me);
+      const bool oob = bi < 0 || bi >= ((int64_t)1 << depth);
+      if (threadIdx.x == 0)
+        latch(meta, oob ? DQ_ST_BAD_INDEX : DQ_ST_NEG_PRIORITY, (int)(c0 + me),
+              oob ? (double)bi : (double)bv);
+    }
+    __threadfence_block();
+    __syncthreads();                   // the next chunk reads what this one stored
+  }
+  if (threadIdx.x == 0) meta->max_recorded_priority = maxrec;
+}
+
+// Prioritized stratified sampling (prioritized_replay_buffer.py:152-170 /
+// sum_tree.py:99-139) with T threads: 32 lanes per stratum descend the tree 5
+// levels per round -- lane j of the group loads the left-child sum of subtree node
+// j (breadth-first), then the group walks the 5 levels through shuffles: 4 round
+// trips instead of 20 for a 2^20-leaf tree.  The retry loop for invalid draws is
+// the reference's sequential one (thread 0).
+template <int T>
+__device__ inline void per_sample_par(const ReplayView& v, int B, int32_t* out, void* lds) {
+  static_assert(T % 32 == 0, "32-lane groups");
+  int64_t* s_idx = (int64_t*)lds;
+  uint8_t* s_ok = (uint8_t*)(s_idx + kMaxBatch);
+  const int t = threadIdx.x, g = t >> 5, j = t & 31;
+  dq_replay_meta* meta = v.meta;
+  const int64_t add_count = meta->add_count;
+  const int64_t pos0 = meta->tape_pos;
+  const int64_t len = meta->tape_len;
+  const double total = v.tree[0];
+  bool fail = meta->status != 0;
+  if (!fail && total == 0.0) {
+    if (t == 0) latch(meta, DQ_ST_EMPTY_TREE, 0, 0.0);
+    fail = true;
+  }
+  if (!fail && pos0 + 2 * (int64_t)B > len) {
+    if (t == 0) latch(meta, DQ_ST_TAPE_EXHAUSTED, 0, 0.0);
+    fail = true;
+  }
+  if (fail) {
+    if (t == 0) meta->reserved[0] = pos0;
+    for (int i = t; i < B; i += T) out[i] = 0;
+    return;
+  }
+  // subtree node j of the group: level offset l (0..4), position p within it
+  const int l = 31 - __clz(j + 1), p = j + 1 - (1 << l);
+  const double step = 1.0 / (double)B;        // np.linspace(0, 1, B + 1)
+  for (int i0 = 0; i0 < B; i0 += T / 32) {
+    const int i = i0 + g;
+    const bool mine = i < B;
+    double q = 0.0;
+    if (mine) {
+      const double u = res53(v.tape[pos0 + 2 * i], v.tape[pos0 + 2 * i + 1]);
+      const double lo = __dmul_rn((double)i, step);
+      const double hi = (i + 1 == B) ? 1.0 : __dmul_rn((double)(i + 1), step);
+      q = __dmul_rn(__dadd_rn(lo, __dmul_rn(__dsub_rn(hi, lo), u)), total);   // uniform * total
+    }
+    int64_t node = 0;                          // index at level d
+    for (int d = 0; d < v.depth; d += 5) {
+      const int lv = d + l + 1;                // level of the left child this lane fetches
+      double left = 0.0;
+      if (mine && j < 31 && lv <= v.depth)
+        left = v.tree[((int64_t)1 << lv) - 1 + 2 * ((node << l) + p)];
+      int64_t pc = 0;                          // path position within the subtree level
+#pragma unroll
+      for (int s = 0; s < 5; ++s) {
+        if (d + s >= v.depth) break;
+        const double lf = __shfl(left, (int)((1 << s) - 1 + pc), 32);
+        if (q < lf) {
+          pc = 2 * pc;
+        } else {
+          pc = 2 * pc + 1;
+          q = __dsub_rn(q, lf);
+        }
+      }
+      const int levels = v.depth - d < 5 ? v.depth - d : 5;
+      node = (node << levels) + pc;
+    }
+    if (mine && j == 0) {
+      s_idx[i] = node;
+      s_ok[i] = is_valid(v, node, add_count);
+    }
+  }
+  __syncthreads();
+  if (t == 0) {
+    int64_t pos = pos0 + 2 * (int64_t)B;
+    int budget = v.max_attempts;
+    for (int i = 0; i < B; ++i) {
+      if (s_ok[i]) continue;
+      if (budget == 0) {
+        latch(meta, DQ_ST_MAX_ATTEMPTS, i, 0.0);
+        break;
+      }
+      int64_t cand = s_idx[i];
+      bool tape_dry = false;
+      while (budget > 0) {
+        if (pos + 2 > len) {
+          tape_dry = true;
+          break;
+        }
+        const double u = res53(v.tape[pos], v.tape[pos + 1]);
+        pos += 2;
+        cand = descend(v.tree, v.depth, __dmul_rn(u, total));
+        --budget;
+        if (is_valid(v, cand, add_count)) break;
+      }
+      s_idx[i] = cand;
+      if (tape_dry) {
+        latch(meta, DQ_ST_TAPE_EXHAUSTED, i, 0.0);
+        break;
+      }
+    }
+    meta->reserved[0] = pos0;   // entry cursor, for dq_replay_rewind_last_sample
+    meta->tape_pos = pos;
+  }
+  __syncthreads();
+  for (int i = t; i < B; i += T) out[i] = (int32_t)s_idx[i];
+}
+
 // A replay operation recorded for a grouped launch instead of launched (the
 // opaque dq_rider of the C ABI): the sum-tree update, an index sample or the
 // NHWC gather, run by RiderOp (nature_cnn.hip) as extra blocks of a launch.
@@ -522,7 +761,7 @@ struct RiderDesc {
 };
 static_assert(sizeof(RiderDesc) <= sizeof(dq_rider), "dq_rider too small");
 
-constexpr int kRiderLds = kSumtreeSetLds > kPerSampleLds ? kSumtreeSetLds : kPerSampleLds;
+constexpr int kRiderLds = kSumtreeParLds > kPerSampleLds ? kSumtreeParLds : kPerSampleLds;
 
 // Runs rider r as block blk of a launch with T >= 256 threads per block.
 template <int T>
@@ -531,10 +770,10 @@ __device__ __forceinline__ void run_rider(const RiderDesc& r, int blk, void* lds
   const int t = threadIdx.x;
   switch (r.kind) {
     case kRiderSet:
-      if (t < kWave) sumtree_set_body(r.v, r.s, lds);
+      sumtree_set_par<T>(r.v, r.s, lds);
       return;
     case kRiderPerSample:
-      if (t < kWave) per_sample_body(r.v, r.batch, r.out, lds);
+      per_sample_par<T>(r.v, r.batch, r.out, lds);
       return;
     case kRiderUniformSample:
       if (t < kWave) uniform_sample_body(r.v, r.batch, r.out);

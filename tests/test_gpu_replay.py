@@ -254,3 +254,39 @@ def test_device_fast_path_rng_accounting():
     assert seen[-1].cpu().tolist() == exp, step
   m.sync_rng()
   assert m._rng.stream.getstate() == o.py_rng.getstate()
+
+
+@pytest.mark.parametrize('n', [37, 150])
+def test_device_set_priority_matches_host_path_and_stops_at_first_negative(n):
+  """Device-tensor set_priority (the learner's path: block-parallel kernel, chunks
+  of 64 updates, duplicates) leaves the same float64 tree as the host-checked path,
+  and at the first negative value applies exactly the updates before it."""
+  _, prb = _buffers()
+  C = 5000
+  rs = np.random.RandomState(n)
+  idx = rs.randint(0, 60, n).astype(np.int32)          # heavy duplication
+  idx[::7] = rs.randint(0, C, len(idx[::7]))
+  val = rs.uniform(0.0, 3.0, n).astype(np.float32)
+  for bad in (None, n // 2):
+    v = val.copy()
+    if bad is not None:
+      v[bad] = -1.0
+    trees = []
+    for device in (False, True):
+      p = prb.OutOfGraphPrioritizedReplayBuffer((4,), 1, C, 2)
+      p.set_priority(np.arange(C, dtype=np.int32), np.full(C, 0.5, np.float32))
+      if device:
+        p.set_priority(torch.from_numpy(idx).cuda(), torch.from_numpy(v).cuda())
+        if bad is None:
+          p.sync_rng()
+        else:
+          with pytest.raises(ValueError, match='nonnegative'):
+            p.sync_rng()
+      elif bad is None:
+        p.set_priority(idx, v)
+      else:
+        with pytest.raises(ValueError, match='nonnegative'):
+          p.set_priority(idx, v)
+      trees.append((np.concatenate(p.sum_tree.nodes), p.sum_tree.max_recorded_priority))
+    np.testing.assert_array_equal(trees[0][0], trees[1][0])
+    assert trees[0][1] == trees[1][1]
