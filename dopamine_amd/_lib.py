@@ -61,6 +61,11 @@ class CnnActs(ctypes.Structure):
   _fields_ = [(n, ctypes.c_void_p) for n in ('a1', 'a2', 'a3', 'h', 'out')]
 
 
+class CnnNet(ctypes.Structure):
+  _fields_ = [('p', ctypes.c_void_p), ('x', ctypes.c_void_p), ('a', ctypes.c_void_p),
+              ('ws', ctypes.c_void_p)]
+
+
 class Rider(ctypes.Structure):
   """dq_rider: a recorded replay operation (opaque)."""
   _fields_ = [('words', ctypes.c_int64 * 40)]
@@ -113,7 +118,11 @@ SIGNATURES = {
                                _I32, _P],
     'dq_cnn_backward_riders': [ctypes.POINTER(CnnParams), ctypes.POINTER(CnnParams), _I32, _P,
                                ctypes.POINTER(CnnActs), _P, ctypes.POINTER(CnnActs), _P,
-                               ctypes.POINTER(Rider), _I32, ctypes.POINTER(AdamArgs), _P],
+                               ctypes.POINTER(Rider), _I32, ctypes.POINTER(AdamArgs),
+                               ctypes.POINTER(CnnNet), _P],
+    'dq_cnn_forward_head': [ctypes.POINTER(CnnParams), _I32, _P, ctypes.POINTER(CnnActs), _P, _P],
+    'dq_cnn_forward_with_tail': [ctypes.POINTER(CnnParams), _P, ctypes.POINTER(CnnActs), _P,
+                                 ctypes.POINTER(CnnParams), ctypes.POINTER(CnnActs), _P, _I32, _P],
     'dq_cnn_backward_layer': [ctypes.POINTER(CnnParams), ctypes.POINTER(CnnParams), _I32, _P,
                               ctypes.POINTER(CnnActs), _P, ctypes.POINTER(CnnActs), _P, _I32, _I32,
                               _P],

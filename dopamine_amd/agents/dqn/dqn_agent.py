@@ -136,6 +136,7 @@ class DQNAgent(object):
     self._has_prefetch = False
     self._prefetch_add_count = -1
     self._online_ready = None
+    self._head = None              # (target net, input) whose forward head rides in the backward
     self._sess = sess
 
     state_shape = (1,) + self.observation_shape + (stack_size,)
@@ -261,15 +262,18 @@ class DQNAgent(object):
     return {'q': out}
 
   def _rides(self):
-    """ride_replay: single-replica HIP-CNN steps run on ONE stream -- the online and
-    target forwards paired at the start, and the next batch's priority write-back
-    -> sample -> gather recorded as riders of the backward's first grouped launches
-    (dq_cnn_backward_riders) instead of a second stream: the graph then has no
-    cross-queue fork/join edges, which cost ~28 us of a ~190 us step on MI355X."""
+    """ride_replay: single-replica HIP-CNN steps run on ONE stream.  The next
+    batch's priority write-back -> sample -> gather are recorded as riders of the
+    backward's first grouped launches (dq_cnn_backward_riders), the target net's
+    forward head on that batch rides in its last four, and the step after finishes
+    the target forward in the online forward's last two launches
+    (dq_cnn_forward_with_tail).  No second stream: the graph has no cross-queue
+    fork/join edges (they cost ~28 us of a ~190 us step on MI355X), and the
+    target forward adds no launches of its own."""
     return self.ride_replay and self._hip is not None and self._pg is None
 
   def _pairs(self):
-    return (self.pair_forward or self._rides()) and self._hip is not None
+    return self.pair_forward and self._hip is not None and not self._rides()
 
   def _forward_pair(self, c):
     """pair_forward: the online net on s and the target net on s' of slot c in ONE
@@ -288,6 +292,12 @@ class DQNAgent(object):
     t = mem.sample_device(self._batch_size, layout=self._replay._layout, out=self._pbuf[i],
                           reserve=False)
     self._pbuf[i] = t
+    if self._rides():               # the target head now (or riding in the backward), tail in the step
+      if mem._riders is not None:
+        self._head = (self._hip['target'][i], t['next_state'])
+      else:
+        self._hip['target'][i].forward_head(t['next_state'])
+      return
     if self._pairs():               # the target forward runs with the online one (_forward_pair)
       return
     tg = self._target_forward(t, i)
@@ -303,15 +313,22 @@ class DQNAgent(object):
     pipe = self.pipeline if pipe is None else pipe
     if not pipe:
       self._prefetch(c)
-    if self._pairs():
+    if self._rides():
+      from dopamine_amd.cnn import forward_with_tail
+      on, tg = forward_with_tail(self._hip['online'], self._pbuf[c]['state'], self._hip['target'][c])
+      self._online_ready = on
+      self._ptgt[c] = self._target_dict(tg)
+    elif self._pairs():
       self._forward_pair(c)
     y, g = self._online_loss(self._pbuf[c], self._ptgt[c])
     if pipe and self._rides():
+      self._head = None
       with self._replay.memory.recording() as riders:
         self._post_loss(self._pbuf[c])
         self._prefetch(1 - c)
       adam = self._opt if self._fused_opt() else None
-      self._hip['online'].backward(g, riders=riders, adam=adam, slot=k)
+      self._hip['online'].backward(g, riders=riders, adam=adam, slot=k, head=self._head)
+      self._head = None
     elif pipe:
       main = torch.cuda.current_stream(self._device)
       ev = torch.cuda.Event()
@@ -505,7 +522,9 @@ class DQNAgent(object):
 
   def _sync_target(self):
     ops.sync_copy(self.target_convnet.fp.flat, self.online_convnet.fp.flat)
-    if self.pipeline and self._has_prefetch and not self._pairs():   # prefetched target outputs are stale
+    if self.pipeline and self._has_prefetch and self._rides():   # the prefetched head is stale
+      self._hip['target'][self._slot].forward_head(self._pbuf[self._slot]['next_state'])
+    elif self.pipeline and self._has_prefetch and not self._pairs():   # prefetched target outputs are stale
       tg = self._target_forward(self._pbuf[self._slot], self._slot)
       for k, v in tg.items():
         if v.data_ptr() != self._ptgt[self._slot][k].data_ptr():

@@ -79,19 +79,37 @@ class HipNatureCNN(object):
                'dq_cnn_forward')
     return self.acts['out']
 
+  def forward_head(self, x):
+    """The head of forward(x): conv1..conv3 and fc1's split-K partial sums (into
+    self.ws); ``forward_with_tail`` finishes it.  Bitwise the same as forward()."""
+    x = self._nhwc(x)
+    self._x = x
+    _lib.check(_lib.lib.dq_cnn_forward_head(ctypes.byref(self._p), self.B, x.data_ptr(),
+                                            ctypes.byref(self._a), self.ws.data_ptr(),
+                                            self._stream(x)), 'dq_cnn_forward_head')
+
+  def cnn_net(self, x):
+    """dq_cnn_net of this network on input x (for a head run elsewhere)."""
+    x = self._nhwc(x)
+    self._x = x
+    return _lib.CnnNet(p=ctypes.cast(ctypes.pointer(self._p), ctypes.c_void_p), x=x.data_ptr(),
+                       a=ctypes.cast(ctypes.pointer(self._a), ctypes.c_void_p), ws=self.ws.data_ptr())
+
   def _adam_args(self, adam, slot):
     assert adam.params.data_ptr() == self.net.fp.flat.data_ptr(), 'adam must own net.fp.flat'
     return _lib.AdamArgs(var=adam.params.data_ptr(), m=adam.m.data_ptr(), v=adam.v.data_ptr(),
                          state=adam.state.data_ptr(), slot=int(slot), lr=adam.lr,
                          beta1=adam.b1, beta2=adam.b2, epsilon=adam.eps)
 
-  def backward(self, dout, parallel=False, adam=None, slot=0, groups=None, riders=None):
+  def backward(self, dout, parallel=False, adam=None, slot=0, groups=None, riders=None, head=None):
     """dout: (B, n_out).  Writes all parameter gradients into net.fp.grad.
 
     riders: replay operations recorded with ``ReplayBuffer.recording()`` (the
     next batch's priority write-back, sample and gather); rider i runs as extra
     blocks of grouped launch i (dq_cnn_backward_riders), in order, on this
-    stream.  Combines with ``adam``.
+    stream.  Combines with ``adam``.  head: (net, x) -- that network's forward head
+    on x runs in launches 4..7 (with riders; e.g. the target net on the batch the
+    riders gather); its forward_with_tail then finishes it.
 
     groups=(first, last): only launches [first, last) of the 7 grouped launches
     (a data-parallel learner all-reduces fc1/fc2's gradients after launch 3).
@@ -109,13 +127,18 @@ class HipNatureCNN(object):
     with the other stream's.  Kept for experimentation; off by default."""
     dout = dout.reshape(self.B, self.n_out)
     assert dout.is_contiguous() and self._x is not None
-    if riders:
+    if riders or head is not None:
       args = None if adam is None else ctypes.byref(self._adam_args(adam, slot))
-      arr = (_lib.Rider * len(riders))(*riders)
+      riders = riders or []
+      arr = (_lib.Rider * max(1, len(riders)))(*riders)
+      hn = None
+      if head is not None:
+        assert head[0] is not self
+        hn = ctypes.byref(head[0].cnn_net(head[1]))
       _lib.check(_lib.lib.dq_cnn_backward_riders(
           ctypes.byref(self._p), ctypes.byref(self._g), self.B, self._x.data_ptr(),
           ctypes.byref(self._a), dout.data_ptr(), ctypes.byref(self._d), self.ws.data_ptr(),
-          arr, len(riders), args, self._stream(dout)), 'dq_cnn_backward_riders')
+          arr, len(riders), args, hn, self._stream(dout)), 'dq_cnn_backward_riders')
       return self.net.fp.grad
     if groups is not None:          # a sub-range of the 7 grouped launches
       _lib.check(_lib.lib.dq_cnn_backward_groups(
@@ -174,4 +197,17 @@ def forward_pair(a, xa, b, xb):
       ctypes.byref(a._p), xa.data_ptr(), ctypes.byref(a._a), a.ws.data_ptr(),
       ctypes.byref(b._p), xb.data_ptr(), ctypes.byref(b._a), b.ws.data_ptr(), a.B,
       a._stream(xa)), 'dq_cnn_forward_pair')
+  return a.acts['out'], b.acts['out']
+
+
+def forward_with_tail(a, xa, b):
+  """``a.forward(xa)`` with ``b``'s tail (after ``b.forward_head`` or a backward
+  ``head=``) in its last two launches.  Returns the two output buffers."""
+  assert a.B == b.B and a is not b
+  xa = a._nhwc(xa)
+  a._x = xa
+  _lib.check(_lib.lib.dq_cnn_forward_with_tail(
+      ctypes.byref(a._p), xa.data_ptr(), ctypes.byref(a._a), a.ws.data_ptr(),
+      ctypes.byref(b._p), ctypes.byref(b._a), b.ws.data_ptr(), a.B, a._stream(xa)),
+      'dq_cnn_forward_with_tail')
   return a.acts['out'], b.acts['out']

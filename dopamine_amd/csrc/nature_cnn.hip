@@ -755,14 +755,24 @@ constexpr int max_lds() {
   return m;
 }
 
+// An op with fewer threads than the launch's block leaves its spare waves idle:
+// they exit at once, and the op's barriers then wait for its own waves only
+// (s_barrier counts the waves of the workgroup that have not ended).
 template <class Op>
 __device__ __forceinline__ bool dispatch(const Op& op, int nb, int& blk, float* smem) {
   if (blk < nb) {
-    op.run(blk, smem);
+    if (Op::kT >= (int)blockDim.x || (int)threadIdx.x < Op::kT) op.run(blk, smem);
     return true;
   }
   blk -= nb;
   return false;
+}
+
+template <class... Ops>
+constexpr int max_threads() {
+  int m = 64;
+  ((m = Ops::kT > m ? Ops::kT : m), ...);
+  return m;
 }
 
 template <class... Ops>
@@ -830,8 +840,7 @@ GemmOp<WM, WN, WK, AL, BL, EP> gemm_op(AL a, BL b, EP e, int M, int N, int K, in
 
 template <class Op0, class... Ops>
 void group(Ctx& c, Op0 op0, Ops... ops) {
-  constexpr int T = Op0::kT;
-  static_assert(((Ops::kT == T) && ...), "grouped ops share one block size");
+  constexpr int T = max_threads<Op0, Ops...>();   // block = the largest op's
   if (c.dry) return;
   GroupArgs<Op0, Ops...> g;
   int i = 0, total = 0;
@@ -871,55 +880,85 @@ void forward(Ctx& c, const dq_cnn_params* p, int B, const float* x, dq_cnn_acts*
                  EpiBiasAct{a->out, p->fc2_b, p->n_out, false}, B, p->n_out, kHidden);
 }
 
-// The online and target networks' forwards together: the same tiles and split
-// order as forward() (bitwise identical outputs), one grouped launch per layer
+// The forward's grouped ops for one network (the same tiles and split order as
+// forward(): bitwise identical outputs).  head = conv1, conv2, conv3, fc1 split-K
+// slabs (into ws); tail = the slab sum (+ bias, ReLU) and fc2.
+struct FwdOps {
+  const dq_cnn_params* p;
+  const float* x;
+  dq_cnn_acts* a;
+  float* ws;
+  int B;
+  static int fc1_chunk() { return split_chunk(kFlat, kSplitFc1, 32 * 16); }
+  static int fc1_slabs() { return (kFlat + fc1_chunk() - 1) / fc1_chunk(); }
+  static size_t ws_floats(int B) { return (size_t)fc1_slabs() * B * kHidden; }
+  auto conv1() const {
+    return gemm_op<1, 1, 8>(Im2col<Conv1>{x}, RowK{p->conv1_w, Conv1::K},
+                            EpiBiasAct{a->a1, p->conv1_b, 32, true}, B * 441, 32, Conv1::K, Conv1::K);
+  }
+  auto conv2() const {
+    return gemm_op<1, 1, 16>(Im2col<Conv2>{a->a1}, RowK{p->conv2_w, Conv2::K},
+                             EpiBiasAct{a->a2, p->conv2_b, 64, true}, B * 121, 64, Conv2::K, Conv2::K);
+  }
+  auto conv3() const {
+    return gemm_op<1, 1, 9>(Im2col<Conv3>{a->a2}, RowK{p->conv3_w, Conv3::K},
+                            EpiBiasAct{a->a3, p->conv3_b, 64, true}, B * 121, 64, Conv3::K, Conv3::K);
+  }
+  auto fc1() const {
+    return gemm_op<1, 1, 16>(RowK{a->a3, kFlat}, RowK{p->fc1_w, kFlat}, EpiPartial{ws, B, kHidden},
+                             B, kHidden, kFlat, fc1_chunk());
+  }
+  auto fc1_sum() const {
+    return ReduceOp<EpiBiasAct, 256>{ws, fc1_slabs(), B, kHidden,
+                                     EpiBiasAct{a->h, p->fc1_b, kHidden, true}};
+  }
+  auto fc2() const {
+    return gemm_op<1, 1, 16>(RowK{a->h, kHidden}, RowK{p->fc2_w, kHidden},
+                             EpiBiasAct{a->out, p->fc2_b, p->n_out, false}, B, p->n_out, kHidden,
+                             kHidden);
+  }
+};
+
+// The online and target networks' forwards together: one grouped launch per layer
 // holding both nets' ops -- 6 launches instead of 12.
 void forward_pair(Ctx& c0, Ctx& c1, const dq_cnn_params* p0, const float* x0, dq_cnn_acts* a0,
                   const dq_cnn_params* p1, const float* x1, dq_cnn_acts* a1, int B) {
-  constexpr int BK16 = 32 * 16;
-  const int ch = split_chunk(kFlat, kSplitFc1, BK16), nz = (kFlat + ch - 1) / ch;
-  const size_t need = (size_t)nz * B * kHidden;
+  const size_t need = FwdOps::ws_floats(B);
   c0.need = need > c0.need ? need : c0.need;
   c1.need = need > c1.need ? need : c1.need;
   if (c0.dry) return;
-  const dq_cnn_params* p[2] = {p0, p1};
-  const float* x[2] = {x0, x1};
-  dq_cnn_acts* a[2] = {a0, a1};
-  float* ws[2] = {c0.ws, c1.ws};
-  auto conv1 = [&](int i) {
-    return gemm_op<1, 1, 8>(Im2col<Conv1>{x[i]}, RowK{p[i]->conv1_w, Conv1::K},
-                            EpiBiasAct{a[i]->a1, p[i]->conv1_b, 32, true}, B * 441, 32, Conv1::K,
-                            Conv1::K);
-  };
-  auto conv2 = [&](int i) {
-    return gemm_op<1, 1, 16>(Im2col<Conv2>{a[i]->a1}, RowK{p[i]->conv2_w, Conv2::K},
-                             EpiBiasAct{a[i]->a2, p[i]->conv2_b, 64, true}, B * 121, 64, Conv2::K,
-                             Conv2::K);
-  };
-  auto conv3 = [&](int i) {
-    return gemm_op<1, 1, 9>(Im2col<Conv3>{a[i]->a2}, RowK{p[i]->conv3_w, Conv3::K},
-                            EpiBiasAct{a[i]->a3, p[i]->conv3_b, 64, true}, B * 121, 64, Conv3::K,
-                            Conv3::K);
-  };
-  auto fc1 = [&](int i) {
-    return gemm_op<1, 1, 16>(RowK{a[i]->a3, kFlat}, RowK{p[i]->fc1_w, kFlat},
-                             EpiPartial{ws[i], B, kHidden}, B, kHidden, kFlat, ch);
-  };
-  auto fc1_sum = [&](int i) {
-    return ReduceOp<EpiBiasAct, 256>{ws[i], nz, B, kHidden,
-                                     EpiBiasAct{a[i]->h, p[i]->fc1_b, kHidden, true}};
-  };
-  auto fc2 = [&](int i) {
-    return gemm_op<1, 1, 16>(RowK{a[i]->h, kHidden}, RowK{p[i]->fc2_w, kHidden},
-                             EpiBiasAct{a[i]->out, p[i]->fc2_b, p[i]->n_out, false}, B,
-                             p[i]->n_out, kHidden, kHidden);
-  };
-  group(c0, conv1(0), conv1(1));
-  group(c0, conv2(0), conv2(1));
-  group(c0, conv3(0), conv3(1));
-  group(c0, fc1(0), fc1(1));
-  group(c0, fc1_sum(0), fc1_sum(1));
-  group(c0, fc2(0), fc2(1));
+  const FwdOps f0{p0, x0, a0, c0.ws, B}, f1{p1, x1, a1, c1.ws, B};
+  group(c0, f0.conv1(), f1.conv1());
+  group(c0, f0.conv2(), f1.conv2());
+  group(c0, f0.conv3(), f1.conv3());
+  group(c0, f0.fc1(), f1.fc1());
+  group(c0, f0.fc1_sum(), f1.fc1_sum());
+  group(c0, f0.fc2(), f1.fc2());
+}
+
+// Net 0's whole forward with net 1's tail (whose head ran earlier, e.g. as riders of
+// the previous backward) in net 0's last two launches.
+void forward_with_tail(Ctx& c0, Ctx& c1, const FwdOps& f0, const FwdOps& f1) {
+  const size_t need = FwdOps::ws_floats(f0.B);
+  c0.need = need > c0.need ? need : c0.need;
+  c1.need = need > c1.need ? need : c1.need;
+  if (c0.dry) return;
+  group(c0, f0.conv1());
+  group(c0, f0.conv2());
+  group(c0, f0.conv3());
+  group(c0, f0.fc1());
+  group(c0, f0.fc1_sum(), f1.fc1_sum());
+  group(c0, f0.fc2(), f1.fc2());
+}
+
+void forward_head(Ctx& c, const FwdOps& f) {
+  const size_t need = FwdOps::ws_floats(f.B);
+  c.need = need > c.need ? need : c.need;
+  if (c.dry) return;
+  group(c, f.conv1());
+  group(c, f.conv2());
+  group(c, f.conv3());
+  group(c, f.fc1());
 }
 
 // Backward of one layer: part 1 = weight/bias gradient, part 0 = input gradient.
@@ -997,7 +1036,8 @@ template <bool kAdam>
 void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int B,
                       const float* x, const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d,
                       const AdamHost& opt, int first = 0, int last = 7,
-                      const RiderDesc* riders = nullptr, int n_riders = 0) {
+                      const RiderDesc* riders = nullptr, int n_riders = 0,
+                      const FwdOps* head = nullptr) {
   const int NO = p->n_out;
   using GE = GradEpi<kAdam>;
   using W16 = Tile<1, 1, 16>;
@@ -1062,6 +1102,13 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
       if (in(0)) group_r(c, rd(0), dX_fc2);
       if (in(1)) group_r(c, rd(1), dW_fc2, dX_fc1);
       if (in(2)) group_r(c, rd(2), dW_fc1, dX_c3, part(p->fc2_w, p->fc2_b + NO));
+      if (head) {
+        if (in(3)) group_r(c, rd(3), dW_c3, dcol, part(f0, f1), head->conv1());
+        if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, da1, part(f1, f2), head->conv2());
+        if (in(5)) group_r(c, rd(5), sum_c2, dW_c1, part(f2, f3), head->conv3());
+        if (in(6)) group_r(c, rd(6), sum_c1, part(p->conv2_w, p->fc1_w), head->fc1());
+        return;
+      }
       if (in(3)) group_r(c, rd(3), dW_c3, dcol, part(f0, f1));
       if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, da1, part(f1, f2));
       if (in(5)) group_r(c, rd(5), sum_c2, dW_c1, part(f2, f3));
@@ -1072,6 +1119,13 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
   if (in(0)) group_r(c, rd(0), dX_fc2);
   if (in(1)) group_r(c, rd(1), dW_fc2, dX_fc1);
   if (in(2)) group_r(c, rd(2), dW_fc1, dX_c3);
+  if (head) {
+    if (in(3)) group_r(c, rd(3), dW_c3, dcol, head->conv1());
+    if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, da1, head->conv2());
+    if (in(5)) group_r(c, rd(5), sum_c2, dW_c1, head->conv3());
+    if (in(6)) group_r(c, rd(6), sum_c1, head->fc1());
+    return;
+  }
   if (in(3)) group_r(c, rd(3), dW_c3, dcol);
   if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, da1);
   if (in(5)) group_r(c, rd(5), sum_c2, dW_c1);
@@ -1129,6 +1183,29 @@ int dq_cnn_forward_pair(const dq_cnn_params* p0, const float* x0, dq_cnn_acts* a
   return DQ_OK;
 }
 
+int dq_cnn_forward_head(const dq_cnn_params* p, int32_t batch, const float* x, dq_cnn_acts* a,
+                        float* ws, void* stream) {
+  DQ_CHECK_ARG(p && a && x && ws && batch >= 1, "null argument");
+  DQ_CHECK_ARG(p->in_channels == 4 && p->n_out >= 1, "the Nature CNN takes 84x84x4 NHWC input");
+  Ctx c{(hipStream_t)stream, ws, false, 0};
+  forward_head(c, FwdOps{p, x, a, ws, batch});
+  DQ_CHECK_LAUNCH("dq_cnn_forward_head");
+  return DQ_OK;
+}
+
+int dq_cnn_forward_with_tail(const dq_cnn_params* p0, const float* x0, dq_cnn_acts* a0, float* ws0,
+                             const dq_cnn_params* p1, dq_cnn_acts* a1, float* ws1, int32_t batch,
+                             void* stream) {
+  DQ_CHECK_ARG(p0 && a0 && x0 && ws0 && p1 && a1 && ws1 && batch >= 1, "null argument");
+  DQ_CHECK_ARG(p0->in_channels == 4 && p1->in_channels == 4 && p0->n_out >= 1 && p1->n_out >= 1,
+               "the Nature CNN takes 84x84x4 NHWC input");
+  DQ_CHECK_ARG(ws0 != ws1, "the two networks need separate workspaces");
+  Ctx c0{(hipStream_t)stream, ws0, false, 0}, c1{(hipStream_t)stream, ws1, false, 0};
+  forward_with_tail(c0, c1, FwdOps{p0, x0, a0, ws0, batch}, FwdOps{p1, nullptr, a1, ws1, batch});
+  DQ_CHECK_LAUNCH("dq_cnn_forward_with_tail");
+  return DQ_OK;
+}
+
 int dq_cnn_backward(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch, const float* x,
                     const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d, float* ws,
                     void* stream) {
@@ -1168,7 +1245,7 @@ int dq_cnn_backward_groups(const dq_cnn_params* p, const dq_cnn_params* g, int32
 int dq_cnn_backward_riders(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch,
                            const float* x, const dq_cnn_acts* a, const float* dout,
                            dq_cnn_acts* d, float* ws, const dq_rider* riders, int32_t n_riders,
-                           const dq_adam_args* opt, void* stream) {
+                           const dq_adam_args* opt, const dq_cnn_net* head, void* stream) {
   DQ_CHECK_ARG(p && g && a && d && x && dout && ws && batch >= 1, "null argument");
   DQ_CHECK_ARG(p->in_channels == 4 && p->n_out >= 1, "the Nature CNN takes 84x84x4 NHWC input");
   DQ_CHECK_ARG(0 <= n_riders && n_riders <= 7 && (riders || n_riders == 0),
@@ -1178,13 +1255,22 @@ int dq_cnn_backward_riders(const dq_cnn_params* p, const dq_cnn_params* g, int32
     memcpy(&r[i], &riders[i], sizeof(RiderDesc));
     DQ_CHECK_ARG(r[i].kind >= kRiderNone && r[i].kind <= kRiderGatherNhwc, "corrupt rider");
   }
+  FwdOps hf{};
+  if (head) {
+    DQ_CHECK_ARG(head->p && head->x && head->a && head->ws, "null head network field");
+    DQ_CHECK_ARG(head->p->in_channels == 4, "the Nature CNN takes 84x84x4 NHWC input");
+    DQ_CHECK_ARG(head->ws != ws, "the head network needs its own workspace");
+    hf = FwdOps{head->p, head->x, head->a, head->ws, batch};
+  }
   Ctx c{(hipStream_t)stream, ws, false, 0};
   if (opt) {
     const int rc = check_adam(p, g, opt);
     if (rc != DQ_OK) return rc;
-    backward_grouped<true>(c, p, g, batch, x, a, dout, d, AdamHost{opt}, 0, 7, r, n_riders);
+    backward_grouped<true>(c, p, g, batch, x, a, dout, d, AdamHost{opt}, 0, 7, r, n_riders,
+                           head ? &hf : nullptr);
   } else {
-    backward_grouped<false>(c, p, g, batch, x, a, dout, d, AdamHost{nullptr}, 0, 7, r, n_riders);
+    backward_grouped<false>(c, p, g, batch, x, a, dout, d, AdamHost{nullptr}, 0, 7, r, n_riders,
+                            head ? &hf : nullptr);
   }
   DQ_CHECK_LAUNCH("dq_cnn_backward_riders");
   return DQ_OK;

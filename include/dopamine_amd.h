@@ -266,14 +266,32 @@ int dq_cnn_backward_adam(const dq_cnn_params* p, const dq_cnn_params* g, int32_t
 int dq_cnn_backward_groups(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch,
                            const float* x, const dq_cnn_acts* a, const float* dout,
                            dq_cnn_acts* d, float* ws, int32_t first, int32_t last, void* stream);
+/* A network's forward split in two, so the head can run where it is cheapest:
+   head = conv1..conv3 and fc1's split-K partial sums (into ws), tail = their sum
+   (+ bias, ReLU) and fc2.  head followed by tail == dq_cnn_forward, bit for bit. */
+typedef struct dq_cnn_net {
+  const dq_cnn_params* p;
+  const float* x;
+  dq_cnn_acts* a;
+  float* ws;
+} dq_cnn_net;
+int dq_cnn_forward_head(const dq_cnn_params* p, int32_t batch, const float* x, dq_cnn_acts* a,
+                        float* ws, void* stream);
+/* net 0's whole forward, with net 1's tail (its head already run into a1 / ws1) in net 0's
+   last two launches. */
+int dq_cnn_forward_with_tail(const dq_cnn_params* p0, const float* x0, dq_cnn_acts* a0, float* ws0,
+                             const dq_cnn_params* p1, dq_cnn_acts* a1, float* ws1, int32_t batch,
+                             void* stream);
 /* dq_cnn_backward (opt NULL) or dq_cnn_backward_adam (opt set) with riders[i] (recorded by
    dq_replay_record_*) as extra blocks of grouped launch i, i < n_riders <= 7: a chain of
    riders runs in order, each after the launches before its own.  Riders must not touch
-   x, a, dout, d, g or ws.  CNN results are bitwise those of the rider-less call. */
+   x, a, dout, d, g or ws.  head (may be NULL): another network's forward head (e.g. the
+   target network on the next batch, which riders gathered) runs in launches 4..7.  CNN
+   results are bitwise those of the separate calls. */
 int dq_cnn_backward_riders(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch,
                            const float* x, const dq_cnn_acts* a, const float* dout,
                            dq_cnn_acts* d, float* ws, const dq_rider* riders, int32_t n_riders,
-                           const dq_adam_args* opt, void* stream);
+                           const dq_adam_args* opt, const dq_cnn_net* head, void* stream);
 /* one layer of the backward: layer 0..4 = fc2, fc1, conv3, conv2, conv1; part 1 = weight and
    bias gradient, part 0 = input gradient (not for conv1).  dW(L) depends only on dX(L-1),
    so the weight gradients may run on a second stream, each with its own ws. */

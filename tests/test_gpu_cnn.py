@@ -113,3 +113,33 @@ def test_forward_pair_equals_two_forwards(B):
   yo, yt = forward_pair(ho, x, ht, nx)
   torch.cuda.synchronize()
   assert torch.equal(yo, ref_o) and torch.equal(yt, ref_t)
+
+
+@pytest.mark.parametrize('B', [32, 5])
+def test_forward_head_and_tail_equal_forward(B):
+  """Head (eager, or riding in another net's backward) + tail (in the other net's
+  forward) == forward(), bit for bit; the backward's own gradients are unchanged
+  by the riding head."""
+  from dopamine_amd.agents.networks import RainbowNetwork
+  from dopamine_amd.cnn import HipNatureCNN, forward_with_tail
+  on, tg = RainbowNetwork(9, device='cuda', seed=1), RainbowNetwork(9, device='cuda', seed=2)
+  ho, ht = HipNatureCNN(on, B), HipNatureCNN(tg, B)
+  x, nx = torch.rand(B, 84, 84, 4, device='cuda'), torch.rand(B, 84, 84, 4, device='cuda')
+  ref_o, ref_t = ho.forward(x).clone(), ht.forward(nx).clone()
+  dout = torch.randn(B, ho.n_out, device='cuda')
+  ho.backward(dout)
+  ref_g = torch.cat([v.reshape(-1) for v in on.fp.grad_views])   # skips alignment pads
+  ht.acts['out'].zero_()
+  ht.forward_head(nx)
+  yo, yt = forward_with_tail(ho, x, ht)
+  torch.cuda.synchronize()
+  assert torch.equal(yo, ref_o) and torch.equal(yt, ref_t)
+  # the head riding in the online backward, then the tail in the next forward
+  ht.acts['out'].zero_()
+  on.fp.grad.zero_()
+  ho.backward(dout, head=(ht, nx))
+  torch.cuda.synchronize()
+  assert torch.equal(torch.cat([v.reshape(-1) for v in on.fp.grad_views]), ref_g)
+  yo, yt = forward_with_tail(ho, x, ht)
+  torch.cuda.synchronize()
+  assert torch.equal(yo, ref_o) and torch.equal(yt, ref_t)
