@@ -119,7 +119,7 @@ SIGNATURES = {
     'dq_cnn_backward_riders': [ctypes.POINTER(CnnParams), ctypes.POINTER(CnnParams), _I32, _P,
                                ctypes.POINTER(CnnActs), _P, ctypes.POINTER(CnnActs), _P,
                                ctypes.POINTER(Rider), _I32, ctypes.POINTER(AdamArgs),
-                               ctypes.POINTER(CnnNet), _P],
+                               ctypes.POINTER(CnnNet), _I32, _I32, _P],
     'dq_cnn_forward_head': [ctypes.POINTER(CnnParams), _I32, _P, ctypes.POINTER(CnnActs), _P, _P],
     'dq_cnn_forward_with_tail': [ctypes.POINTER(CnnParams), _P, ctypes.POINTER(CnnActs), _P,
                                  ctypes.POINTER(CnnParams), ctypes.POINTER(CnnActs), _P, _I32, _P],

@@ -137,6 +137,7 @@ class DQNAgent(object):
     self._prefetch_add_count = -1
     self._online_ready = None
     self._head = None              # (target net, input) whose forward head rides in the backward
+    self._tail_head = None         # ... in the N > 1 tail graph
     self._sess = sess
 
     state_shape = (1,) + self.observation_shape + (stack_size,)
@@ -262,7 +263,8 @@ class DQNAgent(object):
     return {'q': out}
 
   def _rides(self):
-    """ride_replay: single-replica HIP-CNN steps run on ONE stream.  The next
+    """ride_replay: HIP-CNN steps run on ONE stream (plus, with N > 1 replicas, the
+    all-reduce's comm stream).  The next
     batch's priority write-back -> sample -> gather are recorded as riders of the
     backward's first grouped launches (dq_cnn_backward_riders), the target net's
     forward head on that batch rides in its last four, and the step after finishes
@@ -270,7 +272,7 @@ class DQNAgent(object):
     (dq_cnn_forward_with_tail).  No second stream: the graph has no cross-queue
     fork/join edges (they cost ~28 us of a ~190 us step on MI355X), and the
     target forward adds no launches of its own."""
-    return self.ride_replay and self._hip is not None and self._pg is None
+    return self.ride_replay and self._hip is not None
 
   def _pairs(self):
     return self.pair_forward and self._hip is not None and not self._rides()
@@ -358,16 +360,36 @@ class DQNAgent(object):
     pipe = self.pipeline if pipe is None else pipe
     if not pipe:
       self._prefetch(c)
-    if self._pairs():
+    if self._rides():
+      from dopamine_amd.cnn import forward_with_tail
+      on, tg = forward_with_tail(self._hip['online'], self._pbuf[c]['state'], self._hip['target'][c])
+      self._online_ready = on
+      self._ptgt[c] = self._target_dict(tg)
+    elif self._pairs():
       self._forward_pair(c)
     y, g = self._online_loss(self._pbuf[c], self._ptgt[c])
-    self._hip['online'].backward(g, groups=(0, self._SPLIT))
+    if pipe and self._rides():      # priority write-back -> sample -> gather ride in launches 0-2
+      self._head = None
+      with self._replay.memory.recording() as riders:
+        self._post_loss(self._pbuf[c])
+        self._prefetch(1 - c)
+      assert len(riders) <= self._SPLIT
+      self._hip['online'].backward(g, groups=(0, self._SPLIT), riders=riders)
+      self._tail_head, self._head = self._head, None
+    else:
+      self._hip['online'].backward(g, groups=(0, self._SPLIT))
     self._dout = g
 
   def _grad_step_tail(self, c, k, pipe=None):
     pipe = self.pipeline if pipe is None else pipe
     g = self._dout
-    if pipe:
+    if self._rides():               # the target head on the gathered batch rides in launches 3-6
+      if not pipe:
+        self._post_loss(self._pbuf[c])
+      self._hip['online'].backward(g, groups=(self._SPLIT, 7),
+                                   head=self._tail_head if pipe else None)
+      self._tail_head = None
+    elif pipe:
       main = torch.cuda.current_stream(self._device)
       ev = torch.cuda.Event()
       ev.record(main)

@@ -135,10 +135,12 @@ class HipNatureCNN(object):
       if head is not None:
         assert head[0] is not self
         hn = ctypes.byref(head[0].cnn_net(head[1]))
+      first, last = (0, 7) if groups is None else groups
       _lib.check(_lib.lib.dq_cnn_backward_riders(
           ctypes.byref(self._p), ctypes.byref(self._g), self.B, self._x.data_ptr(),
           ctypes.byref(self._a), dout.data_ptr(), ctypes.byref(self._d), self.ws.data_ptr(),
-          arr, len(riders), args, hn, self._stream(dout)), 'dq_cnn_backward_riders')
+          arr, len(riders), args, hn, int(first), int(last), self._stream(dout)),
+          'dq_cnn_backward_riders')
       return self.net.fp.grad
     if groups is not None:          # a sub-range of the 7 grouped launches
       _lib.check(_lib.lib.dq_cnn_backward_groups(

@@ -75,6 +75,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, kOOB, 0x00020000);
 }
 __device__ __forceinline__ float4 bload4(const float* base, int off, bool ok) {   // off in floats
+#ifdef DQ_ABLATE_LOADS   // timing experiments only: operands without memory traffic
+  const float f = ok ? (float)off * 1e-9f : 0.0f;
+  return make_float4(f, f, f, f);
+#endif
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc(base), ok ? off * 4 : kOOB, 0, 0);
   return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
@@ -388,6 +392,9 @@ template <int WM, int WN, int WK, class AL, class BL, class EP>
 __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& E, int M, int N,
                                             int K, int kchunk, int bx, int by, int bz,
                                             float* smem) {
+#ifdef DQ_ABLATE_ALL      // timing experiments only: the launch floor of these grids
+  if (M > 0) return;
+#endif
   using TL = Tile<WM, WN, WK>;
   constexpr int T = TL::T, BM = TL::BM, BN = TL::BN, BKT = TL::BKT;
   constexpr int SA = BM + (AL::kFast ? 1 : 4), SB = BN + (BL::kFast ? 1 : 4);
@@ -512,11 +519,22 @@ __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& 
         if (h == 1 && k0 + BKT < kend) fetch(k0 + BKT);
         if (live) {
           float av[8], bv[8];
+#ifdef DQ_ABLATE_STAGE   // timing experiments only: operands straight from the fetched registers
+          for (int s = 0; s < 8; ++s) {
+            av[s] = (&pa4[s & 3].x)[s >> 2];
+            bv[s] = (&pb4[s & 3].x)[s >> 2];
+          }
+#else
           operands(Aw, AL::kFast, av);
           operands(Bw, BL::kFast, bv);
+#endif
+#ifdef DQ_ABLATE_MFMA    // timing experiments only: no matrix-core chain
+          for (int s = 0; s < 8; ++s) acc[s] += av[s] * bv[s];
+#else
 #pragma unroll
           for (int s = 0; s < 8; ++s)
             acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc, 0, 0, 0);
+#endif
         }
       }
     }
@@ -561,6 +579,16 @@ __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& 
     }
     return;
   }
+#ifdef DQ_ABLATE_REDUCE   // timing experiments only: wave 0's partial goes straight out
+  if (wk == 0) {
+    const int n = n0 + wn * 32 + (lane & 31);
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (m < M && n < N) E(m, n, acc[r], bz);
+    }
+  }
+  return;
+#endif
   // partials -> LDS [wk][tile][r][lane]
   {
     float* red = smem + (wk * WM * WN + wm + WM * wn) * 1024 + lane;
@@ -1245,11 +1273,14 @@ int dq_cnn_backward_groups(const dq_cnn_params* p, const dq_cnn_params* g, int32
 int dq_cnn_backward_riders(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch,
                            const float* x, const dq_cnn_acts* a, const float* dout,
                            dq_cnn_acts* d, float* ws, const dq_rider* riders, int32_t n_riders,
-                           const dq_adam_args* opt, const dq_cnn_net* head, void* stream) {
+                           const dq_adam_args* opt, const dq_cnn_net* head, int32_t first,
+                           int32_t last, void* stream) {
   DQ_CHECK_ARG(p && g && a && d && x && dout && ws && batch >= 1, "null argument");
   DQ_CHECK_ARG(p->in_channels == 4 && p->n_out >= 1, "the Nature CNN takes 84x84x4 NHWC input");
   DQ_CHECK_ARG(0 <= n_riders && n_riders <= 7 && (riders || n_riders == 0),
                "at most one rider per grouped launch (7)");
+  DQ_CHECK_ARG(0 <= first && first <= last && last <= 7, "groups must satisfy 0 <= first <= last <= 7");
+  DQ_CHECK_ARG(!opt || (first == 0 && last == 7), "the fused optimizer needs the whole backward");
   RiderDesc r[7];
   for (int i = 0; i < n_riders; ++i) {
     memcpy(&r[i], &riders[i], sizeof(RiderDesc));
@@ -1266,11 +1297,11 @@ int dq_cnn_backward_riders(const dq_cnn_params* p, const dq_cnn_params* g, int32
   if (opt) {
     const int rc = check_adam(p, g, opt);
     if (rc != DQ_OK) return rc;
-    backward_grouped<true>(c, p, g, batch, x, a, dout, d, AdamHost{opt}, 0, 7, r, n_riders,
+    backward_grouped<true>(c, p, g, batch, x, a, dout, d, AdamHost{opt}, first, last, r, n_riders,
                            head ? &hf : nullptr);
   } else {
-    backward_grouped<false>(c, p, g, batch, x, a, dout, d, AdamHost{nullptr}, 0, 7, r, n_riders,
-                            head ? &hf : nullptr);
+    backward_grouped<false>(c, p, g, batch, x, a, dout, d, AdamHost{nullptr}, first, last, r,
+                            n_riders, head ? &hf : nullptr);
   }
   DQ_CHECK_LAUNCH("dq_cnn_backward_riders");
   return DQ_OK;

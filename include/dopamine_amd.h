@@ -286,12 +286,15 @@ int dq_cnn_forward_with_tail(const dq_cnn_params* p0, const float* x0, dq_cnn_ac
    dq_replay_record_*) as extra blocks of grouped launch i, i < n_riders <= 7: a chain of
    riders runs in order, each after the launches before its own.  Riders must not touch
    x, a, dout, d, g or ws.  head (may be NULL): another network's forward head (e.g. the
-   target network on the next batch, which riders gathered) runs in launches 4..7.  CNN
-   results are bitwise those of the separate calls. */
+   target network on the next batch, which riders gathered) runs in launches 4..7.  Only
+   launches [first, last) are issued (as dq_cnn_backward_groups; riders and head ops of
+   other launches are skipped; opt needs [0, 7)).  CNN results are bitwise those of the
+   separate calls. */
 int dq_cnn_backward_riders(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch,
                            const float* x, const dq_cnn_acts* a, const float* dout,
                            dq_cnn_acts* d, float* ws, const dq_rider* riders, int32_t n_riders,
-                           const dq_adam_args* opt, const dq_cnn_net* head, void* stream);
+                           const dq_adam_args* opt, const dq_cnn_net* head, int32_t first,
+                           int32_t last, void* stream);
 /* one layer of the backward: layer 0..4 = fc2, fc1, conv3, conv2, conv1; part 1 = weight and
    bias gradient, part 0 = input gradient (not for conv1).  dW(L) depends only on dX(L-1),
    so the weight gradients may run on a second stream, each with its own ws. */

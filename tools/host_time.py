@@ -2,7 +2,7 @@
   step_total : K grad steps incl. final sync (what bench.py measures)
   step_host  : the same loop's host time before the final sync
   replay_only: K bare graph replays (alternating parity), no Python agent logic
-    python tools/host_time.py [K]"""
+    python tools/host_time.py [K] [eager]"""
 import os
 import sys
 import time
@@ -22,7 +22,8 @@ def main():
   agent = RainbowAgent(num_actions=9, update_horizon=3, gamma=0.99, replay_scheme='prioritized',
                        min_replay_history=20000, update_period=4, target_update_period=8000,
                        optimizer=AdamOptimizer(learning_rate=0.0000625, epsilon=0.00015),
-                       replay_capacity=1000000, batch_size=32, device=dev)
+                       replay_capacity=1000000, batch_size=32, device=dev,
+                       use_hip_graph=not (len(sys.argv) > 2 and sys.argv[2] == 'eager'))
   bench.fill_synthetic(agent._replay.memory, 9, seed=1)
   torch.cuda.synchronize()
 
@@ -33,6 +34,15 @@ def main():
   for _ in range(30):
     grad_step()
   torch.cuda.synchronize()
+  # host-only cost: the Python step loop with the GPU idle in between (sync each step)
+  t0 = time.perf_counter()
+  host = 0.0
+  for _ in range(200):
+    h0 = time.perf_counter()
+    grad_step()
+    host += time.perf_counter() - h0
+    torch.cuda.synchronize()
+  print('host_alone  %7.1f us  (submission per step, GPU drained between steps)' % (host / 200 * 1e6))
   t0 = time.perf_counter()
   for _ in range(K):
     grad_step()
@@ -42,6 +52,8 @@ def main():
   print('step_total  %7.1f us' % ((t2 - t0) / K * 1e6))
   print('step_host   %7.1f us' % ((t1 - t0) / K * 1e6))
   g = agent._graphs
+  if g is None:
+    return
   torch.cuda.synchronize()
   t0 = time.perf_counter()
   for i in range(K):
