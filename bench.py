@@ -69,16 +69,22 @@ def time_gather(agent, iters):
   from dopamine_amd import _lib
   mem = agent._replay.memory
   out = agent._replay._out
-  idx = out['sample_indices']
   B = agent._batch_size
   layout = agent._replay._layout
   stream = torch.cuda.current_stream()
+  # a fresh random index batch per launch: 400 x 1.8 MB of frames (> the 256 MB
+  # Infinity Cache), so every launch reads cold frames as in the learner step
+  C = mem._replay_capacity
+  gen = torch.Generator(device='cpu').manual_seed(11)
+  sets = torch.randint(mem._stack_size, C - mem._update_horizon - 1, (iters, B), generator=gen,
+                       dtype=torch.int32).to(torch.cuda.current_device())
+  idx = sets[0]
   for _ in range(10):
     mem._gather(idx, B, layout, out)
   g = torch.cuda.CUDAGraph()
   with torch.cuda.graph(g):
-    for _ in range(iters):
-      mem._gather(idx, B, layout, out)
+    for i in range(iters):
+      mem._gather(sets[i], B, layout, out)
   g.replay()
   torch.cuda.synchronize()
   e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -89,8 +95,8 @@ def time_gather(agent, iters):
   graph_us = e0.elapsed_time(e1) * 1e3 / iters
   # eager back-to-back launches on the same stream, for comparison
   e0.record(stream)
-  for _ in range(iters):
-    mem._gather(idx, B, layout, out)
+  for i in range(iters):
+    mem._gather(sets[i], B, layout, out)
   e1.record(stream)
   e1.synchronize()
   eager_us = e0.elapsed_time(e1) * 1e3 / iters

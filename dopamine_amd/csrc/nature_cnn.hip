@@ -216,23 +216,36 @@ struct ColKScalar {
 };
 
 // ---------------------------------------------------------------- epilogues
+// Epilogues with kPrefetch read one input per output element (bias, ReLU mask)
+// that does not depend on the product: the tile kernel issues pf() before its K
+// loop and hands the value to apply(), so that load's latency hides under the
+// operand fetches instead of following the reduction (same arithmetic).
 struct EpiBiasAct {          // out[m][n] = act(acc + bias[n])
   float* out;
   const float* bias;
   int ld;
   bool relu;
-  __device__ __forceinline__ void operator()(int m, int n, float v, int) const {
-    v = __fadd_rn(v, bias[n]);
+  static constexpr bool kPrefetch = true;
+  __device__ __forceinline__ float pf(int, int n) const { return bias[n]; }
+  __device__ __forceinline__ void apply(int m, int n, float v, float b) const {
+    v = __fadd_rn(v, b);
     out[(int64_t)m * ld + n] = relu ? fmaxf(v, 0.0f) : v;
+  }
+  __device__ __forceinline__ void operator()(int m, int n, float v, int) const {
+    apply(m, n, v, pf(m, n));
   }
 };
 struct EpiMask {             // out[m][n] = acc * (act[m][n] > 0)   (ReLU backward)
   float* out;
   const float* act;
   int ld;
+  static constexpr bool kPrefetch = true;
+  __device__ __forceinline__ float pf(int m, int n) const { return act[(int64_t)m * ld + n]; }
+  __device__ __forceinline__ void apply(int m, int n, float v, float a) const {
+    out[(int64_t)m * ld + n] = a > 0.0f ? v : 0.0f;
+  }
   __device__ __forceinline__ void operator()(int m, int n, float v, int) const {
-    const int64_t i = (int64_t)m * ld + n;
-    out[i] = act[i] > 0.0f ? v : 0.0f;
+    apply(m, n, v, pf(m, n));
   }
 };
 struct EpiStore {            // out[m][n] = acc
@@ -309,6 +322,15 @@ struct EpiGradAdam {
   __device__ __forceinline__ void operator()(int m, int n, float g, int) const {
     commit(m, n, g, pre(m, n));
   }
+};
+
+template <class EP, class = void>
+struct HasPf {
+  static constexpr bool value = false;
+};
+template <class EP>
+struct HasPf<EP, decltype((void)EP::kPrefetch)> {
+  static constexpr bool value = EP::kPrefetch;
 };
 
 template <class EP, class = void>
@@ -450,6 +472,25 @@ __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& 
     }
   };
 
+  // the epilogue's product-independent input (bias / ReLU mask) of this thread's
+  // reduction elements, loaded now (clamped, never branching); see kPrefetch
+  constexpr int NE = (OUT + T - 1) / T;
+#ifdef DQ_NO_PF
+  constexpr bool kPf = false;
+#else
+  constexpr bool kPf = WK > 1 && HasPf<EP>::value && NE <= 2;
+#endif
+  float pfv[NE];
+  if constexpr (kPf) {
+#pragma unroll
+    for (int i = 0; i < NE; ++i) {
+      const int e = min(tid + i * T, OUT - 1);
+      const int tile = e >> 10, r = (e >> 6) & 15, l = e & 63;
+      const int m = m0 + (tile % WM) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
+      const int n = n0 + (tile / WM) * 32 + (l & 31);
+      pfv[i] = E.pf(min(m, M - 1), min(n, N - 1));
+    }
+  }
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
@@ -596,6 +637,21 @@ __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& 
     for (int r = 0; r < 16; ++r) red[r * 64] = acc[r];
   }
   __syncthreads();
+  if constexpr (kPf) {
+#pragma unroll
+    for (int i = 0; i < NE; ++i) {
+      const int e = tid + i * T;
+      if (e >= OUT) break;
+      float v = smem[e];
+#pragma unroll
+      for (int j = 1; j < WK; ++j) v = __fadd_rn(v, smem[j * OUT + e]);
+      const int tile = e >> 10, r = (e >> 6) & 15, l = e & 63;
+      const int m = m0 + (tile % WM) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
+      const int n = n0 + (tile / WM) * 32 + (l & 31);
+      if (m < M && n < N) E.apply(m, n, v, pfv[i]);
+    }
+    return;
+  }
   for (int e = tid; e < OUT; e += T) {
     float v = smem[e];
 #pragma unroll
@@ -1131,10 +1187,27 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
       if (in(1)) group_r(c, rd(1), dW_fc2, dX_fc1);
       if (in(2)) group_r(c, rd(2), dW_fc1, dX_c3, part(p->fc2_w, p->fc2_b + NO));
       if (head) {
+#if DQ_ORDER == 1
+        if (in(3)) group_r(c, rd(3), head->conv1(), dW_c3, dcol, part(f0, f1));
+        if (in(4)) group_r(c, rd(4), head->conv2(), sum_c3, dW_c2, da1, part(f1, f2));
+        if (in(5)) group_r(c, rd(5), head->conv3(), sum_c2, dW_c1, part(f2, f3));
+        if (in(6)) group_r(c, rd(6), head->fc1(), sum_c1, part(p->conv2_w, p->fc1_w));
+#elif DQ_ORDER == 2
+        if (in(3)) group_r(c, rd(3), head->conv1(), part(f0, f1), dW_c3, dcol);
+        if (in(4)) group_r(c, rd(4), head->conv2(), part(f1, f2), sum_c3, dW_c2, da1);
+        if (in(5)) group_r(c, rd(5), head->conv3(), part(f2, f3), sum_c2, dW_c1);
+        if (in(6)) group_r(c, rd(6), head->fc1(), part(p->conv2_w, p->fc1_w), sum_c1);
+#elif DQ_ORDER == 3
+        if (in(3)) group_r(c, rd(3), part(f0, f1), dW_c3, dcol, head->conv1());
+        if (in(4)) group_r(c, rd(4), part(f1, f2), sum_c3, dW_c2, da1, head->conv2());
+        if (in(5)) group_r(c, rd(5), part(f2, f3), sum_c2, dW_c1, head->conv3());
+        if (in(6)) group_r(c, rd(6), part(p->conv2_w, p->fc1_w), sum_c1, head->fc1());
+#else
         if (in(3)) group_r(c, rd(3), dW_c3, dcol, part(f0, f1), head->conv1());
         if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, da1, part(f1, f2), head->conv2());
         if (in(5)) group_r(c, rd(5), sum_c2, dW_c1, part(f2, f3), head->conv3());
         if (in(6)) group_r(c, rd(6), sum_c1, part(p->conv2_w, p->fc1_w), head->fc1());
+#endif
         return;
       }
       if (in(3)) group_r(c, rd(3), dW_c3, dcol, part(f0, f1));

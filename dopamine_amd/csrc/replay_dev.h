@@ -310,11 +310,25 @@ __device__ __forceinline__ int64_t stack_base(const ReplayView& v, const GatherO
 // Per-sample scalars (crb:517-555), one wave: lanes load the trajectory's
 // terminal/reward bytes in parallel, the ballot finds L, lane 0 sums the
 // float32 products left to right exactly as numpy's n < 8 reduction does.
+// Loads that need L (next_action/next_reward at idx + L) are issued for the
+// usual L = n together with the trajectory and re-read only when a terminal
+// cuts it short, so the wave waits on two dependent loads (index, then
+// everything else), not three.
 __device__ inline void write_scalars_wave(const ReplayView& v, const GatherOut& g, int b) {
   const int lane = threadIdx.x & 63;
   const int64_t idx = pymod((int64_t)g.indices[b], v.C);
   float p = 0.0f;
   bool t = false;
+  // independent of L: issued with the trajectory
+  const int64_t nspec = pymod(idx + v.n, v.C);
+  int32_t a0 = 0, na = 0;
+  float nr = 0.0f, pr = 0.0f;
+  if (lane == 0) {
+    a0 = v.actions[idx];
+    na = v.actions[nspec];
+    nr = v.rewards[nspec];
+    if (g.probs) pr = (float)v.tree[((int64_t)1 << v.depth) - 1 + idx];
+  }
   if (lane < v.n) {
     const int64_t j = pymod(idx + lane, v.C);
     t = v.terminals[j] != 0;
@@ -339,23 +353,40 @@ __device__ inline void write_scalars_wave(const ReplayView& v, const GatherOut& 
       for (int k = 0; k < L; ++k)
         acc = __fadd_rn(acc, __fmul_rn(v.discount[k], v.rewards[pymod(idx + k, v.C)]));
     }
-    const int64_t nxt = pymod(idx + L, v.C);
-    if (g.action) g.action[b] = v.actions[idx];
+    if (L != v.n) {     // a terminal ended the trajectory early: the loads at idx + L
+      const int64_t nxt = pymod(idx + L, v.C);
+      na = v.actions[nxt];
+      nr = v.rewards[nxt];
+    }
+    if (g.action) g.action[b] = a0;
     if (g.reward) g.reward[b] = acc;
-    if (g.next_action) g.next_action[b] = v.actions[nxt];
-    if (g.next_reward) g.next_reward[b] = v.rewards[nxt];
+    if (g.next_action) g.next_action[b] = na;
+    if (g.next_reward) g.next_reward[b] = nr;
     if (g.terminal) g.terminal[b] = term ? 1 : 0;
     if (g.indices_out) g.indices_out[b] = (int32_t)idx;
-    if (g.probs) g.probs[b] = (float)v.tree[((int64_t)1 << v.depth) - 1 + idx];
+    if (g.probs) g.probs[b] = pr;
   }
 }
 
+// tf.div(tf.cast(x, f32), 255.) for a byte x, correctly rounded: q = x * fl(1/255)
+// is off by one ulp for 126 of the 256 bytes; one Newton residual step
+// r = fma(-q, 255, x), q + r * fl(1/255) (fused) restores the correctly rounded
+// quotient for every byte (checked exhaustively against x / 255.f, and against
+// the oracle by the gather parity tests) -- 3 VALU ops instead of the IEEE
+// division sequence (div_scale/rcp/fma chain/div_fixup).
+__device__ __forceinline__ float u8_unit(uint32_t x) {
+  constexpr float kInv = 1.0f / 255.0f;
+  const float xf = (float)x;
+  const float q = __fmul_rn(xf, kInv);
+  return __builtin_fmaf(__builtin_fmaf(-q, 255.0f, xf), kInv, q);
+}
+
 __device__ __forceinline__ float4 u8x4_to_f32_255(uint32_t w) {
-  float4 o;  // tf.div(tf.cast(x, f32), 255.) -- correctly rounded division
-  o.x = __fdiv_rn((float)(w & 0xffu), 255.0f);
-  o.y = __fdiv_rn((float)((w >> 8) & 0xffu), 255.0f);
-  o.z = __fdiv_rn((float)((w >> 16) & 0xffu), 255.0f);
-  o.w = __fdiv_rn((float)(w >> 24), 255.0f);
+  float4 o;
+  o.x = u8_unit(w & 0xffu);
+  o.y = u8_unit((w >> 8) & 0xffu);
+  o.z = u8_unit((w >> 16) & 0xffu);
+  o.w = u8_unit(w >> 24);
   return o;
 }
 
@@ -376,17 +407,32 @@ __device__ __forceinline__ void gather_nhwc4_body(const ReplayView& v, const Gat
   // this wave's R x 64 dwords of each of the 4 frames
   const int64_t w0 = ((int64_t)bx * 256 + (tid & ~63)) * R;
   if (w0 >= nd) return;
-  const int64_t base = stack_base(v, g, b, which);
-  const uint32_t* fr[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-    fr[k] = (const uint32_t*)(v.frames + pymod(base - 3 + k, v.C) * v.obs_bytes);
+  // next_state's stack ends at idx + L (L = n-step length, crb:517-531).  Its
+  // frames are loaded for the usual L = n together with the trajectory's
+  // terminal bytes and re-loaded only when a terminal makes L < n (wave-uniform
+  // branch), so frames wait on the index alone: two dependent cold loads, not three.
+  const int64_t idx = pymod((int64_t)g.indices[b], v.C);
   uint32_t w[R][4];
+  auto load = [&](int64_t base) {
+    const uint32_t* fr[4];
 #pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int64_t d = w0 + 64 * r + lane;
+    for (int k = 0; k < 4; ++k)
+      fr[k] = (const uint32_t*)(v.frames + pymod(base - 3 + k, v.C) * v.obs_bytes);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) w[r][k] = d < nd ? fr[k][d] : 0u;
+    for (int r = 0; r < R; ++r) {
+      const int64_t d = w0 + 64 * r + lane;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) w[r][k] = d < nd ? fr[k][d] : 0u;
+    }
+  };
+  if (which) {
+    const int64_t spec = pymod(idx + v.n, v.C);
+    load(spec);
+    bool term;
+    const int64_t base = pymod(idx + traj_len_par(v, idx, &term), v.C);
+    if (base != spec) load(base);
+  } else {
+    load(idx);
   }
   // store j of chunk r: lane l writes pixel 64j + l of the chunk (its 4 channels =
   // 16 B), so every store instruction covers 1 KiB contiguous; the bytes come from
@@ -400,10 +446,10 @@ __device__ __forceinline__ void gather_nhwc4_body(const ReplayView& v, const Gat
     for (int j = 0; j < 4; ++j) {
       const int src = 16 * j + (lane >> 2);
       float4 o;
-      o.x = __fdiv_rn((float)((__shfl(w[r][0], src) >> sh) & 0xffu), 255.0f);
-      o.y = __fdiv_rn((float)((__shfl(w[r][1], src) >> sh) & 0xffu), 255.0f);
-      o.z = __fdiv_rn((float)((__shfl(w[r][2], src) >> sh) & 0xffu), 255.0f);
-      o.w = __fdiv_rn((float)((__shfl(w[r][3], src) >> sh) & 0xffu), 255.0f);
+      o.x = u8_unit((__shfl(w[r][0], src) >> sh) & 0xffu);
+      o.y = u8_unit((__shfl(w[r][1], src) >> sh) & 0xffu);
+      o.z = u8_unit((__shfl(w[r][2], src) >> sh) & 0xffu);
+      o.w = u8_unit((__shfl(w[r][3], src) >> sh) & 0xffu);
       if (4 * d0 + 64 * j + lane < 4 * nd) dst[64 * j + lane] = o;
     }
   }
