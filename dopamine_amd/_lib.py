@@ -119,7 +119,13 @@ SIGNATURES = {
     'dq_cnn_backward_riders': [ctypes.POINTER(CnnParams), ctypes.POINTER(CnnParams), _I32, _P,
                                ctypes.POINTER(CnnActs), _P, ctypes.POINTER(CnnActs), _P,
                                ctypes.POINTER(Rider), _I32, ctypes.POINTER(AdamArgs),
-                               ctypes.POINTER(CnnNet), _I32, _I32, _P],
+                               ctypes.POINTER(CnnNet), _I32, _I32, _I32, _P],
+    'dq_cnn_forward_fused': [ctypes.POINTER(CnnParams), _P, ctypes.POINTER(CnnActs), _P,
+                             ctypes.POINTER(CnnParams), ctypes.POINTER(CnnActs), _P, _I32, _I32,
+                             _P],
+    'dq_cnn_fc2_parts_offset': [_I32],
+    'dq_c51_loss_fused': [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _I32, _I32, _I32, _F, _P, _P,
+                          _P, _P, _P, _P, _I32, _P, _P, _P],
     'dq_cnn_forward_head': [ctypes.POINTER(CnnParams), _I32, _P, ctypes.POINTER(CnnActs), _P, _P],
     'dq_cnn_forward_with_tail': [ctypes.POINTER(CnnParams), _P, ctypes.POINTER(CnnActs), _P,
                                  ctypes.POINTER(CnnParams), ctypes.POINTER(CnnActs), _P, _I32, _P],
@@ -128,7 +134,8 @@ SIGNATURES = {
                               _P],
     'dq_cnn_workspace_floats': [_I32, _I32],
 }
-RESTYPES = {'dq_last_error': ctypes.c_char_p, 'dq_cnn_workspace_floats': ctypes.c_size_t}
+RESTYPES = {'dq_last_error': ctypes.c_char_p, 'dq_cnn_workspace_floats': ctypes.c_size_t,
+            'dq_cnn_fc2_parts_offset': ctypes.c_size_t}
 
 
 class DQError(RuntimeError):

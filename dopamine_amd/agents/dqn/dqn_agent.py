@@ -86,6 +86,7 @@ class DQNAgent(object):
                fuse_optimizer=True,
                pair_forward=False,
                ride_replay=True,
+               fused_head=True,
                device=None,
                seed=0,
                process_group=None):
@@ -123,6 +124,7 @@ class DQNAgent(object):
     self.fuse_optimizer = fuse_optimizer
     self.pair_forward = pair_forward
     self.ride_replay = ride_replay
+    self.fused_head = fused_head
     self._graph_sets = {}          # pipe -> (graphs per parity, optimizer graphs per parity)
     self._graph_pool = None
     self._eager_steps = {True: 0, False: 0}
@@ -234,10 +236,11 @@ class DQNAgent(object):
 
   def _backward(self, y, g, k=0):
     if self._hip is not None:       # all gradients stored into the flat buffer
+      groups = (1, 7) if self._fused() else None    # fused: d h came with the loss
       if self._fused_opt():
-        self._hip['online'].backward(g, adam=self._opt, slot=k)
+        self._hip['online'].backward(g, adam=self._opt, slot=k, groups=groups)
       else:
-        self._hip['online'].backward(g)
+        self._hip['online'].backward(g, groups=groups)
       return
     # Fresh per-parameter gradients (no flat-buffer zeroing + accumulate kernels);
     # the multi-tensor TF1 Adam reads them in place.
@@ -273,6 +276,34 @@ class DQNAgent(object):
     fork/join edges (they cost ~28 us of a ~190 us step on MI355X), and the
     target forward adds no launches of its own."""
     return self.ride_replay and self._hip is not None
+
+  def _fused(self):
+    """fused_head: the loss kernel consumes the CNN's fc2 k-band partials and writes
+    fc2's input gradient (cnn.forward_fused + a loss override of _fused_loss), so
+    the forward and the backward each lose a launch.  Rainbow/C51 only."""
+    return False
+
+  def _fused_loss(self, t, c):
+    raise NotImplementedError
+
+  def _loss(self, t, c):
+    """(output, d loss / d output) of step slot c, by the fused or the plain path."""
+    if self._fused():
+      return self._fused_loss(t, c)
+    return self._online_loss(t, self._ptgt[c])
+
+  def _forward_ride(self, c):
+    """The online forward of slot c with the target network's tail (ride mode)."""
+    from dopamine_amd import cnn
+    if self._fused():
+      cnn.forward_fused(self._hip['online'], self._pbuf[c]['state'], self._hip['target'][c])
+      return
+    on, tg = cnn.forward_with_tail(self._hip['online'], self._pbuf[c]['state'], self._hip['target'][c])
+    self._online_ready = on
+    self._ptgt[c] = self._target_dict(tg)
+
+  def _bwd_first(self):
+    return 1 if self._fused() else 0
 
   def _pairs(self):
     return self.pair_forward and self._hip is not None and not self._rides()
@@ -316,20 +347,19 @@ class DQNAgent(object):
     if not pipe:
       self._prefetch(c)
     if self._rides():
-      from dopamine_amd.cnn import forward_with_tail
-      on, tg = forward_with_tail(self._hip['online'], self._pbuf[c]['state'], self._hip['target'][c])
-      self._online_ready = on
-      self._ptgt[c] = self._target_dict(tg)
+      self._forward_ride(c)
     elif self._pairs():
       self._forward_pair(c)
-    y, g = self._online_loss(self._pbuf[c], self._ptgt[c])
+    y, g = self._loss(self._pbuf[c], c)
     if pipe and self._rides():
       self._head = None
       with self._replay.memory.recording() as riders:
         self._post_loss(self._pbuf[c])
         self._prefetch(1 - c)
       adam = self._opt if self._fused_opt() else None
-      self._hip['online'].backward(g, riders=riders, adam=adam, slot=k, head=self._head)
+      f = self._bwd_first()
+      self._hip['online'].backward(g, riders=riders, adam=adam, slot=k, head=self._head,
+                                   groups=(f, 7), head_from=3 + f)
       self._head = None
     elif pipe:
       main = torch.cuda.current_stream(self._device)
@@ -361,23 +391,23 @@ class DQNAgent(object):
     if not pipe:
       self._prefetch(c)
     if self._rides():
-      from dopamine_amd.cnn import forward_with_tail
-      on, tg = forward_with_tail(self._hip['online'], self._pbuf[c]['state'], self._hip['target'][c])
-      self._online_ready = on
-      self._ptgt[c] = self._target_dict(tg)
+      self._forward_ride(c)
     elif self._pairs():
       self._forward_pair(c)
-    y, g = self._online_loss(self._pbuf[c], self._ptgt[c])
-    if pipe and self._rides():      # priority write-back -> sample -> gather ride in launches 0-2
+    y, g = self._loss(self._pbuf[c], c)
+    f = self._bwd_first()
+    self._tail_riders = None
+    if pipe and self._rides():      # priority write-back -> sample -> gather ride in launches f..2
       self._head = None
       with self._replay.memory.recording() as riders:
         self._post_loss(self._pbuf[c])
         self._prefetch(1 - c)
-      assert len(riders) <= self._SPLIT
-      self._hip['online'].backward(g, groups=(0, self._SPLIT), riders=riders)
+      n = self._SPLIT - f
+      self._hip['online'].backward(g, groups=(f, self._SPLIT), riders=riders[:n])
+      self._tail_riders = riders[n:] or None     # the fused path's gather rides in launch 3
       self._tail_head, self._head = self._head, None
     else:
-      self._hip['online'].backward(g, groups=(0, self._SPLIT))
+      self._hip['online'].backward(g, groups=(f, self._SPLIT))
     self._dout = g
 
   def _grad_step_tail(self, c, k, pipe=None):
@@ -386,9 +416,11 @@ class DQNAgent(object):
     if self._rides():               # the target head on the gathered batch rides in launches 3-6
       if not pipe:
         self._post_loss(self._pbuf[c])
+      f = self._bwd_first()
       self._hip['online'].backward(g, groups=(self._SPLIT, 7),
-                                   head=self._tail_head if pipe else None)
-      self._tail_head = None
+                                   head=self._tail_head if pipe else None,
+                                   riders=self._tail_riders if pipe else None, head_from=3 + f)
+      self._tail_head = self._tail_riders = None
     elif pipe:
       main = torch.cuda.current_stream(self._device)
       ev = torch.cuda.Event()

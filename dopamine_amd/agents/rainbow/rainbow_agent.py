@@ -129,6 +129,19 @@ class RainbowAgent(dqn_agent.DQNAgent):
                        out=self._loss_out)
     return logits, out['grad']
 
+  def _fused(self):
+    return self.fused_head and self._rides()
+
+  def _fused_loss(self, t, c):
+    """_online_loss on the CNN's fc2 partials (cnn.forward_fused): the logits are
+    summed inside the loss kernel, which also writes fc2's input gradient."""
+    prioritized = self._replay_scheme == 'prioritized'
+    out = ops.c51_loss_fused(self._hip['online'], self._hip['target'][c], t['action'], t['reward'],
+                             t['terminal'], self._support, self.cumulative_gamma,
+                             probs=t['sampling_probabilities'] if prioritized else None,
+                             out=self._loss_out)
+    return None, out['grad']
+
   def _post_loss(self, t):
     if self._replay_scheme == 'prioritized':
       # sqrt(loss + 1e-10) of the UNWEIGHTED loss (rb:289-290); it precedes the

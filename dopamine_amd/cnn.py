@@ -101,7 +101,8 @@ class HipNatureCNN(object):
                          state=adam.state.data_ptr(), slot=int(slot), lr=adam.lr,
                          beta1=adam.b1, beta2=adam.b2, epsilon=adam.eps)
 
-  def backward(self, dout, parallel=False, adam=None, slot=0, groups=None, riders=None, head=None):
+  def backward(self, dout, parallel=False, adam=None, slot=0, groups=None, riders=None, head=None,
+               head_from=3):
     """dout: (B, n_out).  Writes all parameter gradients into net.fp.grad.
 
     riders: replay operations recorded with ``ReplayBuffer.recording()`` (the
@@ -112,7 +113,11 @@ class HipNatureCNN(object):
     riders gather); its forward_with_tail then finishes it.
 
     groups=(first, last): only launches [first, last) of the 7 grouped launches
-    (a data-parallel learner all-reduces fc1/fc2's gradients after launch 3).
+    (a data-parallel learner all-reduces fc1/fc2's gradients after launch 3);
+    rider i rides in launch first + i.  first = 1 skips fc2's input gradient
+    (dacts['h'] already written, by ``c51_loss_fused``).  head_from = 4: the
+    head's conv1..conv3 ride in launches 4..6 and its fc1 slabs are left to
+    ``forward_fused`` (the Rainbow fast path).
 
     adam: an ops.TF1Adam over net.fp.flat -- its step (beta-power slot ``slot``)
     is applied inside the gradient epilogues (dq_cnn_backward_adam), so no
@@ -127,7 +132,7 @@ class HipNatureCNN(object):
     with the other stream's.  Kept for experimentation; off by default."""
     dout = dout.reshape(self.B, self.n_out)
     assert dout.is_contiguous() and self._x is not None
-    if riders or head is not None:
+    if riders or head is not None or (groups is not None and adam is not None):
       args = None if adam is None else ctypes.byref(self._adam_args(adam, slot))
       riders = riders or []
       arr = (_lib.Rider * max(1, len(riders)))(*riders)
@@ -139,7 +144,7 @@ class HipNatureCNN(object):
       _lib.check(_lib.lib.dq_cnn_backward_riders(
           ctypes.byref(self._p), ctypes.byref(self._g), self.B, self._x.data_ptr(),
           ctypes.byref(self._a), dout.data_ptr(), ctypes.byref(self._d), self.ws.data_ptr(),
-          arr, len(riders), args, hn, int(first), int(last), self._stream(dout)),
+          arr, len(riders), args, hn, int(head_from), int(first), int(last), self._stream(dout)),
           'dq_cnn_backward_riders')
       return self.net.fp.grad
     if groups is not None:          # a sub-range of the 7 grouped launches
@@ -213,3 +218,27 @@ def forward_with_tail(a, xa, b):
       ctypes.byref(b._p), ctypes.byref(b._a), b.ws.data_ptr(), a.B, a._stream(xa)),
       'dq_cnn_forward_with_tail')
   return a.acts['out'], b.acts['out']
+
+
+def fc2_parts(net):
+  """The (16, B, n_out) view of ``net``'s fc2 k-band partials (forward_fused)."""
+  off = int(_lib.lib.dq_cnn_fc2_parts_offset(net.B))
+  n = 16 * net.B * net.n_out
+  return net.ws[off:off + n].view(16, net.B, net.n_out)
+
+
+def forward_fused(a, xa, b, fc1_b=True):
+  """The Rainbow fast path's forward (dq_cnn_forward_fused): ``a`` (online) on
+  ``xa`` through fc1, ``b`` (target; conv1..conv3 already run, e.g. riding in the
+  previous backward with head_from=4) from its fc1 slabs (if ``fc1_b``), then one
+  launch summing both nets' fc1 slabs and forming fc2's 16 k-band partials.
+  Neither net's logits are stored: ``ops.c51_loss_fused`` sums the partials
+  (bitwise the logits of ``forward``).  Returns the two partial views."""
+  assert a.B == b.B and a is not b
+  xa = a._nhwc(xa)
+  a._x = xa
+  _lib.check(_lib.lib.dq_cnn_forward_fused(
+      ctypes.byref(a._p), xa.data_ptr(), ctypes.byref(a._a), a.ws.data_ptr(),
+      ctypes.byref(b._p), ctypes.byref(b._a), b.ws.data_ptr(), a.B, int(bool(fc1_b)),
+      a._stream(xa)), 'dq_cnn_forward_fused')
+  return fc2_parts(a), fc2_parts(b)

@@ -45,39 +45,122 @@ __device__ float per_weight(const float* probs, int B, int b, float* s_red) {
   return __fdiv_rn(w, m);
 }
 
-// One block per sample b; wave a (strided) computes the target softmax / Q of
-// action a; wave 0 then takes the greedy action (first max), builds Tz, the
-// Eq.-7 projection (lane = target atom, LDS broadcast of the source atoms) and
-// the softmax cross-entropy of the chosen online logits; the other waves zero
-// the gradient rows of the non-chosen actions.
-__global__ __launch_bounds__(1024) void k_c51(C51Args a) {
+// Logit sources: stored logits, or (the fused Rainbow path) fc2's 16 k-band
+// partial products summed in band order plus the bias -- exactly the reduction
+// order of the CNN's fc2 tile, so the logits are bitwise dq_cnn_forward's.
+struct LogitsDirect {
+  const float* p;
+  __device__ __forceinline__ float get(int64_t i) const { return p[i]; }
+};
+struct LogitsParts {
+  const float* part;   // [np][B * NO]
+  const float* bias;   // [NO]
+  int64_t stride;      // B * NO
+  int np, NO;
+  __device__ __forceinline__ float get(int64_t i) const {
+    float v[16];
+#pragma unroll
+    for (int z = 0; z < 16; ++z) v[z] = part[(int64_t)min(z, np - 1) * stride + i];
+    float x = v[0];
+#pragma unroll
+    for (int z = 1; z < 16; ++z)
+      if (z < np) x = __fadd_rn(x, v[z]);
+    for (int z = 16; z < np; ++z) x = __fadd_rn(x, part[(int64_t)z * stride + i]);
+    return __fadd_rn(x, bias[i % NO]);
+  }
+};
+
+// The fused path's extras: logits written out (the CNN never stores them), and the
+// fc2 input gradient d h = (dlogits . W2) * (h > 0) -- only the chosen action's
+// N logits of a sample have a nonzero gradient, so row b of d h is an N-term sum.
+struct C51Extra {
+  float* ol_out;       // (B, A*N) online logits, may be NULL
+  float* tl_out;       // (B, A*N) target logits, may be NULL
+  const float* w2;     // (A*N, H) online fc2 weights; NULL: no d h
+  const float* h;      // (B, H) online fc1 activation (ReLU mask)
+  float* dh;           // (B, H)
+  int H;
+};
+
+// One block per sample b.  Wave a (strided) computes the target softmax / Q of
+// action a; every wave then takes the greedy action (first max) and builds Tz,
+// the waves split the Eq.-7 projection's source atoms j between them (lane =
+// target atom i, term c(i, j) * p_j into LDS), and wave 0 sums the terms in j
+// order -- the reference's arithmetic and order, in N / waves serial steps
+// instead of N -- before the softmax cross-entropy of the chosen online logits.
+// The fused path (x.w2) also forms d h from the chosen action's N logit
+// gradients; its W2 rows are fetched into LDS at the start, under the chain.
+constexpr int kC51PreMax = 48;       // W2 prefetch registers per thread (fused d h)
+
+template <class LS>
+__global__ __launch_bounds__(1024) void k_c51(C51Args a, LS ol, LS tl, C51Extra x) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int N = a.N, A = a.A, b = blockIdx.x;
+  const int N = a.N, A = a.A, b = blockIdx.x, T = blockDim.x;
   float* s_p = smem;                 // [A][N] target probabilities
   float* s_q = s_p + A * N;          // [A]    target Q
   float* s_tz = s_q + A;             // [N]    clipped Bellman support
+  float* s_g = s_tz + N;             // [N]    the chosen action's logit gradient
+  float* s_c = s_g + N;              // [N][64] projection terms c(i, j) p_j
+  float* s_w = s_c + N * kWave;      // [N][H] the chosen action's fc2 rows (fused d h)
   __shared__ float s_red[16];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = T >> 6;
   const bool on = lane < N;
   const float ninf = -__builtin_inff();
   const float z = on ? a.support[lane] : 0.0f;
-  for (int act = wave; act < A; act += nw) {
-    const float x = on ? a.tl[((int64_t)b * A + act) * N + lane] : ninf;
-    const float mx = wave_max(x);
-    const float e = on ? expf(__fsub_rn(x, mx)) : 0.0f;
+  const int ab = a.act[b];
+  // the chosen online logit row, issued with the target rows (wave 0 uses it last)
+  const float y = (wave == 0 && on) ? ol.get(((int64_t)b * A + ab) * N + lane) : ninf;
+  float xv[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int act = wave + r * nw;
+    xv[r] = (act < A && on) ? tl.get(((int64_t)b * A + act) * N + lane) : ninf;
+  }
+  // fused d h: this sample's W2 rows (N x H) and h mask, loaded now, stored after the softmax
+  const bool pre = x.w2 && N * x.H <= kC51PreMax * T;
+  const float* wr = x.w2 ? x.w2 + (int64_t)ab * N * x.H : nullptr;
+  float wv[kC51PreMax];
+  if (pre) {
+#pragma unroll
+    for (int u = 0; u < kC51PreMax; ++u) {
+      const int e = threadIdx.x + u * T;
+      wv[u] = e < N * x.H ? wr[e] : 0.0f;
+    }
+  }
+  const float hv = (x.w2 && (int)threadIdx.x < x.H) ? x.h[(int64_t)b * x.H + threadIdx.x] : 0.0f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int act = wave + r * nw;
+    if (act >= A) break;
+    const float v = xv[r];
+    if (x.tl_out && on) x.tl_out[((int64_t)b * A + act) * N + lane] = v;
+    const float mx = wave_max(v);
+    const float e = on ? expf(__fsub_rn(v, mx)) : 0.0f;
     const float p = __fdiv_rn(e, wave_sum(e));
     const float q = wave_sum(on ? __fmul_rn(z, p) : 0.0f);
     if (on) s_p[act * N + lane] = p;
     if (lane == 0) s_q[act] = q;
   }
-  const int ab = a.act[b];
-  const float w = per_weight(a.probs, a.B, b, s_red);   // contains a __syncthreads
+  if (x.ol_out)
+    for (int act = wave; act < A; act += nw) {
+      const int64_t i = ((int64_t)b * A + act) * N + lane;
+      if (on) x.ol_out[i] = act == ab && wave == 0 ? y : ol.get(i);
+    }
+  if (pre) {
+#pragma unroll
+    for (int u = 0; u < kC51PreMax; ++u) {
+      const int e = threadIdx.x + u * T;
+      if (e < N * x.H) s_w[e] = wv[u];
+    }
+  }
+  __syncthreads();            // s_p, s_q (and s_w) complete
+  const float w = per_weight(a.probs, a.B, b, s_red);
   const float gscale = __fmul_rn(w, __fdiv_rn(1.0f, (float)a.B));
   for (int act = wave; act < A; act += nw) {
     if (act == ab) continue;
     if (on) a.grad[((int64_t)b * A + act) * N + lane] = 0.0f;
   }
-  if (wave != 0) return;
+  // greedy target action (first max) and Tz, redundantly per wave (no barrier)
   int astar = 0;
   float best = s_q[0];
   for (int act = 1; act < A; ++act)
@@ -88,30 +171,57 @@ __global__ __launch_bounds__(1024) void k_c51(C51Args a) {
   const float vmin = a.support[0], vmax = a.support[N - 1];
   const float dz = __fsub_rn(a.support[1], a.support[0]);
   const float gt = __fmul_rn(a.cg, __fsub_rn(1.0f, (float)a.term[b]));
-  if (on) s_tz[lane] = fminf(fmaxf(__fadd_rn(a.rew[b], __fmul_rn(gt, z)), vmin), vmax);
-  __builtin_amdgcn_s_barrier();   // single wave: orders the LDS writes above before the reads
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   const float* pst = s_p + astar * N;
-  float proj = 0.0f;
-  if (on) {
-    for (int j = 0; j < N; ++j) {
-      float c = __fsub_rn(1.0f, __fdiv_rn(fabsf(__fsub_rn(s_tz[j], z)), dz));
+  // projection terms: wave w takes source atoms j = w, w + nw, ...; lane = target atom i
+  for (int j = wave; j < N; j += nw) {
+    const float zj = a.support[j];
+    const float tzj = fminf(fmaxf(__fadd_rn(a.rew[b], __fmul_rn(gt, zj)), vmin), vmax);
+    if (on) {
+      float c = __fsub_rn(1.0f, __fdiv_rn(fabsf(__fsub_rn(tzj, z)), dz));
       c = fminf(fmaxf(c, 0.0f), 1.0f);
-      proj = __fadd_rn(proj, __fmul_rn(c, pst[j]));
+      s_c[j * kWave + lane] = __fmul_rn(c, pst[j]);
     }
   }
-  const float y = on ? a.ol[((int64_t)b * A + ab) * N + lane] : ninf;
-  const float my = wave_max(y);
-  const float sh = on ? __fsub_rn(y, my) : 0.0f;
-  const float ey = on ? expf(sh) : 0.0f;
-  const float sy = wave_sum(ey);
-  const float loss = wave_sum(on ? __fmul_rn(proj, __fsub_rn(logf(sy), sh)) : 0.0f);
-  if (on)
-    a.grad[((int64_t)b * A + ab) * N + lane] = __fmul_rn(gscale, __fsub_rn(__fdiv_rn(ey, sy), proj));
-  if (lane == 0) {
-    if (a.loss_out) a.loss_out[b] = loss;
-    if (a.prio_out) a.prio_out[b] = __fsqrt_rn(__fadd_rn(loss, 1e-10f));
+  __syncthreads();
+  if (wave == 0) {
+    float proj = 0.0f;
+    if (on)
+      for (int j = 0; j < N; ++j) proj = __fadd_rn(proj, s_c[j * kWave + lane]);
+    const float my = wave_max(y);
+    const float sh = on ? __fsub_rn(y, my) : 0.0f;
+    const float ey = on ? expf(sh) : 0.0f;
+    const float sy = wave_sum(ey);
+    const float loss = wave_sum(on ? __fmul_rn(proj, __fsub_rn(logf(sy), sh)) : 0.0f);
+    const float gr = on ? __fmul_rn(gscale, __fsub_rn(__fdiv_rn(ey, sy), proj)) : 0.0f;
+    if (on) {
+      a.grad[((int64_t)b * A + ab) * N + lane] = gr;
+      s_g[lane] = gr;
+    }
+    if (lane == 0) {
+      if (a.loss_out) a.loss_out[b] = loss;
+      if (a.prio_out) a.prio_out[b] = __fsqrt_rn(__fadd_rn(loss, 1e-10f));
+    }
   }
+  if (!x.w2) return;
+  __syncthreads();
+  // d h[b][j] = (h[b][j] > 0) * sum_i g_i W2[ab*N + i][j], i in order
+  for (int j = threadIdx.x; j < x.H; j += T) {
+    const float m = j == (int)threadIdx.x ? hv : x.h[(int64_t)b * x.H + j];
+    float acc = 0.0f;
+    if (pre) {
+      for (int i = 0; i < N; ++i) acc = __fadd_rn(acc, __fmul_rn(s_g[i], s_w[i * x.H + j]));
+    } else {
+      for (int i = 0; i < N; ++i) acc = __fadd_rn(acc, __fmul_rn(s_g[i], wr[(int64_t)i * x.H + j]));
+    }
+    x.dh[(int64_t)b * x.H + j] = m > 0.0f ? acc : 0.0f;
+  }
+}
+
+// dynamic LDS of k_c51 (bytes), with the fused path's W2 rows when they fit the prefetch
+static size_t c51_lds(int A, int N, int T, int H) {
+  size_t f = (size_t)A * N + A + 2 * N + (size_t)N * kWave;
+  if (H > 0 && N * H <= kC51PreMax * T) f += (size_t)N * H;
+  return f * sizeof(float);
 }
 
 // mean(w * loss) for summaries (rb:298-301); launched only when requested.
@@ -359,15 +469,47 @@ int dq_c51_loss(const float* online_logits, const float* target_logits, const in
             batch, num_actions, num_atoms, cumulative_gamma, grad_logits, loss_out,
             priorities_out, mean_loss_out};
   DQ_CHECK_ARG(!mean_loss_out || loss_out, "mean_loss_out needs loss_out");
-  const size_t shm = sizeof(float) * ((size_t)num_actions * num_atoms + num_actions + num_atoms);
+  DQ_CHECK_ARG(num_actions <= 64, "num_actions must be <= 64");
   const int waves = num_actions < 16 ? num_actions : 16;
-  hipLaunchKernelGGL(k_c51, dim3(batch), dim3(64 * waves), shm, (hipStream_t)stream, a);
+  const size_t shm = c51_lds(num_actions, num_atoms, 64 * waves, 0);
+  hipLaunchKernelGGL(k_c51<LogitsDirect>, dim3(batch), dim3(64 * waves), shm, (hipStream_t)stream,
+                     a, LogitsDirect{online_logits}, LogitsDirect{target_logits}, C51Extra{});
   DQ_CHECK_LAUNCH("k_c51");
   if (mean_loss_out) {
     hipLaunchKernelGGL(k_wmean, dim3(1), dim3(64), 0, (hipStream_t)stream, loss_out, probs, batch,
                        mean_loss_out);
     DQ_CHECK_LAUNCH("k_wmean");
   }
+  return DQ_OK;
+}
+
+int dq_c51_loss_fused(const float* online_parts, const float* online_bias,
+                      const float* target_parts, const float* target_bias, int32_t n_parts,
+                      const int32_t* actions, const float* rewards, const uint8_t* terminals,
+                      const float* probs, const float* support, int32_t batch,
+                      int32_t num_actions, int32_t num_atoms, float cumulative_gamma,
+                      float* grad_logits, float* loss_out, float* priorities_out,
+                      const float* fc2_w, const float* h, float* dh, int32_t hidden,
+                      float* online_logits_out, float* target_logits_out, void* stream) {
+  DQ_CHECK_ARG(online_parts && online_bias && target_parts && target_bias && actions && rewards &&
+                   terminals && support && grad_logits,
+               "null argument");
+  DQ_CHECK_ARG(n_parts >= 1, "n_parts must be >= 1");
+  DQ_CHECK_ARG(num_atoms >= 2 && num_atoms <= 64, "num_atoms must be in [2, 64]");
+  DQ_CHECK_ARG(batch >= 1 && num_actions >= 1 && num_actions <= 256, "bad batch / num_actions");
+  DQ_CHECK_ARG(!fc2_w || (h && dh && hidden >= 1), "d h needs h, dh and hidden");
+  C51Args a{nullptr, nullptr, actions, rewards, terminals, probs, support, batch, num_actions,
+            num_atoms, cumulative_gamma, grad_logits, loss_out, priorities_out, nullptr};
+  const int NO = num_actions * num_atoms;
+  const int64_t stride = (int64_t)batch * NO;
+  DQ_CHECK_ARG(num_actions <= 64, "num_actions must be <= 64");
+  const int waves = num_actions < 16 ? num_actions : 16;
+  const size_t shm = c51_lds(num_actions, num_atoms, 64 * waves, fc2_w ? hidden : 0);
+  hipLaunchKernelGGL(k_c51<LogitsParts>, dim3(batch), dim3(64 * waves), shm, (hipStream_t)stream,
+                     a, LogitsParts{online_parts, online_bias, stride, n_parts, NO},
+                     LogitsParts{target_parts, target_bias, stride, n_parts, NO},
+                     C51Extra{online_logits_out, target_logits_out, fc2_w, h, dh, hidden});
+  DQ_CHECK_LAUNCH("k_c51 fused");
   return DQ_OK;
 }
 

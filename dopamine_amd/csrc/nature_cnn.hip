@@ -741,6 +741,9 @@ __global__ __launch_bounds__(256) void k_col2im(const float* dcol, const float* 
 // each op owns a contiguous range of blockIdx.x.  All ops of a group run with
 // the same block size kGroupT, and the block's LDS is the largest op's.
 constexpr int kGroupT = 1024;
+#ifndef DQ_ADAM_U
+#define DQ_ADAM_U 1
+#endif
 
 template <int WM, int WN, int WK, class AL, class BL, class EP>
 struct GemmOp {
@@ -770,6 +773,97 @@ struct ReduceOp {                 // ordered split-K sum of nz slabs + epilogue
   int blocks() const { return (int)(((int64_t)M * N + T - 1) / T); }
 };
 
+// fc1's split-K sum (+ bias, ReLU) fused with fc2's k-band products: block
+// (m tile, k band j of the 16 32-wide bands of fc2's K = 512, group of 4 fc2
+// n-tiles) sums the fc1 slabs of its 32 x 32 slice of h in slab order (as
+// splitk_sum), applies bias + ReLU (as EpiBiasAct), writes that slice of h (first
+// n-group only) and keeps it in LDS; each wave then runs the 16-MFMA chain of one
+// fc2 n-tile over band j in exactly the operand order of the tile kernel's wave j
+// and stores the 32 x 32 partial to part[j].  Summing part[0..15] in order and
+// adding the bias (dq_c51_loss_fused) reproduces the separate fc1-sum + fc2
+// launches bit for bit, with one launch fewer on the forward's critical path.
+struct FcHeadOp {
+  static constexpr int kT = 256;
+  static constexpr int kBands = kHidden / 32;      // 16
+  static constexpr int kLds = 32 * 33;             // the h slice, rows padded to 33
+  const float* ws;      // fc1 split-K slabs [nz][B][512]
+  int nz;
+  const float* b1;
+  const float* w2;      // [NO][512]
+  float* h;             // [B][512]
+  float* part;          // [16][B][NO]
+  int B, NO, mt, ng;
+  int blocks() const { return mt * kBands * ng; }
+  static int groups(int NO) { return ((NO + 31) / 32 + 3) / 4; }
+  __device__ __forceinline__ void run(int blk, float* smem) const {
+    const int g = blk % ng, j = (blk / ng) % kBands, m0 = 32 * (blk / (ng * kBands));
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    {
+      const int r = tid >> 3, c = 4 * (tid & 7);
+      const int m = min(m0 + r, B - 1);
+      const int64_t i = (int64_t)m * kHidden + 32 * j + c, MN = (int64_t)B * kHidden;
+      float4 s = *reinterpret_cast<const float4*>(ws + i);
+      for (int z0 = 1; z0 < nz; z0 += 8) {
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          v[u] = *reinterpret_cast<const float4*>(ws + (int64_t)min(z0 + u, nz - 1) * MN + i);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (z0 + u < nz) {
+            s.x = __fadd_rn(s.x, v[u].x);
+            s.y = __fadd_rn(s.y, v[u].y);
+            s.z = __fadd_rn(s.z, v[u].z);
+            s.w = __fadd_rn(s.w, v[u].w);
+          }
+      }
+      const float4 bb = *reinterpret_cast<const float4*>(b1 + 32 * j + c);
+      s.x = fmaxf(__fadd_rn(s.x, bb.x), 0.0f);
+      s.y = fmaxf(__fadd_rn(s.y, bb.y), 0.0f);
+      s.z = fmaxf(__fadd_rn(s.z, bb.z), 0.0f);
+      s.w = fmaxf(__fadd_rn(s.w, bb.w), 0.0f);
+      if (g == 0 && m0 + r < B) *reinterpret_cast<float4*>(h + i) = s;
+      float* q = smem + r * 33 + c;
+      q[0] = s.x;
+      q[1] = s.y;
+      q[2] = s.z;
+      q[3] = s.w;
+    }
+    __syncthreads();
+    const int nt = 4 * g + wave;
+    if (32 * nt >= NO) return;
+    const int r = lane & 31, hh = lane >> 5, n = 32 * nt + r;
+    // B operand: lane r's 8 k of each half, straight from W2's row n (k contiguous)
+    float bv[2][8];
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const float* src = w2 + (int64_t)min(n, NO - 1) * kHidden + 32 * j + 16 * hf + 8 * hh;
+      const float4 x0 = *reinterpret_cast<const float4*>(src);
+      const float4 x1 = *reinterpret_cast<const float4*>(src + 4);
+      const bool ok = n < NO;
+      bv[hf][0] = ok ? x0.x : 0.0f; bv[hf][1] = ok ? x0.y : 0.0f;
+      bv[hf][2] = ok ? x0.z : 0.0f; bv[hf][3] = ok ? x0.w : 0.0f;
+      bv[hf][4] = ok ? x1.x : 0.0f; bv[hf][5] = ok ? x1.y : 0.0f;
+      bv[hf][6] = ok ? x1.z : 0.0f; bv[hf][7] = ok ? x1.w : 0.0f;
+    }
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.0f;
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+      for (int s8 = 0; s8 < 8; ++s8)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(smem[r * 33 + 16 * hf + 8 * hh + s8],
+                                                    bv[hf][s8], acc, 0, 0, 0);
+    float* dst = part + (int64_t)j * B * NO;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int m = m0 + (e & 3) + 8 * (e >> 2) + 4 * hh;
+      if (m < B && n < NO) dst[(int64_t)m * NO + n] = acc[e];
+    }
+  }
+};
+
 template <class G>
 struct Col2imOp {
   static constexpr int kT = kGroupT;
@@ -797,21 +891,35 @@ struct AdamOp {
   int64_t n;
   AdamDev o;
   int nb;
+  // kU float4 per array per thread with all 4 kU loads issued before the first
+  // update: more bytes in flight per CU, so the rider holds a CU for less time
+  static constexpr int kU = DQ_ADAM_U;
   __device__ __forceinline__ void run(int blk, float*) const {
     const float alpha = adam_alpha_of(o.state, o.slot, o.lr);
     const float omb1 = __fsub_rn(1.0f, o.b1), omb2 = __fsub_rn(1.0f, o.b2);
-    const int64_t n4 = n >> 2, stride = (int64_t)nb * kT;
-    for (int64_t i = (int64_t)blk * kT + threadIdx.x; i < n4; i += stride) {
-      float4 p = reinterpret_cast<float4*>(var)[i];
-      const float4 g = reinterpret_cast<const float4*>(grad)[i];
-      float4 mm = reinterpret_cast<float4*>(m)[i], vv = reinterpret_cast<float4*>(v)[i];
-      adam1(p.x, g.x, mm.x, vv.x, alpha, omb1, omb2, o.eps);
-      adam1(p.y, g.y, mm.y, vv.y, alpha, omb1, omb2, o.eps);
-      adam1(p.z, g.z, mm.z, vv.z, alpha, omb1, omb2, o.eps);
-      adam1(p.w, g.w, mm.w, vv.w, alpha, omb1, omb2, o.eps);
-      reinterpret_cast<float4*>(var)[i] = p;
-      reinterpret_cast<float4*>(m)[i] = mm;
-      reinterpret_cast<float4*>(v)[i] = vv;
+    const int64_t n4 = n >> 2, stride = (int64_t)nb * kT * kU;
+    for (int64_t i0 = (int64_t)blk * kT * kU + threadIdx.x; i0 < n4; i0 += stride) {
+      float4 p[kU], g[kU], mm[kU], vv[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int64_t i = min(i0 + (int64_t)u * kT, n4 - 1);   // clamped: loads never branch
+        p[u] = reinterpret_cast<float4*>(var)[i];
+        g[u] = reinterpret_cast<const float4*>(grad)[i];
+        mm[u] = reinterpret_cast<float4*>(m)[i];
+        vv[u] = reinterpret_cast<float4*>(v)[i];
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int64_t i = i0 + (int64_t)u * kT;
+        if (i >= n4) break;
+        adam1(p[u].x, g[u].x, mm[u].x, vv[u].x, alpha, omb1, omb2, o.eps);
+        adam1(p[u].y, g[u].y, mm[u].y, vv[u].y, alpha, omb1, omb2, o.eps);
+        adam1(p[u].z, g[u].z, mm[u].z, vv[u].z, alpha, omb1, omb2, o.eps);
+        adam1(p[u].w, g[u].w, mm[u].w, vv[u].w, alpha, omb1, omb2, o.eps);
+        reinterpret_cast<float4*>(var)[i] = p[u];
+        reinterpret_cast<float4*>(m)[i] = mm[u];
+        reinterpret_cast<float4*>(v)[i] = vv[u];
+      }
     }
     if (blk == 0 && threadIdx.x < (n & 3)) {
       const int64_t i = (n4 << 2) + threadIdx.x;
@@ -1001,7 +1109,36 @@ struct FwdOps {
                              EpiBiasAct{a->out, p->fc2_b, p->n_out, false}, B, p->n_out, kHidden,
                              kHidden);
   }
+  // fc2's 16 k-band partials live in ws right after fc1's slabs
+  static size_t part_offset(int B) { return ws_floats(B); }
+  static size_t fused_ws_floats(int B, int NO) {
+    return ws_floats(B) + (size_t)FcHeadOp::kBands * B * NO;
+  }
+  FcHeadOp fchead() const {
+    return FcHeadOp{ws, fc1_slabs(), p->fc1_b, p->fc2_w, a->h, ws + part_offset(B), B, p->n_out,
+                    (B + 31) / 32, FcHeadOp::groups(p->n_out)};
+  }
 };
+
+// The Rainbow fast path's forward: net 0 (online) whole up to fc2's k-band
+// partials, net 1 (target, head run earlier: conv1..conv3 into a1) finishing with
+// its fc1 slabs (if fc1_1) in net 0's fc1 launch and its fused head beside net 0's:
+// 5 launches.  The logits are summed by dq_c51_loss_fused.
+void forward_fused(Ctx& c0, Ctx& c1, const FwdOps& f0, const FwdOps& f1, bool fc1_1) {
+  const size_t n0 = FwdOps::fused_ws_floats(f0.B, f0.p->n_out);
+  const size_t n1 = FwdOps::fused_ws_floats(f1.B, f1.p->n_out);
+  c0.need = n0 > c0.need ? n0 : c0.need;
+  c1.need = n1 > c1.need ? n1 : c1.need;
+  if (c0.dry) return;
+  group(c0, f0.conv1());
+  group(c0, f0.conv2());
+  group(c0, f0.conv3());
+  if (fc1_1)
+    group(c0, f0.fc1(), f1.fc1());
+  else
+    group(c0, f0.fc1());
+  group(c0, f0.fchead(), f1.fchead());
+}
 
 // The online and target networks' forwards together: one grouped launch per layer
 // holding both nets' ops -- 6 launches instead of 12.
@@ -1116,7 +1253,11 @@ bool backward_layer(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int 
 // instead of running as an 18 us launch of its own.
 // Each GEMM writes its gradient/activation exactly as the per-layer form does
 // (same tiles, same summation order), so the two are bitwise identical.
-template <bool kAdam>
+// kHeadFrom: the launch of the head network's conv1 (3: conv1..conv3 and the fc1
+// slabs in launches 3..6; 4: conv1..conv3 in launches 4..6, its fc1 slabs left to
+// forward_fused).  Riders are numbered from launch `first`: rider i rides in launch
+// first + i.
+template <bool kAdam, int kHeadFrom = 3>
 void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int B,
                       const float* x, const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d,
                       const AdamHost& opt, int first = 0, int last = 7,
@@ -1164,7 +1305,9 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
       ws + o1, nz1, 32, Conv1::K + 1,
       GE::make(g->conv1_w, g->conv1_b, Conv1::K, p->conv1_w, p->conv1_b, opt, 1)};
   auto in = [&](int i) { return first <= i && i < last; };
-  auto rd = [&](int i) { return i < n_riders ? riders + i : nullptr; };   // rider of launch i
+  auto rd = [&](int i) {   // rider of launch i
+    return i >= first && i - first < n_riders ? riders + (i - first) : nullptr;
+  };
   if constexpr (kAdam) {
     {
       // The optimizer spread over the launches after each gradient is final (fc2 after
@@ -1175,7 +1318,8 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
       auto part = [&](float* w0, float* w1) {
         const ptrdiff_t off = w0 - o->var;
         const int64_t n = (int64_t)(w1 - w0);
-        const int nb = (int)std::max<int64_t>(1, ((n >> 2) + kGroupT - 1) / kGroupT);
+        const int64_t per = (int64_t)kGroupT * AdamOp::kU;
+        const int nb = (int)std::max<int64_t>(1, ((n >> 2) + per - 1) / per);
         return AdamOp{w0, g->conv1_w + (w0 - p->conv1_w), o->m + off, o->v + off, n, od, nb};
       };
       float* f0 = p->fc1_w;
@@ -1187,27 +1331,17 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
       if (in(1)) group_r(c, rd(1), dW_fc2, dX_fc1);
       if (in(2)) group_r(c, rd(2), dW_fc1, dX_c3, part(p->fc2_w, p->fc2_b + NO));
       if (head) {
-#if DQ_ORDER == 1
-        if (in(3)) group_r(c, rd(3), head->conv1(), dW_c3, dcol, part(f0, f1));
-        if (in(4)) group_r(c, rd(4), head->conv2(), sum_c3, dW_c2, da1, part(f1, f2));
-        if (in(5)) group_r(c, rd(5), head->conv3(), sum_c2, dW_c1, part(f2, f3));
-        if (in(6)) group_r(c, rd(6), head->fc1(), sum_c1, part(p->conv2_w, p->fc1_w));
-#elif DQ_ORDER == 2
-        if (in(3)) group_r(c, rd(3), head->conv1(), part(f0, f1), dW_c3, dcol);
-        if (in(4)) group_r(c, rd(4), head->conv2(), part(f1, f2), sum_c3, dW_c2, da1);
-        if (in(5)) group_r(c, rd(5), head->conv3(), part(f2, f3), sum_c2, dW_c1);
-        if (in(6)) group_r(c, rd(6), head->fc1(), part(p->conv2_w, p->fc1_w), sum_c1);
-#elif DQ_ORDER == 3
-        if (in(3)) group_r(c, rd(3), part(f0, f1), dW_c3, dcol, head->conv1());
-        if (in(4)) group_r(c, rd(4), part(f1, f2), sum_c3, dW_c2, da1, head->conv2());
-        if (in(5)) group_r(c, rd(5), part(f2, f3), sum_c2, dW_c1, head->conv3());
-        if (in(6)) group_r(c, rd(6), part(p->conv2_w, p->fc1_w), sum_c1, head->fc1());
-#else
-        if (in(3)) group_r(c, rd(3), dW_c3, dcol, part(f0, f1), head->conv1());
-        if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, da1, part(f1, f2), head->conv2());
-        if (in(5)) group_r(c, rd(5), sum_c2, dW_c1, part(f2, f3), head->conv3());
-        if (in(6)) group_r(c, rd(6), sum_c1, part(p->conv2_w, p->fc1_w), head->fc1());
-#endif
+if constexpr (kHeadFrom == 4) {
+          if (in(3)) group_r(c, rd(3), dW_c3, dcol, part(f0, f1));
+          if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, da1, part(f1, f2), head->conv1());
+          if (in(5)) group_r(c, rd(5), sum_c2, dW_c1, part(f2, f3), head->conv2());
+          if (in(6)) group_r(c, rd(6), sum_c1, part(p->conv2_w, p->fc1_w), head->conv3());
+        } else {
+          if (in(3)) group_r(c, rd(3), dW_c3, dcol, part(f0, f1), head->conv1());
+          if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, da1, part(f1, f2), head->conv2());
+          if (in(5)) group_r(c, rd(5), sum_c2, dW_c1, part(f2, f3), head->conv3());
+          if (in(6)) group_r(c, rd(6), sum_c1, part(p->conv2_w, p->fc1_w), head->fc1());
+        }
         return;
       }
       if (in(3)) group_r(c, rd(3), dW_c3, dcol, part(f0, f1));
@@ -1221,10 +1355,17 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
   if (in(1)) group_r(c, rd(1), dW_fc2, dX_fc1);
   if (in(2)) group_r(c, rd(2), dW_fc1, dX_c3);
   if (head) {
-    if (in(3)) group_r(c, rd(3), dW_c3, dcol, head->conv1());
-    if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, da1, head->conv2());
-    if (in(5)) group_r(c, rd(5), sum_c2, dW_c1, head->conv3());
-    if (in(6)) group_r(c, rd(6), sum_c1, head->fc1());
+    if constexpr (kHeadFrom == 4) {
+      if (in(3)) group_r(c, rd(3), dW_c3, dcol);
+      if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, da1, head->conv1());
+      if (in(5)) group_r(c, rd(5), sum_c2, dW_c1, head->conv2());
+      if (in(6)) group_r(c, rd(6), sum_c1, head->conv3());
+    } else {
+      if (in(3)) group_r(c, rd(3), dW_c3, dcol, head->conv1());
+      if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, da1, head->conv2());
+      if (in(5)) group_r(c, rd(5), sum_c2, dW_c1, head->conv3());
+      if (in(6)) group_r(c, rd(6), sum_c1, head->fc1());
+    }
     return;
   }
   if (in(3)) group_r(c, rd(3), dW_c3, dcol);
@@ -1307,6 +1448,22 @@ int dq_cnn_forward_with_tail(const dq_cnn_params* p0, const float* x0, dq_cnn_ac
   return DQ_OK;
 }
 
+int dq_cnn_forward_fused(const dq_cnn_params* p0, const float* x0, dq_cnn_acts* a0, float* ws0,
+                         const dq_cnn_params* p1, dq_cnn_acts* a1, float* ws1, int32_t batch,
+                         int32_t fc1_1, void* stream) {
+  DQ_CHECK_ARG(p0 && a0 && x0 && ws0 && p1 && a1 && ws1 && batch >= 1, "null argument");
+  DQ_CHECK_ARG(p0->in_channels == 4 && p1->in_channels == 4 && p0->n_out >= 1 && p1->n_out >= 1,
+               "the Nature CNN takes 84x84x4 NHWC input");
+  DQ_CHECK_ARG(ws0 != ws1, "the two networks need separate workspaces");
+  Ctx c0{(hipStream_t)stream, ws0, false, 0}, c1{(hipStream_t)stream, ws1, false, 0};
+  forward_fused(c0, c1, FwdOps{p0, x0, a0, ws0, batch}, FwdOps{p1, nullptr, a1, ws1, batch},
+                fc1_1 != 0);
+  DQ_CHECK_LAUNCH("dq_cnn_forward_fused");
+  return DQ_OK;
+}
+
+size_t dq_cnn_fc2_parts_offset(int32_t batch) { return FwdOps::part_offset(batch); }
+
 int dq_cnn_backward(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch, const float* x,
                     const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d, float* ws,
                     void* stream) {
@@ -1346,14 +1503,15 @@ int dq_cnn_backward_groups(const dq_cnn_params* p, const dq_cnn_params* g, int32
 int dq_cnn_backward_riders(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch,
                            const float* x, const dq_cnn_acts* a, const float* dout,
                            dq_cnn_acts* d, float* ws, const dq_rider* riders, int32_t n_riders,
-                           const dq_adam_args* opt, const dq_cnn_net* head, int32_t first,
-                           int32_t last, void* stream) {
+                           const dq_adam_args* opt, const dq_cnn_net* head, int32_t head_from,
+                           int32_t first, int32_t last, void* stream) {
   DQ_CHECK_ARG(p && g && a && d && x && dout && ws && batch >= 1, "null argument");
   DQ_CHECK_ARG(p->in_channels == 4 && p->n_out >= 1, "the Nature CNN takes 84x84x4 NHWC input");
   DQ_CHECK_ARG(0 <= n_riders && n_riders <= 7 && (riders || n_riders == 0),
                "at most one rider per grouped launch (7)");
   DQ_CHECK_ARG(0 <= first && first <= last && last <= 7, "groups must satisfy 0 <= first <= last <= 7");
-  DQ_CHECK_ARG(!opt || (first == 0 && last == 7), "the fused optimizer needs the whole backward");
+  DQ_CHECK_ARG(!opt || (first <= 1 && last == 7), "the fused optimizer needs the whole backward");
+  DQ_CHECK_ARG(head_from == 3 || head_from == 4, "head_from must be 3 or 4");
   RiderDesc r[7];
   for (int i = 0; i < n_riders; ++i) {
     memcpy(&r[i], &riders[i], sizeof(RiderDesc));
@@ -1367,14 +1525,23 @@ int dq_cnn_backward_riders(const dq_cnn_params* p, const dq_cnn_params* g, int32
     hf = FwdOps{head->p, head->x, head->a, head->ws, batch};
   }
   Ctx c{(hipStream_t)stream, ws, false, 0};
+  const FwdOps* hp = head ? &hf : nullptr;
   if (opt) {
     const int rc = check_adam(p, g, opt);
     if (rc != DQ_OK) return rc;
-    backward_grouped<true>(c, p, g, batch, x, a, dout, d, AdamHost{opt}, first, last, r, n_riders,
-                           head ? &hf : nullptr);
+    if (head_from == 4)
+      backward_grouped<true, 4>(c, p, g, batch, x, a, dout, d, AdamHost{opt}, first, last, r,
+                                n_riders, hp);
+    else
+      backward_grouped<true>(c, p, g, batch, x, a, dout, d, AdamHost{opt}, first, last, r,
+                             n_riders, hp);
   } else {
-    backward_grouped<false>(c, p, g, batch, x, a, dout, d, AdamHost{nullptr}, first, last, r,
-                            n_riders, head ? &hf : nullptr);
+    if (head_from == 4)
+      backward_grouped<false, 4>(c, p, g, batch, x, a, dout, d, AdamHost{nullptr}, first, last, r,
+                                 n_riders, hp);
+    else
+      backward_grouped<false>(c, p, g, batch, x, a, dout, d, AdamHost{nullptr}, first, last, r,
+                              n_riders, hp);
   }
   DQ_CHECK_LAUNCH("dq_cnn_backward_riders");
   return DQ_OK;
@@ -1410,7 +1577,11 @@ size_t dq_cnn_workspace_floats(int32_t batch, int32_t n_out) {
     }
   Ctx g{nullptr, nullptr, true, 0};
   backward_grouped<false>(g, &p, &p, batch, nullptr, &a, nullptr, &a, AdamHost{nullptr});
-  return g.need > need ? g.need : need;
+  need = g.need > need ? g.need : need;
+  Ctx f0{nullptr, nullptr, true, 0}, f1{nullptr, nullptr, true, 0};
+  forward_fused(f0, f1, FwdOps{&p, nullptr, &a, nullptr, batch}, FwdOps{&p, nullptr, &a, nullptr, batch},
+                true);
+  return f0.need > need ? f0.need : need;
 }
 
 }  // extern "C"

@@ -39,6 +39,34 @@ def c51_loss(online_logits, target_logits, actions, rewards, terminals, support,
   return out
 
 
+def c51_loss_fused(online, target, actions, rewards, terminals, support, cumulative_gamma,
+                   probs=None, out=None, logits_out=False):
+  """c51_loss on the HIP CNN's fc2 k-band partials (cnn.forward_fused) of the
+  online and target executors (``cnn.HipNatureCNN``); also writes the fc2 input
+  gradient into ``online.dacts['h']``, so ``online.backward(..., groups=(1, 7))``
+  can skip launch 0.  logits_out: also store both nets' logits in their
+  ``acts['out']``.  Returns dict(grad, loss, priorities)."""
+  from dopamine_amd import cnn
+  B, NO = online.B, online.n_out
+  N = int(support.numel())
+  A = NO // N
+  f32 = torch.float32
+  dev = support.device
+  if out is None:
+    out = dict(grad=torch.empty((B, A, N), dtype=f32, device=dev),
+               loss=torch.empty(B, dtype=f32, device=dev),
+               priorities=torch.empty(B, dtype=f32, device=dev))
+  po, pt = cnn.fc2_parts(online), cnn.fc2_parts(target)
+  _lib.call('dq_c51_loss_fused', p(po), online._p.fc2_b, p(pt), target._p.fc2_b, po.shape[0],
+            p(_c(actions, torch.int32)), p(_c(rewards, f32)), p(_c(terminals, torch.uint8)),
+            p(probs if probs is None else _c(probs, f32)), p(_c(support, f32)), B, A, N,
+            float(cumulative_gamma), p(out['grad']), p(out['loss']), p(out['priorities']),
+            online._p.fc2_w, p(online.acts['h']), p(online.dacts['h']), 512,
+            p(online.acts['out']) if logits_out else None,
+            p(target.acts['out']) if logits_out else None, _stream(support))
+  return out
+
+
 def dqn_huber_loss(online_q, target_q, actions, rewards, terminals, cumulative_gamma, out=None):
   """dqn_agent.py:283-322."""
   B, A = online_q.shape

@@ -171,6 +171,19 @@ int dq_c51_loss(const float* online_logits, const float* target_logits, const in
                 float cumulative_gamma, float* grad_logits, float* loss_out,
                 float* priorities_out, float* mean_loss_out, void* stream);
 
+/* dq_c51_loss on the CNN's fc2 k-band partials (dq_cnn_forward_fused): logits = the n_parts
+   partial slabs [n_parts][B][A*N] summed in order + bias (bitwise dq_cnn_forward's logits,
+   written to *_logits_out when non-NULL); with fc2_w set it also writes the fc2 input
+   gradient dh = (grad_logits . fc2_w) * (h > 0), (B, hidden), so the CNN backward can start
+   at its launch 1.  The mean-loss summary is not produced here. */
+int dq_c51_loss_fused(const float* online_parts, const float* online_bias,
+                      const float* target_parts, const float* target_bias, int32_t n_parts,
+                      const int32_t* actions, const float* rewards, const uint8_t* terminals,
+                      const float* probs, const float* support, int32_t batch,
+                      int32_t num_actions, int32_t num_atoms, float cumulative_gamma,
+                      float* grad_logits, float* loss_out, float* priorities_out,
+                      const float* fc2_w, const float* h, float* dh, int32_t hidden,
+                      float* online_logits_out, float* target_logits_out, void* stream);
 /* DQN Bellman max target + Huber(delta=1) (dqn_agent.py:283-322). */
 int dq_dqn_huber_loss(const float* online_q, const float* target_q, const int32_t* actions,
                       const float* rewards, const uint8_t* terminals, int32_t batch,
@@ -286,15 +299,32 @@ int dq_cnn_forward_with_tail(const dq_cnn_params* p0, const float* x0, dq_cnn_ac
    dq_replay_record_*) as extra blocks of grouped launch i, i < n_riders <= 7: a chain of
    riders runs in order, each after the launches before its own.  Riders must not touch
    x, a, dout, d, g or ws.  head (may be NULL): another network's forward head (e.g. the
-   target network on the next batch, which riders gathered) runs in launches 4..7.  Only
+   target network on the next batch, which riders gathered) runs in launches 4..7
+   (head_from = 3: conv1..conv3 + fc1 slabs) or 5..7 (head_from = 4: conv1..conv3, the fc1
+   slabs then run in dq_cnn_forward_fused).  Rider i rides in launch first + i.  Only
    launches [first, last) are issued (as dq_cnn_backward_groups; riders and head ops of
    other launches are skipped; opt needs [0, 7)).  CNN results are bitwise those of the
    separate calls. */
 int dq_cnn_backward_riders(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch,
                            const float* x, const dq_cnn_acts* a, const float* dout,
                            dq_cnn_acts* d, float* ws, const dq_rider* riders, int32_t n_riders,
-                           const dq_adam_args* opt, const dq_cnn_net* head, int32_t first,
-                           int32_t last, void* stream);
+                           const dq_adam_args* opt, const dq_cnn_net* head, int32_t head_from,
+                           int32_t first, int32_t last, void* stream);
+/* The Rainbow fast path (rainbow_agent.py:200-305 on the Nature CNN, one launch less in
+   the forward and one in the backward than dq_cnn_forward_with_tail + dq_c51_loss +
+   dq_cnn_backward_riders(first 0)):
+   dq_cnn_forward_fused: net 0 (online) conv1..fc1 and net 1's (target's) fc1 slabs (if fc1_1;
+   its conv1..conv3 ran earlier, e.g. as head_from = 4 riders of the previous backward), then
+   ONE launch that sums both nets' fc1 slabs (+ bias, ReLU -> a->h) and stores fc2's 16 k-band
+   partial products at ws + dq_cnn_fc2_parts_offset(batch) ([16][B][n_out]).  The logits are
+   never stored by the CNN: dq_c51_loss_fused sums the partials in band order and adds the
+   bias -- bit for bit the logits of dq_cnn_forward.  The backward then starts at launch 1
+   (dq_cnn_backward_riders with first = 1, riders numbered from it): dq_c51_loss_fused also
+   writes d h. */
+int dq_cnn_forward_fused(const dq_cnn_params* p0, const float* x0, dq_cnn_acts* a0, float* ws0,
+                         const dq_cnn_params* p1, dq_cnn_acts* a1, float* ws1, int32_t batch,
+                         int32_t fc1_1, void* stream);
+size_t dq_cnn_fc2_parts_offset(int32_t batch);
 /* one layer of the backward: layer 0..4 = fc2, fc1, conv3, conv2, conv1; part 1 = weight and
    bias gradient, part 0 = input gradient (not for conv1).  dW(L) depends only on dX(L-1),
    so the weight gradients may run on a second stream, each with its own ws. */

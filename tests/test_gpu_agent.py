@@ -166,13 +166,14 @@ def test_action_q_values_on_the_hip_cnn_match_torch(kind):
 def test_replay_riders_match_the_two_stream_schedule(kind, graph):
   """ride_replay (priority write-back -> sample -> gather as riders of the
   backward's grouped launches, one stream) draws the same batches and produces
-  the same parameters and sum tree, bit for bit, as the two-stream prefetch."""
+  the same parameters and sum tree, bit for bit, as the two-stream prefetch
+  (Rainbow's fused head off: it sums fc2's input gradient in another order)."""
   from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
   res = []
   for ride in (False, True):
     random.seed(7); np.random.seed(7); torch.manual_seed(7)
     if kind == 'rainbow':
-      a = _rainbow(use_hip_graph=graph, ride_replay=ride)
+      a = _rainbow(use_hip_graph=graph, ride_replay=ride, fused_head=False)
     else:
       a = DQNAgent(num_actions=6, replay_capacity=3000, batch_size=32, min_replay_history=100,
                    use_hip_graph=graph, ride_replay=ride)
@@ -192,3 +193,28 @@ def test_replay_riders_match_the_two_stream_schedule(kind, graph):
   np.testing.assert_array_equal(res[0][3], res[1][3])
   if kind == 'rainbow':
     np.testing.assert_array_equal(res[0][2], res[1][2])
+
+
+@pytest.mark.parametrize('graph', [False, True])
+def test_fused_head_matches_the_plain_schedule(graph):
+  """Rainbow's fused head (fc1 sum + fc2 partials in one launch, logits summed and
+  fc2's input gradient formed in the loss kernel, backward from launch 1, the
+  target head shifted one launch) draws the same batches and keeps parameters
+  and priorities within fp32 reordering of the plain ride schedule over 9 steps."""
+  res = []
+  for fused in (False, True):
+    random.seed(7); np.random.seed(7); torch.manual_seed(7)
+    a = _rainbow(use_hip_graph=graph, ride_replay=True, fused_head=fused)
+    assert a._fused() == fused
+    idx = []
+    for _ in range(9):
+      a._run_train_op()
+      idx.append(a._replay.transition['indices'].cpu().numpy().copy())
+    a._discard_prefetch()
+    a._replay.memory.sync_rng()
+    res.append((np.stack(idx), a.online_convnet.fp.flat.cpu().numpy().astype(np.float64),
+                a._replay.memory.sum_tree.nodes[-1].copy(), a._loss_out['loss'].cpu().numpy()))
+  np.testing.assert_array_equal(res[0][0], res[1][0])
+  np.testing.assert_allclose(res[1][1], res[0][1], rtol=0, atol=1e-6)
+  np.testing.assert_allclose(res[1][2], res[0][2], rtol=1e-4)
+  np.testing.assert_allclose(res[1][3], res[0][3], rtol=1e-4)

@@ -143,3 +143,54 @@ def test_forward_head_and_tail_equal_forward(B):
   yo, yt = forward_with_tail(ho, x, ht)
   torch.cuda.synchronize()
   assert torch.equal(yo, ref_o) and torch.equal(yt, ref_t)
+
+
+@pytest.mark.parametrize('B,A', [(32, 9), (7, 4)])
+def test_fused_forward_and_c51_equal_separate_path(B, A):
+  """The Rainbow fast path: forward_fused's fc2 k-band partials summed by
+  c51_loss_fused give bitwise dq_cnn_forward's logits (written out on request)
+  and therefore bitwise dq_c51_loss's gradient, loss and priorities; its fused fc2
+  input gradient equals the backward's dX_fc2 within fp32 reordering; the
+  backward from launch 1 then matches the full backward within tolerance."""
+  from dopamine_amd import ops
+  from dopamine_amd.agents.networks import RainbowNetwork
+  from dopamine_amd.cnn import HipNatureCNN, forward_fused
+  N = 51
+  on, tg = RainbowNetwork(A, device='cuda', seed=1), RainbowNetwork(A, device='cuda', seed=2)
+  with torch.no_grad():
+    for net in (on, tg):
+      for n, prm in net.fp.params.items():
+        if n.endswith('_b'):
+          prm.uniform_(-0.05, 0.1)
+  ho, ht = HipNatureCNN(on, B), HipNatureCNN(tg, B)
+  torch.manual_seed(3)
+  x, nx = torch.rand(B, 84, 84, 4, device='cuda'), torch.rand(B, 84, 84, 4, device='cuda')
+  act = torch.randint(0, A, (B,), device='cuda', dtype=torch.int32)
+  rew = torch.randn(B, device='cuda')
+  term = (torch.rand(B, device='cuda') < 0.2).to(torch.uint8)
+  probs = torch.rand(B, device='cuda') + 0.1
+  sup = torch.linspace(-10, 10, N, device='cuda')
+  ref_t = ht.forward(nx).clone()
+  ref_o = ho.forward(x).clone()
+  ref_h = ho.acts['h'].clone()
+  ref = ops.c51_loss(ref_o.view(B, A, N), ref_t.view(B, A, N), act, rew, term, sup, 0.970299,
+                     probs=probs)
+  ref = {k: v.clone() for k, v in ref.items()}
+  ho.backward(ref['grad'].view(B, -1))
+  ref_dh = ho.dacts['h'].clone()
+  ref_g = torch.cat([v.reshape(-1) for v in on.fp.grad_views]).clone()
+  # fused: the target's head (conv1..conv3) stays from its forward above; fc1 slabs redone
+  for t in (ho.acts['out'], ht.acts['out'], ho.acts['h'], ho.dacts['h']):
+    t.fill_(float('nan'))
+  forward_fused(ho, x, ht)
+  got = ops.c51_loss_fused(ho, ht, act, rew, term, sup, 0.970299, probs=probs, logits_out=True)
+  torch.cuda.synchronize()
+  assert torch.equal(ho.acts['h'], ref_h)
+  assert torch.equal(ho.acts['out'], ref_o) and torch.equal(ht.acts['out'], ref_t)
+  for k in ('grad', 'loss', 'priorities'):
+    assert torch.equal(got[k], ref[k]), k
+  _close(ho.dacts['h'], ref_dh, rtol=1e-5)
+  on.fp.grad.fill_(float('nan'))
+  ho.backward(got['grad'].view(B, -1), groups=(1, 7))
+  torch.cuda.synchronize()
+  _close(torch.cat([v.reshape(-1) for v in on.fp.grad_views]), ref_g, rtol=2e-5)
