@@ -169,12 +169,20 @@ def main():
   world = int(os.environ.get('WORLD_SIZE', '1'))
   rank = int(os.environ.get('RANK', '0'))
   local = int(os.environ.get('LOCAL_RANK', '0'))
+  # DQ_BENCH_REHEARSE=1: every rank on cuda:0 over gloo -- a one-GPU rehearsal of
+  # the N-rank code path (schedule, barriers, max-over-ranks timing), not a measurement
+  rehearse = os.environ.get('DQ_BENCH_REHEARSE') == '1'
+  if rehearse:
+    local = 0
   torch.cuda.set_device(local)
   dev = torch.device('cuda', local)
   pg = None
   if world > 1:
     os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-    dist.init_process_group('nccl', device_id=dev)
+    if rehearse:
+      dist.init_process_group('gloo')
+    else:
+      dist.init_process_group('nccl', device_id=dev)
     pg = dist.group.WORLD
   from dopamine_amd.agents.optimizers import AdamOptimizer
   from dopamine_amd.agents.rainbow.rainbow_agent import RainbowAgent
@@ -211,7 +219,7 @@ def main():
     dist.barrier()
   elapsed = time.perf_counter() - t0
   if pg is not None:
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed], dtype=torch.float64, device='cpu' if rehearse else dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
   agent._replay.memory.sync_rng()   # raises if the device latched a sampling error

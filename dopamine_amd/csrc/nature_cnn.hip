@@ -972,8 +972,12 @@ struct GroupArgs {
   int nblocks[sizeof...(Ops)];
 };
 
+#ifndef DQ_GROUP_WPE
+#define DQ_GROUP_WPE 1
+#endif
 template <int T, class... Ops>
-__global__ __launch_bounds__(T) void k_grouped(GroupArgs<Ops...> g, Ops... ops) {
+__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(DQ_GROUP_WPE)))
+void k_grouped(GroupArgs<Ops...> g, Ops... ops) {
   __shared__ __attribute__((aligned(16))) float smem[max_lds<Ops...>()];
   int blk = blockIdx.x, i = 0;
   ((dispatch(ops, g.nblocks[i++], blk, smem)) || ...);
