@@ -102,6 +102,7 @@ SIGNATURES = {
     'dq_dqn_huber_loss': [_P, _P, _P, _P, _P, _I32, _I32, _F, _P, _P, _P, _P],
     'dq_iqn_loss': [_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _F, _F, _P, _P, _P, _P],
     'dq_adam_tf1': [_P, _P, _P, _P, _P, _I32, _I64, _F, _F, _F, _F, _P],
+    'dq_adam_tf1_part': [_P, _P, _P, _P, _P, _I32, _I64, _F, _F, _F, _F, _I32, _P],
     'dq_adam_tf1_multi': [ctypes.POINTER(TensorList), _P, _I32, _F, _F, _F, _F, _P],
     'dq_rmsprop_tf1': [_P, _P, _P, _P, _P, _I64, _F, _F, _F, _F, _I32, _P],
     'dq_sync_copy': [_P, _P, _I64, _P],

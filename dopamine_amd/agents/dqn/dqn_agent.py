@@ -440,19 +440,32 @@ class DQNAgent(object):
     o = fp.offsets['fc1_w'][0]
     return fp.grad[o:], fp.grad[:o]           # fc1 + fc2 (final after the head), convs
 
-  def _split_step(self, head, tail, opt):
+  def _split_step(self, head, tail, opt, k=0):
+    """head | tail on the main stream with the fc bucket's all-reduce on the comm
+    stream beside the tail; with TF1 Adam the fc parameters' update follows their
+    all-reduce on the comm stream (hidden under the conv bucket's all-reduce) and
+    only the conv parameters' update (which advances the beta powers) is left
+    after the join: same arithmetic, split in two launches (dq_adam_tf1_part)."""
     main = torch.cuda.current_stream(self._device)
     fc, conv = self._grad_buckets()
+    split_opt = isinstance(self._opt, ops.TF1Adam)
+    grad = self.online_convnet.fp.grad
+    o = grad.numel() - fc.numel()
     head()
     ev = torch.cuda.Event()
     ev.record(main)
     self._comm.wait_event(ev)
     with torch.cuda.stream(self._comm):
       parallel.allreduce_mean_(fc, self._pg)
+      if split_opt:
+        self._opt.step_part(grad, o, grad.numel(), slot=k, bump=False)
     tail()
     parallel.allreduce_mean_(conv, self._pg)
     main.wait_stream(self._comm)
-    opt()
+    if split_opt:
+      self._opt.step_part(grad, 0, o, slot=k, bump=True)
+    else:
+      opt()
 
   def _post_loss(self, t):
     """Work that needs the loss but not the gradient (PER priority write-back)."""
@@ -503,11 +516,11 @@ class DQNAgent(object):
     graphs = self._graph_sets.get(pipe)
     if self._split_allreduce():
       if graphs is not None:
-        self._split_step(*[g.replay for g in graphs[0][k]])
+        self._split_step(*[g.replay for g in graphs[0][k]], k=k)
       else:
         self._split_step(lambda: self._grad_step_head(c, k, pipe),
                          lambda: self._grad_step_tail(c, k, pipe),
-                         lambda: self._device_opt_step(k))
+                         lambda: self._device_opt_step(k), k=k)
         self._eager_steps[pipe] += 1
     elif graphs is not None:
       graphs[0][k].replay()

@@ -385,6 +385,20 @@ __device__ __forceinline__ void adam_range(float* __restrict__ var, const float*
     adam1(var[i], grad[i], m[i], v[i], alpha, omb1, omb2, eps);
 }
 
+// one part of a step split over several launches: only the part with bump != 0
+// advances the beta powers (every part reads this step's slot)
+__global__ __launch_bounds__(256) void k_adam_part(float* __restrict__ var,
+                                                   const float* __restrict__ grad,
+                                                   float* __restrict__ m, float* __restrict__ v,
+                                                   float* state, int slot, int64_t n, float lr,
+                                                   float b1, float b2, float eps, int bump) {
+  if (bump && blockIdx.x == 0 && threadIdx.x == 0) adam_bump(state, slot, b1, b2);
+  const float alpha = adam_alpha_of(state, slot, lr);
+  const float omb1 = __fsub_rn(1.0f, b1), omb2 = __fsub_rn(1.0f, b2);
+  adam_range(var, grad, m, v, n, (int64_t)blockIdx.x * blockDim.x + threadIdx.x,
+             (int64_t)gridDim.x * blockDim.x, alpha, omb1, omb2, eps);
+}
+
 __global__ __launch_bounds__(256) void k_adam(float* __restrict__ var, const float* __restrict__ grad,
                                               float* __restrict__ m, float* __restrict__ v,
                                               float* state, int slot, int64_t n, float lr,
@@ -560,6 +574,18 @@ int dq_adam_tf1(float* var, const float* grad, float* m, float* v, float* state,
   hipLaunchKernelGGL(k_adam, dim3(elementwise_grid(n)), dim3(256), 0, (hipStream_t)stream, var,
                      grad, m, v, state, slot, n, lr, beta1, beta2, eps);
   DQ_CHECK_LAUNCH("k_adam");
+  return DQ_OK;
+}
+
+int dq_adam_tf1_part(float* var, const float* grad, float* m, float* v, float* state,
+                     int32_t slot, int64_t n, float lr, float beta1, float beta2, float eps,
+                     int32_t bump, void* stream) {
+  DQ_CHECK_ARG(var && grad && m && v && state && n >= 0 && (slot == 0 || slot == 1), "bad arguments");
+  DQ_CHECK_ARG(((uintptr_t)var | (uintptr_t)grad | (uintptr_t)m | (uintptr_t)v) % 16 == 0,
+               "adam buffers must be 16-byte aligned");
+  hipLaunchKernelGGL(k_adam_part, dim3(elementwise_grid(n)), dim3(256), 0, (hipStream_t)stream,
+                     var, grad, m, v, state, slot, n, lr, beta1, beta2, eps, bump);
+  DQ_CHECK_LAUNCH("k_adam_part");
   return DQ_OK;
 }
 

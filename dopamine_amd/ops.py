@@ -129,6 +129,15 @@ class TF1Adam(object):
               p(self.state), self._slot(slot), self.params.numel(), self.lr, self.b1, self.b2,
               self.eps, _stream(self.params))
 
+  def step_part(self, grad, lo, hi, slot, bump):
+    """Adam on the flat range [lo, hi) only (grad: the whole flat gradient).  One
+    step may be split into parts; exactly one of them passes bump=True."""
+    assert 0 <= lo <= hi <= self.params.numel() and lo % 4 == 0
+    f = lambda t: t.data_ptr() + 4 * lo
+    _lib.call('dq_adam_tf1_part', f(self.params), f(_c(grad, torch.float32)), f(self.m), f(self.v),
+              p(self.state), int(slot), hi - lo, self.lr, self.b1, self.b2, self.eps, int(bool(bump)),
+              _stream(self.params))
+
   def step_multi(self, grads, slot=None):
     """Update from per-parameter gradient tensors (memory order = the parameter
     slices ``segments`` of the flat buffer) in one launch."""

@@ -208,6 +208,12 @@ int dq_adam_tf1(float* var, const float* grad, float* m, float* v, float* state,
 /* The same update over up to DQ_MAX_TENSORS separately allocated tensors in ONE
  * launch (e.g. autograd's per-parameter gradients; no flat-gradient copy). */
 #define DQ_MAX_TENSORS 16
+/* dq_adam_tf1 over one part [var, var + n) of the parameters: a step may be split into
+   parts (e.g. each all-reduce bucket as soon as it lands); every part reads the beta powers
+   of slot `slot`, and exactly one part per step passes bump = 1 to advance them. */
+int dq_adam_tf1_part(float* var, const float* grad, float* m, float* v, float* state,
+                     int32_t slot, int64_t n, float lr, float beta1, float beta2, float eps,
+                     int32_t bump, void* stream);
 typedef struct dq_tensor_list {
   int32_t count;
   int32_t pad_;
