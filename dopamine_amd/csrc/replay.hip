@@ -367,6 +367,13 @@ int dq_replay_read_meta(dq_replay* h, dq_replay_meta* out, void* stream) {
   return DQ_OK;
 }
 
+int dq_replay_read_meta_async(dq_replay* h, dq_replay_meta* out, void* stream) {
+  DQ_CHECK_ARG(h && out, "null argument");
+  DQ_CHECK_HIP(hipMemcpyAsync(out, h->st.meta, sizeof(dq_replay_meta), hipMemcpyDeviceToHost,
+                              (hipStream_t)stream));
+  return DQ_OK;
+}
+
 static int record(dq_replay* h, RiderDesc& r, dq_rider* out) {
   DQ_CHECK_ARG(out, "null rider");
   r.v = h->view();

@@ -16,6 +16,7 @@ synchronisation point the host stream is advanced by exactly the number of
 words the device consumed, so the Python/numpy RNG state is identical to the
 reference's after the same calls -- including the data-dependent retries.
 """
+import ctypes
 import random as _random
 
 import numpy as np
@@ -53,6 +54,15 @@ class RNGTape:
     self._len = 0
     self._budget = 0               # words guaranteed left (host-side worst-case accounting)
     self._host_synced = False      # last invalidation came from a host-side sync
+    # Budget probe: the worst case (B + max_attempts retries per draw) is ~30x what a
+    # PER step really uses, so instead of syncing when the worst-case budget runs low,
+    # an async read of the device's tape position (pinned, stream-ordered, polled by
+    # event) re-bases the budget on the words actually consumed.
+    self._reserved = 0             # worst-case words reserved since the rebuild
+    self._probe = None             # (event, words reserved before the probe point)
+    self._probe_buf = None
+    if self.words.is_cuda:
+      self._probe_buf = torch.zeros(ctypes.sizeof(_lib.Meta), dtype=torch.uint8).pin_memory()
 
   @property
   def valid(self):
@@ -60,6 +70,7 @@ class RNGTape:
 
   def invalidate(self):
     self._base = None
+    self._probe = None
 
   def rebuild(self, nwords, stream_handle):
     """Draw the next ``nwords`` words of the host stream onto the device tape.
@@ -76,15 +87,36 @@ class RNGTape:
     self._base = full
     self._len = nwords
     self._budget = nwords
+    self._reserved = 0
+    self._probe = None
     _lib.call('dq_replay_set_tape', self._replay._h, nwords, stream_handle)
     # keep the pinned staging buffer alive until the copy is done
     self._staging = host
 
+  def _poll(self):
+    ev, before = self._probe
+    if not ev.query():
+      return
+    self._probe = None
+    pos = int(_lib.Meta.from_address(self._probe_buf.data_ptr()).tape_pos)
+    self._budget = max(self._budget, self._len - pos - (self._reserved - before))
+
   def reserve(self, worst_case, stream_handle):
     """Ensure ``worst_case`` more words are available without synchronising
     unless the tape might run dry; returns True if it had to sync."""
+    if self.valid and self._probe is not None:
+      self._poll()
     if self.valid and self._budget >= worst_case:
       self._budget -= worst_case
+      self._reserved += worst_case
+      if (self._probe is None and self._probe_buf is not None and
+          self._budget < self._len // 2):
+        # enqueued before this reservation's work: it sees the earlier steps' use
+        _lib.call('dq_replay_read_meta_async', self._replay._h, self._probe_buf.data_ptr(),
+                  stream_handle)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.words.device))
+        self._probe = (ev, self._reserved - worst_case)
       return False
     synced = False
     if self.valid:
@@ -101,6 +133,7 @@ class RNGTape:
     self._host_synced = False
     self.rebuild(max(worst_case, min(size, self.capacity)), stream_handle)
     self._budget -= worst_case
+    self._reserved = worst_case
     return synced
 
   def sync(self, stream_handle, meta=None):
@@ -124,6 +157,7 @@ class RNGTape:
     _set_stream(self.stream, base, np.asarray(st[1], np.uint32), int(st[2]))
     self._base = None
     self._host_synced = True
+    self._probe = None
     return meta
 
 

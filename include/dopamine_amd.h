@@ -137,6 +137,9 @@ int dq_replay_set_tape(dq_replay* h, int64_t len, void* stream);
 int dq_replay_rewind_last_sample(dq_replay* h, void* stream);
 /* synchronous: copies the control block to host memory. */
 int dq_replay_read_meta(dq_replay* h, dq_replay_meta* out, void* stream);
+/* the same copy, stream-ordered and NOT waited for: `out` must be pinned host memory and is
+   valid once the stream reaches this point (e.g. an event recorded after the call). */
+int dq_replay_read_meta_async(dq_replay* h, dq_replay_meta* out, void* stream);
 
 /* Recorded replay operations ("riders").  Instead of launching, these fill an
  * opaque descriptor with exactly the work the matching call above would launch

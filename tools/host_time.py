@@ -62,6 +62,23 @@ def main():
   torch.cuda.synchronize()
   t2 = time.perf_counter()
   print('replay_only %7.1f us (host %7.1f us)' % ((t2 - t0) / K * 1e6, (t1 - t0) / K * 1e6))
+  # the same steps with S consecutive steps captured in ONE graph: the graph
+  # boundary's cost per step (what a multi-step learner graph would save)
+  for S in (2, 4, 8):
+    gs = torch.cuda.CUDAGraph()
+    torch.cuda.synchronize()
+    with torch.cuda.graph(gs, pool=agent._graph_pool):
+      for j in range(S):
+        agent._grad_step(j % 2, j % 2, True)
+        agent._device_opt_step(j % 2)
+    torch.cuda.synchronize()
+    n = K // S
+    t0 = time.perf_counter()
+    for _ in range(n):
+      gs.replay()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    print('multi_step  S=%d %7.1f us per step' % (S, (t2 - t0) / (n * S) * 1e6))
 
 
 if __name__ == '__main__':

@@ -11,14 +11,15 @@ def name_of(n):
   if n.startswith('k_grouped'):
     ops = []
     for m in re.finditer(r'(GemmOp<(\d+), (\d+), (\d+), (\w+)(?:<[^>]*(?:<[^>]*>)?[^>]*>)?, (\w+)'
-                         r'(?:<[^>]*(?:<[^>]*>)?[^>]*>)?, (\w+)|ReduceOp<(\w+)>|Col2imOp)', n):
+                         r'(?:<[^>]*(?:<[^>]*>)?[^>]*>)?, (\w+)|ReduceOp<(\w+)|Col2imOp|AdamOp|RiderOp'
+                         r'|FcHeadOp)', n):
       if m.group(1).startswith('GemmOp'):
         ops.append('G%s%s%s:%s/%s/%s' % (m.group(2), m.group(3), m.group(4), m.group(5),
                                           m.group(6), m.group(7)))
       elif m.group(8):
         ops.append('Sum:' + m.group(8))
       else:
-        ops.append('Col2im')
+        ops.append(m.group(1).replace('Op', ''))
     # the kernel name repeats the op list in its parameter types: keep the first half
     ops = ops[:max(1, len(ops) // 2)]
     return 'group[' + ' | '.join(ops) + ']'
