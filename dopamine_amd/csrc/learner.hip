@@ -90,7 +90,6 @@ struct C51Extra {
 // instead of N -- before the softmax cross-entropy of the chosen online logits.
 // The fused path (x.w2) also forms d h from the chosen action's N logit
 // gradients; its W2 rows are fetched into LDS at the start, under the chain.
-constexpr int kC51PreMax = 48;       // W2 prefetch registers per thread (fused d h)
 
 template <class LS>
 __global__ __launch_bounds__(1024) void k_c51(C51Args a, LS ol, LS tl, C51Extra x) {
@@ -101,7 +100,7 @@ __global__ __launch_bounds__(1024) void k_c51(C51Args a, LS ol, LS tl, C51Extra 
   float* s_tz = s_q + A;             // [N]    clipped Bellman support
   float* s_g = s_tz + N;             // [N]    the chosen action's logit gradient
   float* s_c = s_g + N;              // [N][64] projection terms c(i, j) p_j
-  float* s_w = s_c + N * kWave;      // [N][H] the chosen action's fc2 rows (fused d h)
+  float* s_w = smem + (A * N + A + 2 * N + N * kWave + 3) / 4 * 4;   // [N][H] fc2 rows, 16-B aligned
   __shared__ float s_red[16];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = T >> 6;
   const bool on = lane < N;
@@ -116,15 +115,20 @@ __global__ __launch_bounds__(1024) void k_c51(C51Args a, LS ol, LS tl, C51Extra 
     const int act = wave + r * nw;
     xv[r] = (act < A && on) ? tl.get(((int64_t)b * A + act) * N + lane) : ninf;
   }
-  // fused d h: this sample's W2 rows (N x H) and h mask, loaded now, stored after the softmax
-  const bool pre = x.w2 && N * x.H <= kC51PreMax * T;
-  const float* wr = x.w2 ? x.w2 + (int64_t)ab * N * x.H : nullptr;
-  float wv[kC51PreMax];
+  // fused d h: this sample's N contiguous W2 rows (N x H floats) stream into LDS by
+  // LDS-DMA (global_load_lds, 1 KB per wave instruction, no registers) issued here,
+  // with the target rows' loads, so they land under the whole loss chain
+  const bool pre = x.w2 != nullptr;
+  const float* wr = pre ? x.w2 + (int64_t)ab * N * x.H : nullptr;
   if (pre) {
-#pragma unroll
-    for (int u = 0; u < kC51PreMax; ++u) {
-      const int e = threadIdx.x + u * T;
-      wv[u] = e < N * x.H ? wr[e] : 0.0f;
+    const int bytes = N * x.H * 4, nq = (bytes + 1023) >> 10;
+    const char* src = reinterpret_cast<const char*>(wr);
+    for (int q = wave; q < nq; q += nw) {
+      const int off = min(q * 1024 + lane * 16, bytes - 16);   // the tail re-reads in-bounds bytes
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + off),
+                                       (__attribute__((address_space(3))) void*)(
+                                           reinterpret_cast<char*>(s_w) + q * 1024),
+                                       16, 0, 0);
     }
   }
   const float hv = (x.w2 && (int)threadIdx.x < x.H) ? x.h[(int64_t)b * x.H + threadIdx.x] : 0.0f;
@@ -146,13 +150,6 @@ __global__ __launch_bounds__(1024) void k_c51(C51Args a, LS ol, LS tl, C51Extra 
       const int64_t i = ((int64_t)b * A + act) * N + lane;
       if (on) x.ol_out[i] = act == ab && wave == 0 ? y : ol.get(i);
     }
-  if (pre) {
-#pragma unroll
-    for (int u = 0; u < kC51PreMax; ++u) {
-      const int e = threadIdx.x + u * T;
-      if (e < N * x.H) s_w[e] = wv[u];
-    }
-  }
   __syncthreads();            // s_p, s_q (and s_w) complete
   const float w = per_weight(a.probs, a.B, b, s_red);
   const float gscale = __fmul_rn(w, __fdiv_rn(1.0f, (float)a.B));
@@ -203,25 +200,22 @@ __global__ __launch_bounds__(1024) void k_c51(C51Args a, LS ol, LS tl, C51Extra 
     }
   }
   if (!x.w2) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's LDS-DMA has landed
   __syncthreads();
   // d h[b][j] = (h[b][j] > 0) * sum_i g_i W2[ab*N + i][j], i in order
   for (int j = threadIdx.x; j < x.H; j += T) {
     const float m = j == (int)threadIdx.x ? hv : x.h[(int64_t)b * x.H + j];
     float acc = 0.0f;
-    if (pre) {
-      for (int i = 0; i < N; ++i) acc = __fadd_rn(acc, __fmul_rn(s_g[i], s_w[i * x.H + j]));
-    } else {
-      for (int i = 0; i < N; ++i) acc = __fadd_rn(acc, __fmul_rn(s_g[i], wr[(int64_t)i * x.H + j]));
-    }
+    for (int i = 0; i < N; ++i) acc = __fadd_rn(acc, __fmul_rn(s_g[i], s_w[i * x.H + j]));
     x.dh[(int64_t)b * x.H + j] = m > 0.0f ? acc : 0.0f;
   }
 }
 
 // dynamic LDS of k_c51 (bytes), with the fused path's W2 rows when they fit the prefetch
-static size_t c51_lds(int A, int N, int T, int H) {
-  size_t f = (size_t)A * N + A + 2 * N + (size_t)N * kWave;
-  if (H > 0 && N * H <= kC51PreMax * T) f += (size_t)N * H;
-  return f * sizeof(float);
+static size_t c51_lds(int A, int N, int H) {
+  // s_w must be 16-byte aligned for the LDS-DMA: round the head up to 4 floats
+  const size_t head = ((size_t)A * N + A + 2 * N + (size_t)N * kWave + 3) / 4 * 4;
+  return (head + (size_t)N * H) * sizeof(float);
 }
 
 // mean(w * loss) for summaries (rb:298-301); launched only when requested.
@@ -485,7 +479,7 @@ int dq_c51_loss(const float* online_logits, const float* target_logits, const in
   DQ_CHECK_ARG(!mean_loss_out || loss_out, "mean_loss_out needs loss_out");
   DQ_CHECK_ARG(num_actions <= 64, "num_actions must be <= 64");
   const int waves = num_actions < 16 ? num_actions : 16;
-  const size_t shm = c51_lds(num_actions, num_atoms, 64 * waves, 0);
+  const size_t shm = c51_lds(num_actions, num_atoms, 0);
   hipLaunchKernelGGL(k_c51<LogitsDirect>, dim3(batch), dim3(64 * waves), shm, (hipStream_t)stream,
                      a, LogitsDirect{online_logits}, LogitsDirect{target_logits}, C51Extra{});
   DQ_CHECK_LAUNCH("k_c51");
@@ -518,7 +512,7 @@ int dq_c51_loss_fused(const float* online_parts, const float* online_bias,
   const int64_t stride = (int64_t)batch * NO;
   DQ_CHECK_ARG(num_actions <= 64, "num_actions must be <= 64");
   const int waves = num_actions < 16 ? num_actions : 16;
-  const size_t shm = c51_lds(num_actions, num_atoms, 64 * waves, fc2_w ? hidden : 0);
+  const size_t shm = c51_lds(num_actions, num_atoms, fc2_w ? hidden : 0);
   hipLaunchKernelGGL(k_c51<LogitsParts>, dim3(batch), dim3(64 * waves), shm, (hipStream_t)stream,
                      a, LogitsParts{online_parts, online_bias, stride, n_parts, NO},
                      LogitsParts{target_parts, target_bias, stride, n_parts, NO},

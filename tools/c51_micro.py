@@ -50,6 +50,15 @@ def main():
       yo.view(B, A, N), yt.view(B, A, N), act, rew, term, sup, 0.97, probs=probs, out=out)))
   print('c51 fused + dh          %7.2f us' % timed(lambda: ops.c51_loss_fused(
       ho, ht, act, rew, term, sup, 0.97, probs=probs, out=out)))
+  from dopamine_amd import _lib, cnn
+  from dopamine_amd.ops import p as ptr, _stream
+  po, pt = cnn.fc2_parts(ho), cnn.fc2_parts(ht)
+
+  def nodh():
+    _lib.call('dq_c51_loss_fused', ptr(po), ho._p.fc2_b, ptr(pt), ht._p.fc2_b, 16, ptr(act), ptr(rew),
+              ptr(term), ptr(probs), ptr(sup), B, A, N, 0.97, ptr(out['grad']), ptr(out['loss']),
+              ptr(out['priorities']), None, None, None, 512, None, None, _stream(sup))
+  print('c51 fused, no dh        %7.2f us' % timed(nodh))
   print('forward_fused           %7.2f us' % timed(lambda: forward_fused(ho, x, ht)))
   print('forward_fused (no tfc1) %7.2f us' % timed(lambda: forward_fused(ho, x, ht, fc1_b=False)))
   print('forward                 %7.2f us' % timed(lambda: ho.forward(x)))
