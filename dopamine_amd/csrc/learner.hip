@@ -27,24 +27,6 @@ struct C51Args {
   float* mean_out;
 };
 
-// PER importance weight of sample b, normalised by the batch max (rb:277-280).
-// Every block recomputes the max over the B probabilities (B tiny loads) so no
-// cross-block reduction is needed.
-__device__ float per_weight(const float* probs, int B, int b, float* s_red) {
-  if (!probs) return 1.0f;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  float m = 0.0f;
-  for (int i = threadIdx.x; i < B; i += blockDim.x)
-    m = fmaxf(m, __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(probs[i], 1e-10f))));
-  m = wave_max(m);
-  if (lane == 0) s_red[wave] = m;
-  __syncthreads();
-  m = s_red[0];
-  for (int i = 1; i < nw; ++i) m = fmaxf(m, s_red[i]);
-  const float w = __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(probs[b], 1e-10f)));
-  return __fdiv_rn(w, m);
-}
-
 // Logit sources: stored logits, or (the fused Rainbow path) fc2's 16 k-band
 // partial products summed in band order plus the bias -- exactly the reduction
 // order of the CNN's fc2 tile, so the logits are bitwise dq_cnn_forward's.
@@ -102,11 +84,19 @@ __global__ __launch_bounds__(1024) void k_c51(C51Args a, LS ol, LS tl, C51Extra 
   float* s_c = s_g + N;              // [N][64] projection terms c(i, j) p_j
   float* s_w = smem + (A * N + A + 2 * N + N * kWave + 3) / 4 * 4;   // [N][H] fc2 rows, 16-B aligned
   __shared__ float s_red[16];
+  __shared__ float s_z[kWave];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = T >> 6;
   const bool on = lane < N;
   const float ninf = -__builtin_inff();
+  // every ordinary global load of the chain is issued here, before any LDS-DMA
+  // (hipcc drains vmcnt to 0 at the first use of a plain load issued behind one)
   const float z = on ? a.support[lane] : 0.0f;
   const int ab = a.act[b];
+  const float rew_b = a.rew[b], term_b = (float)a.term[b];
+  const float vmin = a.support[0], vmax = a.support[N - 1], z1 = a.support[1];
+  const float pr_t = (a.probs && (int)threadIdx.x < a.B) ? a.probs[threadIdx.x] : 0.0f;
+  const float pr_b = a.probs ? a.probs[b] : 0.0f;
+  const float hv = (x.w2 && (int)threadIdx.x < x.H) ? x.h[(int64_t)b * x.H + threadIdx.x] : 0.0f;
   // the chosen online logit row, issued with the target rows (wave 0 uses it last)
   const float y = (wave == 0 && on) ? ol.get(((int64_t)b * A + ab) * N + lane) : ninf;
   float xv[4];
@@ -115,23 +105,7 @@ __global__ __launch_bounds__(1024) void k_c51(C51Args a, LS ol, LS tl, C51Extra 
     const int act = wave + r * nw;
     xv[r] = (act < A && on) ? tl.get(((int64_t)b * A + act) * N + lane) : ninf;
   }
-  // fused d h: this sample's N contiguous W2 rows (N x H floats) stream into LDS by
-  // LDS-DMA (global_load_lds, 1 KB per wave instruction, no registers) issued here,
-  // with the target rows' loads, so they land under the whole loss chain
-  const bool pre = x.w2 != nullptr;
-  const float* wr = pre ? x.w2 + (int64_t)ab * N * x.H : nullptr;
-  if (pre) {
-    const int bytes = N * x.H * 4, nq = (bytes + 1023) >> 10;
-    const char* src = reinterpret_cast<const char*>(wr);
-    for (int q = wave; q < nq; q += nw) {
-      const int off = min(q * 1024 + lane * 16, bytes - 16);   // the tail re-reads in-bounds bytes
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + off),
-                                       (__attribute__((address_space(3))) void*)(
-                                           reinterpret_cast<char*>(s_w) + q * 1024),
-                                       16, 0, 0);
-    }
-  }
-  const float hv = (x.w2 && (int)threadIdx.x < x.H) ? x.h[(int64_t)b * x.H + threadIdx.x] : 0.0f;
+  if (wave == 0) s_z[lane] = z;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int act = wave + r * nw;
@@ -150,8 +124,34 @@ __global__ __launch_bounds__(1024) void k_c51(C51Args a, LS ol, LS tl, C51Extra 
       const int64_t i = ((int64_t)b * A + act) * N + lane;
       if (on) x.ol_out[i] = act == ab && wave == 0 ? y : ol.get(i);
     }
-  __syncthreads();            // s_p, s_q (and s_w) complete
-  const float w = per_weight(a.probs, a.B, b, s_red);
+  // fused d h: this sample's N contiguous W2 rows (N x H floats) stream into LDS by
+  // LDS-DMA (global_load_lds, 1 KB per wave instruction, no registers), landing under
+  // the rest of the loss chain
+  if (x.w2) {
+    const int bytes = N * x.H * 4, nq = (bytes + 1023) >> 10;
+    const char* src = reinterpret_cast<const char*>(x.w2 + (int64_t)ab * N * x.H);
+    for (int q = wave; q < nq; q += nw) {
+      const int off = min(q * 1024 + lane * 16, bytes - 16);   // the tail re-reads in-bounds bytes
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + off),
+                                       (__attribute__((address_space(3))) void*)(
+                                           reinterpret_cast<char*>(s_w) + q * 1024),
+                                       16, 0, 0);
+    }
+  }
+  __syncthreads();            // s_p, s_q, s_z complete
+  // PER importance weight (rb:277-280) from the probabilities loaded above
+  float w = 1.0f;
+  if (a.probs) {
+    float m = (int)threadIdx.x < a.B ? __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(pr_t, 1e-10f))) : 0.0f;
+    for (int i = threadIdx.x + T; i < a.B; i += T)
+      m = fmaxf(m, __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(a.probs[i], 1e-10f))));
+    m = wave_max(m);
+    if (lane == 0) s_red[wave] = m;
+    __syncthreads();
+    m = s_red[0];
+    for (int i = 1; i < nw; ++i) m = fmaxf(m, s_red[i]);
+    w = __fdiv_rn(__fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(pr_b, 1e-10f))), m);
+  }
   const float gscale = __fmul_rn(w, __fdiv_rn(1.0f, (float)a.B));
   for (int act = wave; act < A; act += nw) {
     if (act == ab) continue;
@@ -165,14 +165,13 @@ __global__ __launch_bounds__(1024) void k_c51(C51Args a, LS ol, LS tl, C51Extra 
       best = s_q[act];
       astar = act;
     }
-  const float vmin = a.support[0], vmax = a.support[N - 1];
-  const float dz = __fsub_rn(a.support[1], a.support[0]);
-  const float gt = __fmul_rn(a.cg, __fsub_rn(1.0f, (float)a.term[b]));
+  const float dz = __fsub_rn(z1, vmin);
+  const float gt = __fmul_rn(a.cg, __fsub_rn(1.0f, term_b));
   const float* pst = s_p + astar * N;
   // projection terms: wave w takes source atoms j = w, w + nw, ...; lane = target atom i
   for (int j = wave; j < N; j += nw) {
-    const float zj = a.support[j];
-    const float tzj = fminf(fmaxf(__fadd_rn(a.rew[b], __fmul_rn(gt, zj)), vmin), vmax);
+    const float zj = s_z[j];
+    const float tzj = fminf(fmaxf(__fadd_rn(rew_b, __fmul_rn(gt, zj)), vmin), vmax);
     if (on) {
       float c = __fsub_rn(1.0f, __fdiv_rn(fabsf(__fsub_rn(tzj, z)), dz));
       c = fminf(fmaxf(c, 0.0f), 1.0f);
