@@ -390,6 +390,9 @@ __device__ __forceinline__ void group_coord(int g, int& rr, int& kk) {
 // in wave order (deterministic), and handed to the epilogue with consecutive
 // threads on consecutive columns.
 // compile with -DDQ_SHARED_STAGING=1 for the block-shared operand staging (A/B builds)
+#ifndef DQ_LATE_FETCH
+#define DQ_LATE_FETCH 1
+#endif
 #ifndef DQ_SHARED_STAGING
 #define DQ_SHARED_STAGING 0
 #endif
@@ -568,20 +571,14 @@ __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& 
         stage_h(h);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         __builtin_amdgcn_wave_barrier();
+#if !DQ_LATE_FETCH
         if (h == 0) fetch_h(k0, 1);
         else if (k0 + BKT < kend) fetch_h(k0 + BKT, 0);
-
+#endif
         if (live) {
           float av[8], bv[8];
-#ifdef DQ_ABLATE_STAGE   // timing experiments only: operands straight from the fetched registers
-          for (int s = 0; s < 8; ++s) {
-            av[s] = (&pa4[s & 3].x)[s >> 2];
-            bv[s] = (&pb4[s & 3].x)[s >> 2];
-          }
-#else
           operands(Aw, AL::kFast, av);
           operands(Bw, BL::kFast, bv);
-#endif
 #ifdef DQ_ABLATE_MFMA    // timing experiments only: no matrix-core chain
           for (int s = 0; s < 8; ++s) acc[s] += av[s] * bv[s];
 #else
@@ -590,6 +587,10 @@ __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& 
             acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc, 0, 0, 0);
 #endif
         }
+#if DQ_LATE_FETCH
+        if (h == 0) fetch_h(k0, 1);
+        else if (k0 + BKT < kend) fetch_h(k0 + BKT, 0);
+#endif
       }
     }
     __syncthreads();                 // staging windows are reused as reduction scratch
@@ -986,7 +987,7 @@ struct GroupArgs {
 };
 
 #ifndef DQ_GROUP_WPE
-#define DQ_GROUP_WPE 1
+#define DQ_GROUP_WPE 8
 #endif
 template <int T, class... Ops>
 __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(DQ_GROUP_WPE)))
