@@ -390,9 +390,6 @@ __device__ __forceinline__ void group_coord(int g, int& rr, int& kk) {
 // in wave order (deterministic), and handed to the epilogue with consecutive
 // threads on consecutive columns.
 // compile with -DDQ_SHARED_STAGING=1 for the block-shared operand staging (A/B builds)
-#ifndef DQ_LATE_FETCH
-#define DQ_LATE_FETCH 1
-#endif
 #ifndef DQ_SHARED_STAGING
 #define DQ_SHARED_STAGING 0
 #endif
@@ -413,7 +410,10 @@ struct Tile {
   }
 };
 
-template <int WM, int WN, int WK, class AL, class BL, class EP>
+// kLate: issue each half-band fetch after the previous half's MFMAs (<= 64 VGPRs,
+// for launches with several rounds of blocks, two 16-wave blocks per CU); else
+// while they run (one more fetch in flight, for single-round launches).
+template <int WM, int WN, int WK, class AL, class BL, class EP, bool kLate = true>
 __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& E, int M, int N,
                                             int K, int kchunk, int bx, int by, int bz,
                                             float* smem) {
@@ -571,10 +571,10 @@ __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& 
         stage_h(h);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         __builtin_amdgcn_wave_barrier();
-#if !DQ_LATE_FETCH
-        if (h == 0) fetch_h(k0, 1);
-        else if (k0 + BKT < kend) fetch_h(k0 + BKT, 0);
-#endif
+        if constexpr (!kLate) {
+          if (h == 0) fetch_h(k0, 1);
+          else if (k0 + BKT < kend) fetch_h(k0 + BKT, 0);
+        }
         if (live) {
           float av[8], bv[8];
           operands(Aw, AL::kFast, av);
@@ -587,10 +587,10 @@ __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& 
             acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc, 0, 0, 0);
 #endif
         }
-#if DQ_LATE_FETCH
-        if (h == 0) fetch_h(k0, 1);
-        else if (k0 + BKT < kend) fetch_h(k0 + BKT, 0);
-#endif
+        if constexpr (kLate) {
+          if (h == 0) fetch_h(k0, 1);
+          else if (k0 + BKT < kend) fetch_h(k0 + BKT, 0);
+        }
       }
     }
     __syncthreads();                 // staging windows are reused as reduction scratch
@@ -759,9 +759,10 @@ constexpr int kGroupT = 1024;
 #define DQ_ADAM_U 1
 #endif
 
-template <int WM, int WN, int WK, class AL, class BL, class EP>
+template <int WM, int WN, int WK, class AL, class BL, class EP, bool kLate = true>
 struct GemmOp {
   static constexpr int kT = 64 * WM * WN * WK;
+  static constexpr bool kLateFetch = kLate;
   static constexpr int kLds = Tile<WM, WN, WK>::template lds<AL, BL>();
   AL a;
   BL b;
@@ -769,7 +770,7 @@ struct GemmOp {
   int M, N, K, kchunk, gx, gy, gz;
   __device__ __forceinline__ void run(int blk, float* smem) const {
     const int bx = blk % gx, by = (blk / gx) % gy, bz = blk / (gx * gy);
-    igemm_block<WM, WN, WK>(a, b, e, M, N, K, kchunk, bx, by, bz, smem);
+    igemm_block<WM, WN, WK, AL, BL, EP, kLate>(a, b, e, M, N, K, kchunk, bx, by, bz, smem);
   }
   int blocks() const { return gx * gy * gz; }
 };
@@ -989,8 +990,22 @@ struct GroupArgs {
 #ifndef DQ_GROUP_WPE
 #define DQ_GROUP_WPE 8
 #endif
+// 8 waves per SIMD (<= 64 VGPRs: two 16-wave blocks per CU) unless a tile op of the
+// group fetches early (single-round launches, where the registers buy more)
+template <class Op, class = void>
+struct LateOk {
+  static constexpr bool value = true;
+};
+template <class Op>
+struct LateOk<Op, decltype((void)Op::kLateFetch)> {
+  static constexpr bool value = Op::kLateFetch;
+};
+template <class... Ops>
+constexpr int group_wpe() {
+  return (LateOk<Ops>::value && ...) ? DQ_GROUP_WPE : 1;
+}
 template <int T, class... Ops>
-__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(DQ_GROUP_WPE)))
+__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(group_wpe<Ops...>())))
 void k_grouped(GroupArgs<Ops...> g, Ops... ops) {
   __shared__ __attribute__((aligned(16))) float smem[max_lds<Ops...>()];
   int blk = blockIdx.x, i = 0;
@@ -1039,9 +1054,9 @@ void gemm(Ctx& c, AL a, BL b, EP e, int M, int N, int K, int splits = 1) {
 }
 
 // a grouped GEMM op; split-K ops write slabs into ws + off (EpiPartial)
-template <int WM, int WN, int WK, class AL, class BL, class EP>
-GemmOp<WM, WN, WK, AL, BL, EP> gemm_op(AL a, BL b, EP e, int M, int N, int K, int kchunk) {
-  GemmOp<WM, WN, WK, AL, BL, EP> op{a, b, e, M, N, K, kchunk, 0, 0, 0};
+template <int WM, int WN, int WK, bool kLate = true, class AL, class BL, class EP>
+GemmOp<WM, WN, WK, AL, BL, EP, kLate> gemm_op(AL a, BL b, EP e, int M, int N, int K, int kchunk) {
+  GemmOp<WM, WN, WK, AL, BL, EP, kLate> op{a, b, e, M, N, K, kchunk, 0, 0, 0};
   op.gx = (M + 32 * WM - 1) / (32 * WM);
   op.gy = (N + 32 * WN - 1) / (32 * WN);
   op.gz = (K + kchunk - 1) / kchunk;
@@ -1102,16 +1117,19 @@ struct FwdOps {
   static int fc1_chunk() { return split_chunk(kFlat, kSplitFc1, 32 * 16); }
   static int fc1_slabs() { return (kFlat + fc1_chunk() - 1) / fc1_chunk(); }
   static size_t ws_floats(int B) { return (size_t)fc1_slabs() * B * kHidden; }
+  template <bool kLate = true>
   auto conv1() const {
-    return gemm_op<1, 1, 8>(Im2col<Conv1>{x}, RowK{p->conv1_w, Conv1::K},
+    return gemm_op<1, 1, 8, kLate>(Im2col<Conv1>{x}, RowK{p->conv1_w, Conv1::K},
                             EpiBiasAct{a->a1, p->conv1_b, 32, true}, B * 441, 32, Conv1::K, Conv1::K);
   }
+  template <bool kLate = true>
   auto conv2() const {
-    return gemm_op<1, 1, 16>(Im2col<Conv2>{a->a1}, RowK{p->conv2_w, Conv2::K},
+    return gemm_op<1, 1, 16, kLate>(Im2col<Conv2>{a->a1}, RowK{p->conv2_w, Conv2::K},
                              EpiBiasAct{a->a2, p->conv2_b, 64, true}, B * 121, 64, Conv2::K, Conv2::K);
   }
+  template <bool kLate = true>
   auto conv3() const {
-    return gemm_op<1, 1, 9>(Im2col<Conv3>{a->a2}, RowK{p->conv3_w, Conv3::K},
+    return gemm_op<1, 1, 9, kLate>(Im2col<Conv3>{a->a2}, RowK{p->conv3_w, Conv3::K},
                             EpiBiasAct{a->a3, p->conv3_b, 64, true}, B * 121, 64, Conv3::K, Conv3::K);
   }
   auto fc1() const {
@@ -1148,9 +1166,9 @@ void forward_fused(Ctx& c0, Ctx& c1, const FwdOps& f0, const FwdOps& f1, bool fc
   c0.need = n0 > c0.need ? n0 : c0.need;
   c1.need = n1 > c1.need ? n1 : c1.need;
   if (c0.dry) return;
-  group(c0, f0.conv1());
-  group(c0, f0.conv2());
-  group(c0, f0.conv3());
+  group(c0, f0.conv1<false>());      // single-round launches: fetch early
+  group(c0, f0.conv2<false>());
+  group(c0, f0.conv3<false>());
   if (fc1_1)
     group(c0, f0.fc1(), f1.fc1());
   else
