@@ -990,6 +990,12 @@ struct GroupArgs {
 #ifndef DQ_GROUP_WPE
 #define DQ_GROUP_WPE 8
 #endif
+#ifndef DQ_B1_LATE
+#define DQ_B1_LATE false   // B1 is one round of blocks: early fetch (+1.5%)
+#endif
+#ifndef DQ_B6_LATE
+#define DQ_B6_LATE true
+#endif
 // 8 waves per SIMD (<= 64 VGPRs: two 16-wave blocks per CU) unless a tile op of the
 // group fetches early (single-round launches, where the registers buy more)
 template <class Op, class = void>
@@ -1317,7 +1323,7 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
   auto dW_fc2 = gemm_op<4, 4, 1>(ColKScalar{dout, NO}, ColKOnes{a->h, kHidden},
                                  EpiGrad{g->fc2_w, g->fc2_b, kHidden},
                                  NO, kHidden + 1, B, B);
-  auto dX_fc1 = gemm_op<1, 1, 16>(RowK{d->h, kHidden}, ColK{p->fc1_w, kFlat},
+  auto dX_fc1 = gemm_op<1, 1, 16, DQ_B1_LATE>(RowK{d->h, kHidden}, ColK{p->fc1_w, kFlat},
                                   EpiMask{d->a3, a->a3, kFlat}, B, kFlat, kHidden, kHidden);
   auto dW_fc1 = gemm_op<4, 4, 1>(ColK{d->h, kHidden}, ColKOnes{a->a3, kFlat},
                                  EpiGrad{g->fc1_w, g->fc1_b, kFlat},
@@ -1371,7 +1377,7 @@ if constexpr (kHeadFrom == 4) {
           if (in(3)) group_r(c, rd(3), dW_c3, dcol, part(f0, f1));
           if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, da1, part(f1, f2), head->conv1());
           if (in(5)) group_r(c, rd(5), sum_c2, dW_c1, part(f2, f3), head->conv2());
-          if (in(6)) group_r(c, rd(6), sum_c1, part(p->conv2_w, p->fc1_w), head->conv3());
+          if (in(6)) group_r(c, rd(6), sum_c1, part(p->conv2_w, p->fc1_w), head->conv3<DQ_B6_LATE>());
         } else {
           if (in(3)) group_r(c, rd(3), dW_c3, dcol, part(f0, f1), head->conv1());
           if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, da1, part(f1, f2), head->conv2());
