@@ -993,6 +993,9 @@ struct GroupArgs {
 #ifndef DQ_B1_LATE
 #define DQ_B1_LATE false   // B1 is one round of blocks: early fetch (+1.5%)
 #endif
+#ifndef DQ_F4_LATE
+#define DQ_F4_LATE true
+#endif
 #ifndef DQ_B6_LATE
 #define DQ_B6_LATE true
 #endif
@@ -1138,8 +1141,9 @@ struct FwdOps {
     return gemm_op<1, 1, 9, kLate>(Im2col<Conv3>{a->a2}, RowK{p->conv3_w, Conv3::K},
                             EpiBiasAct{a->a3, p->conv3_b, 64, true}, B * 121, 64, Conv3::K, Conv3::K);
   }
+  template <bool kLate = true>
   auto fc1() const {
-    return gemm_op<1, 1, 16>(RowK{a->a3, kFlat}, RowK{p->fc1_w, kFlat}, EpiPartial{ws, B, kHidden},
+    return gemm_op<1, 1, 16, kLate>(RowK{a->a3, kFlat}, RowK{p->fc1_w, kFlat}, EpiPartial{ws, B, kHidden},
                              B, kHidden, kFlat, fc1_chunk());
   }
   auto fc1_sum() const {
@@ -1176,7 +1180,7 @@ void forward_fused(Ctx& c0, Ctx& c1, const FwdOps& f0, const FwdOps& f1, bool fc
   group(c0, f0.conv2<false>());
   group(c0, f0.conv3<false>());
   if (fc1_1)
-    group(c0, f0.fc1(), f1.fc1());
+    group(c0, f0.fc1<DQ_F4_LATE>(), f1.fc1<DQ_F4_LATE>());
   else
     group(c0, f0.fc1());
   group(c0, f0.fchead(), f1.fchead());
