@@ -84,7 +84,6 @@ __global__ __launch_bounds__(1024) void k_c51(C51Args a, LS ol, LS tl, C51Extra 
   float* s_c = s_g + N;              // [N][64] projection terms c(i, j) p_j
   float* s_w = smem + (A * N + A + 2 * N + N * kWave + 3) / 4 * 4;   // [N][H] fc2 rows, 16-B aligned
   __shared__ float s_red[16];
-  __shared__ float s_z[kWave];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = T >> 6;
   const bool on = lane < N;
   const float ninf = -__builtin_inff();
@@ -105,7 +104,21 @@ __global__ __launch_bounds__(1024) void k_c51(C51Args a, LS ol, LS tl, C51Extra 
     const int act = wave + r * nw;
     xv[r] = (act < A && on) ? tl.get(((int64_t)b * A + act) * N + lane) : ninf;
   }
-  if (wave == 0) s_z[lane] = z;
+  // The Eq.-7 clipped quotients c(i, j) = clip(1 - |clip(Tz_j) - z_i| / dz, 0, 1) need only
+  // the reward, the terminal flag and the support: formed now, while the logits load
+  // (wave w takes source atoms j = w, w + nw, ...; lane = target atom i)
+  {
+    const float dz = __fsub_rn(z1, vmin);
+    const float gt = __fmul_rn(a.cg, __fsub_rn(1.0f, term_b));
+    for (int j = wave; j < N; j += nw) {
+      const float zj = a.support[j];
+      const float tzj = fminf(fmaxf(__fadd_rn(rew_b, __fmul_rn(gt, zj)), vmin), vmax);
+      if (on) {
+        float c = __fsub_rn(1.0f, __fdiv_rn(fabsf(__fsub_rn(tzj, z)), dz));
+        s_c[j * kWave + lane] = fminf(fmaxf(c, 0.0f), 1.0f);
+      }
+    }
+  }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int act = wave + r * nw;
@@ -165,24 +178,11 @@ __global__ __launch_bounds__(1024) void k_c51(C51Args a, LS ol, LS tl, C51Extra 
       best = s_q[act];
       astar = act;
     }
-  const float dz = __fsub_rn(z1, vmin);
-  const float gt = __fmul_rn(a.cg, __fsub_rn(1.0f, term_b));
   const float* pst = s_p + astar * N;
-  // projection terms: wave w takes source atoms j = w, w + nw, ...; lane = target atom i
-  for (int j = wave; j < N; j += nw) {
-    const float zj = s_z[j];
-    const float tzj = fminf(fmaxf(__fadd_rn(rew_b, __fmul_rn(gt, zj)), vmin), vmax);
-    if (on) {
-      float c = __fsub_rn(1.0f, __fdiv_rn(fabsf(__fsub_rn(tzj, z)), dz));
-      c = fminf(fmaxf(c, 0.0f), 1.0f);
-      s_c[j * kWave + lane] = __fmul_rn(c, pst[j]);
-    }
-  }
-  __syncthreads();
   if (wave == 0) {
-    float proj = 0.0f;
+    float proj = 0.0f;        // sum_j c(i, j) p_j in j order (rb:340-494)
     if (on)
-      for (int j = 0; j < N; ++j) proj = __fadd_rn(proj, s_c[j * kWave + lane]);
+      for (int j = 0; j < N; ++j) proj = __fadd_rn(proj, __fmul_rn(s_c[j * kWave + lane], pst[j]));
     const float my = wave_max(y);
     const float sh = on ? __fsub_rn(y, my) : 0.0f;
     const float ey = on ? expf(sh) : 0.0f;
