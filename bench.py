@@ -41,6 +41,9 @@ def parse():
   ap.add_argument('--no-graph', action='store_true')
   ap.add_argument('--cpu-seconds', type=float, default=12.0)
   ap.add_argument('--skip-cpu-baseline', action='store_true')
+  ap.add_argument('--per-call', action='store_true',
+                  help='drive the agent by update_period _train_step() calls per gradient '
+                       'step (one graph replay per step) instead of train_gradient_steps')
   ap.add_argument('--gather-iters', type=int, default=400)
   ap.add_argument('--fuse-opt', type=int, default=None,
                   help='override the agent default fuse_optimizer (0/1)')
@@ -201,19 +204,21 @@ def main():
   fill_synthetic(agent._replay.memory, args.actions, seed=1 + rank)
   torch.cuda.synchronize()
 
-  def grad_step():
-    for _ in range(agent.update_period):   # the reference's _train_step cadence
-      agent._train_step()
+  def grad_steps(n):
+    if args.per_call:
+      for _ in range(n):
+        for _ in range(agent.update_period):   # the reference's _train_step cadence
+          agent._train_step()
+    else:   # the same calls, consecutive steps replayed K per HIP graph (learner-only loop)
+      agent.train_gradient_steps(n)
 
-  for _ in range(args.warmup):
-    grad_step()
+  grad_steps(args.warmup)
   torch.cuda.synchronize()
   if pg is not None:
     dist.barrier()
   torch.cuda.synchronize()
   t0 = time.perf_counter()
-  for _ in range(args.steps):
-    grad_step()
+  grad_steps(args.steps)
   torch.cuda.synchronize()
   if pg is not None:
     dist.barrier()

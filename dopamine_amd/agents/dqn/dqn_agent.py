@@ -679,6 +679,79 @@ class DQNAgent(object):
       return random.randint(0, self.num_actions - 1)
     return int(torch.argmax(self._q_values(self.state), dim=1)[0].item())
 
+  # ------------------------------------------------------ learner-only loop
+  _UNROLL = 4
+
+  def train_gradient_steps(self, n):
+    """What ``n * update_period`` consecutive ``_train_step()`` calls do when nothing is
+    added or acted between them -- a learner-only loop over a fixed buffer (the
+    benchmark; Dopamine's fixed-replay / offline training phases).  Where the
+    pipelined single-replica HIP-graph path applies, _UNROLL consecutive gradient
+    steps are ONE graph replay (the graph-to-graph gap, ~5 us on MI355X, is paid
+    once per chunk); the steps, their order, RNG use and target syncs are exactly
+    those of the per-call loop (tests/test_gpu_agent.py)."""
+    n = int(n)
+    while n > 0:
+      K = self._UNROLL
+      if n >= K and self._chunk_ok():
+        self._run_train_ops_chunk(K)
+        t0 = self.training_steps
+        self.training_steps += K * self.update_period
+        # a sync falling on the chunk's last gradient step or after it (see _chunk_ok)
+        for t in range(t0, self.training_steps):
+          if t % self.target_update_period == 0:
+            self._sync_target()
+        n -= K
+        continue
+      for _ in range(self.update_period):
+        self._train_step()
+      n -= 1
+
+  def _chunk_ok(self):
+    K, U = self._UNROLL, self.update_period
+    t0 = self.training_steps
+    if not (self.pipeline and self.use_hip_graph and self._pg is None and self._hip is not None
+            and self.summary_writer is None
+            and self._has_prefetch and not self._interleaved()
+            and self._graph_sets.get(True) is not None and t0 % U == 0
+            and self._replay.memory.add_count > self.min_replay_history):
+      return False
+    if self._prefetch_add_count != int(self._replay.memory.add_count):
+      return False
+    # a target sync must not fall between two of the chunk's gradient steps
+    last = t0 + U * (K - 1)
+    return not any(t % self.target_update_period == 0 for t in range(t0, last))
+
+  def _run_train_ops_chunk(self, K):
+    """K pipelined gradient steps as one replay of a K-step graph (captured per
+    starting parity on first use)."""
+    mem = self._replay.memory
+    k0 = self._opt_steps % 2
+    key = ('chunk', K, k0)
+    g = self._graph_sets.get(key)
+    if g is None:
+      torch.cuda.synchronize(self._device)
+      g = torch.cuda.CUDAGraph()
+      with torch.cuda.graph(g, pool=self._graph_pool):
+        for j in range(K):
+          k = (k0 + j) % 2
+          self._grad_step(k, k, True)
+          self._device_opt_step(k)
+      self._graph_pool = g.pool()
+      self._graph_sets[key] = g
+    for _ in range(K):
+      mem.reserve_rng(self._batch_size)
+    g.replay()
+    self._opt_steps += K
+    c = (k0 + K - 1) % 2
+    self._replay._out = self._pbuf[c]
+    self._replay.unpack_transition(self._pbuf[c])
+    self._slot = 1 - c
+    self._has_prefetch = True
+    self._prefetch_add_count = int(mem.add_count)
+    self._last_train_add_count = int(mem.add_count)
+    self._selects_since_train = 0
+
   def _train_step(self):
     """dqn_agent.py:418-442."""
     if self._replay.memory.add_count > self.min_replay_history:

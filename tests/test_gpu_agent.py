@@ -218,3 +218,41 @@ def test_fused_head_matches_the_plain_schedule(graph):
   np.testing.assert_allclose(res[1][1], res[0][1], rtol=0, atol=1e-6)
   np.testing.assert_allclose(res[1][2], res[0][2], rtol=1e-4)
   np.testing.assert_allclose(res[1][3], res[0][3], rtol=1e-4)
+
+
+@pytest.mark.parametrize('kind', ['rainbow', 'dqn'])
+def test_learner_loop_chunks_equal_per_call_loop(kind):
+  """train_gradient_steps(n) (K consecutive steps per graph replay) == n *
+  update_period _train_step() calls: same batches, parameters, sum tree, RNG state
+  and training_steps, with target syncs falling inside and at the end of chunks."""
+  from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
+  res = []
+  for chunked in (False, True):
+    random.seed(5); np.random.seed(5); torch.manual_seed(5)
+    if kind == 'rainbow':
+      a = _rainbow(target_update_period=28)
+    else:
+      a = DQNAgent(num_actions=6, replay_capacity=3000, batch_size=32, min_replay_history=100,
+                   target_update_period=28)
+      _fill(a._replay.memory, 6, 3)
+    idx = []
+    for n in (6, 5, 9, 3, 8):
+      if chunked:
+        a.train_gradient_steps(n)
+      else:
+        for _ in range(n * a.update_period):
+          a._train_step()
+      idx.append(a._replay.transition['indices'].cpu().numpy().copy())
+    a._discard_prefetch()
+    a._replay.memory.sync_rng()
+    leaves = a._replay.memory.sum_tree.nodes[-1].copy() if kind == 'rainbow' else None
+    res.append((np.stack(idx), a.online_convnet.fp.flat.cpu().numpy(),
+                a.target_convnet.fp.flat.cpu().numpy(), leaves, a.training_steps,
+                a._opt_steps, random.getstate()))
+    if chunked:
+      assert any(k[0] == 'chunk' for k in a._graph_sets if isinstance(k, tuple)), 'no chunk ran'
+  for x, y in zip(res[0], res[1]):
+    if isinstance(x, np.ndarray):
+      np.testing.assert_array_equal(x, y)
+    else:
+      assert x == y
