@@ -27,16 +27,10 @@ def measure(make, actions, steps, warmup=20):
   bench.fill_synthetic(agent._replay.memory, actions, seed=1)
   torch.cuda.synchronize()
 
-  def grad_step():
-    for _ in range(agent.update_period):
-      agent._train_step()
-
-  for _ in range(warmup):
-    grad_step()
+  agent.train_gradient_steps(warmup)     # = update_period _train_step() calls per step
   torch.cuda.synchronize()
   t0 = time.perf_counter()
-  for _ in range(steps):
-    grad_step()
+  agent.train_gradient_steps(steps)
   torch.cuda.synchronize()
   dt = time.perf_counter() - t0
   agent._replay.memory.sync_rng()
