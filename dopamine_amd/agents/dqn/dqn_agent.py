@@ -296,7 +296,8 @@ class DQNAgent(object):
     """The online forward of slot c with the target network's tail (ride mode)."""
     from dopamine_amd import cnn
     if self._fused():
-      cnn.forward_fused(self._hip['online'], self._pbuf[c]['state'], self._hip['target'][c])
+      cnn.forward_fused(self._hip['online'], self._pbuf[c]['state'], self._hip['target'][c],
+                        conv3_b=self._head_from() == 5)
       return
     on, tg = cnn.forward_with_tail(self._hip['online'], self._pbuf[c]['state'], self._hip['target'][c])
     self._online_ready = on
@@ -304,6 +305,11 @@ class DQNAgent(object):
 
   def _bwd_first(self):
     return 1 if self._fused() else 0
+
+  def _head_from(self):
+    """The backward's schedule: 7 launches with the target head from launch 3, or
+    (fused) 5 launches from launch 1, the target's conv3 left to forward_fused."""
+    return 5 if self._fused() else 3
 
   def _pairs(self):
     return self.pair_forward and self._hip is not None and not self._rides()
@@ -359,7 +365,7 @@ class DQNAgent(object):
       adam = self._opt if self._fused_opt() else None
       f = self._bwd_first()
       self._hip['online'].backward(g, riders=riders, adam=adam, slot=k, head=self._head,
-                                   groups=(f, 7), head_from=3 + f)
+                                   groups=(f, 7), head_from=self._head_from())
       self._head = None
     elif pipe:
       main = torch.cuda.current_stream(self._device)
@@ -419,7 +425,7 @@ class DQNAgent(object):
       f = self._bwd_first()
       self._hip['online'].backward(g, groups=(self._SPLIT, 7),
                                    head=self._tail_head if pipe else None,
-                                   riders=self._tail_riders if pipe else None, head_from=3 + f)
+                                   riders=self._tail_riders if pipe else None, head_from=self._head_from())
       self._tail_head = self._tail_riders = None
     elif pipe:
       main = torch.cuda.current_stream(self._device)

@@ -117,7 +117,9 @@ class HipNatureCNN(object):
     rider i rides in launch first + i.  first = 1 skips fc2's input gradient
     (dacts['h'] already written, by ``c51_loss_fused``).  head_from = 4: the
     head's conv1..conv3 ride in launches 4..6 and its fc1 slabs are left to
-    ``forward_fused`` (the Rainbow fast path).
+    ``forward_fused`` (the Rainbow fast path).  head_from = 5: a five-launch
+    backward (from launch 1), the head's conv1/conv2 in launches 4/5 and its conv3
+    left to ``forward_fused(..., conv3_b=True)``.
 
     adam: an ops.TF1Adam over net.fp.flat -- its step (beta-power slot ``slot``)
     is applied inside the gradient epilogues (dq_cnn_backward_adam), so no
@@ -227,10 +229,11 @@ def fc2_parts(net):
   return net.ws[off:off + n].view(16, net.B, net.n_out)
 
 
-def forward_fused(a, xa, b, fc1_b=True):
+def forward_fused(a, xa, b, fc1_b=True, conv3_b=False):
   """The Rainbow fast path's forward (dq_cnn_forward_fused): ``a`` (online) on
   ``xa`` through fc1, ``b`` (target; conv1..conv3 already run, e.g. riding in the
-  previous backward with head_from=4) from its fc1 slabs (if ``fc1_b``), then one
+  previous backward with head_from=4) from its fc1 slabs (if ``fc1_b``; with
+  ``conv3_b`` its conv3 too, beside ``a``'s conv1: head_from=5), then one
   launch summing both nets' fc1 slabs and forming fc2's 16 k-band partials.
   Neither net's logits are stored: ``ops.c51_loss_fused`` sums the partials
   (bitwise the logits of ``forward``).  Returns the two partial views."""
@@ -239,6 +242,6 @@ def forward_fused(a, xa, b, fc1_b=True):
   a._x = xa
   _lib.check(_lib.lib.dq_cnn_forward_fused(
       ctypes.byref(a._p), xa.data_ptr(), ctypes.byref(a._a), a.ws.data_ptr(),
-      ctypes.byref(b._p), ctypes.byref(b._a), b.ws.data_ptr(), a.B, int(bool(fc1_b)),
-      a._stream(xa)), 'dq_cnn_forward_fused')
+      ctypes.byref(b._p), ctypes.byref(b._a), b.ws.data_ptr(), a.B,
+      int(bool(fc1_b)) | 2 * int(bool(conv3_b)), a._stream(xa)), 'dq_cnn_forward_fused')
   return fc2_parts(a), fc2_parts(b)

@@ -18,9 +18,9 @@
 // launch boundary does.
 //
 // The stride-2 conv2 input gradient is NOT an implicit GEMM over the 4x4 taps
-// (3/4 of those MACs would hit stride holes): it is the dense product
-// dcol = dy * W (pixels x (kh,kw,ci), K = 64) followed by an ordered col2im
-// gather that also applies the ReLU mask.
+// (3/4 of those MACs would hit stride holes): it is four dense GEMMs, one per
+// sub-pixel class (py, px) of the input, each over that class's 2x2 taps
+// (K = 4 * 64), with the ReLU mask in the epilogue (SubPix below).
 //
 // Activations are NHWC fp32; weights live in the flat parameter buffer as
 // conv (out, kh, kw, in) and FC (out, in) -- the GEMM's natural [M][K] layouts.
@@ -124,7 +124,7 @@ struct Im2colT {
 // stride-1 conv input gradient (transposed conv): rows m = input pixels, k = (kh, kw, co)
 template <class G>
 struct Col2im {
-  static_assert(G::S == 1, "strided input gradients go through dcol + col2im gather");
+  static_assert(G::S == 1, "strided input gradients go through the sub-pixel classes (SubPix)");
   static constexpr bool kFast = true;
   const float* dy;
   __device__ __forceinline__ float4 get(int m, int k, int mlim, int klim) const {
@@ -146,6 +146,59 @@ struct WeightT {
   __device__ __forceinline__ float4 get(int n, int k, int nlim, int klim) const {
     const int kk = k / G::CO, co = k - kk * G::CO;
     return bload4(w, (co * (G::KH * G::KW) + kk) * G::CI + n, n < nlim && k < klim);
+  }
+};
+
+// Stride-S conv input gradient by sub-pixel class: the input pixels with
+// (ih % S, iw % S) == (PY, PX) receive exactly the taps kh = (PY + PT) mod S + S*th,
+// kw = (PX + PL) mod S + S*tw, so the transposed conv is S*S dense GEMMs (rows = that
+// class's pixels, k = (th, tw, co)) with no stride holes and no dcol round trip.
+template <class G, int PY, int PX>
+struct SubPix {
+  static_assert(G::KH % G::S == 0 && G::KW % G::S == 0, "taps split evenly over the classes");
+  static constexpr int NY = (G::H - PY + G::S - 1) / G::S, NX = (G::W - PX + G::S - 1) / G::S;
+  static constexpr int TW = G::KW / G::S, K = (G::KH / G::S) * TW * G::CO;
+  static constexpr int KH0 = (PY + G::PT) % G::S, KW0 = (PX + G::PL) % G::S;
+  __device__ static __forceinline__ int pixel(int m) {      // NHWC pixel index of class row m
+    const int b = m / (NY * NX), q = m - b * (NY * NX);
+    const int i = q / NX, j = q - i * NX;
+    return (b * G::H + PY + G::S * i) * G::W + PX + G::S * j;
+  }
+  __device__ static __forceinline__ void tap(int k, int& kh, int& kw, int& co) {
+    const int t = k / G::CO;
+    co = k - t * G::CO;
+    const int th = t / TW;
+    kh = KH0 + G::S * th;
+    kw = KW0 + G::S * (t - th * TW);
+  }
+};
+// A: dy of the taps landing on class row m, k = (th, tw, co) with co contiguous
+template <class G, int PY, int PX>
+struct SubPixDy {
+  using SP = SubPix<G, PY, PX>;
+  static constexpr bool kFast = true;
+  const float* dy;
+  __device__ __forceinline__ float4 get(int m, int k, int mlim, int klim) const {
+    const int b = m / (SP::NY * SP::NX), q = m - b * (SP::NY * SP::NX);
+    const int i = q / SP::NX, j = q - i * SP::NX;
+    int kh, kw, co;
+    SP::tap(k, kh, kw, co);
+    const int th = PY + G::S * i + G::PT - kh, tw = PX + G::S * j + G::PL - kw;   // even
+    const int oh = th / G::S, ow = tw / G::S;
+    const bool ok = m < mlim && k < klim && th >= 0 && tw >= 0 && oh < G::OH && ow < G::OW;
+    return bload4(dy, ((b * G::OH + oh) * G::OW + ow) * G::CO + co, ok);
+  }
+};
+// B: W[co][kh][kw][ci] as B(n = ci, k = (th, tw, co)), ci contiguous
+template <class G, int PY, int PX>
+struct SubPixW {
+  using SP = SubPix<G, PY, PX>;
+  static constexpr bool kFast = false;
+  const float* w;
+  __device__ __forceinline__ float4 get(int n, int k, int nlim, int klim) const {
+    int kh, kw, co;
+    SP::tap(k, kh, kw, co);
+    return bload4(w, ((co * G::KH + kh) * G::KW + kw) * G::CI + n, n < nlim && k < klim);
   }
 };
 
@@ -243,6 +296,21 @@ struct EpiMask {             // out[m][n] = acc * (act[m][n] > 0)   (ReLU backwa
   __device__ __forceinline__ float pf(int m, int n) const { return act[(int64_t)m * ld + n]; }
   __device__ __forceinline__ void apply(int m, int n, float v, float a) const {
     out[(int64_t)m * ld + n] = a > 0.0f ? v : 0.0f;
+  }
+  __device__ __forceinline__ void operator()(int m, int n, float v, int) const {
+    apply(m, n, v, pf(m, n));
+  }
+};
+template <class SP, int C>
+struct EpiMaskPix {          // EpiMask on a sub-pixel class: row m -> its NHWC pixel
+  float* out;
+  const float* act;
+  static constexpr bool kPrefetch = true;
+  __device__ __forceinline__ float pf(int m, int n) const {
+    return act[(int64_t)SP::pixel(m) * C + n];
+  }
+  __device__ __forceinline__ void apply(int m, int n, float v, float a) const {
+    out[(int64_t)SP::pixel(m) * C + n] = a > 0.0f ? v : 0.0f;
   }
   __device__ __forceinline__ void operator()(int m, int n, float v, int) const {
     apply(m, n, v, pf(m, n));
@@ -706,49 +774,6 @@ __global__ __launch_bounds__(256) void k_splitk_reduce(const float* ws, int spli
   splitk_sum(ws, splits, M, N, E, (int64_t)blockIdx.x * blockDim.x + threadIdx.x);
 }
 
-// strided conv input gradient from dcol[(b, oh, ow)][(kh, kw, ci)]:
-// dx[b][ih][iw][ci] = (act > 0) * sum over the taps that land on (ih, iw), in (kh, kw) order
-template <class G>
-__device__ __forceinline__ void col2im_group(const float* dcol, const float* act, float* dx, int i,
-                                             int total4) {
-  if (i >= total4) return;
-  constexpr int C4 = G::CI / 4;
-  const int ci = (i % C4) * 4, pix = i / C4;
-  const int b = pix / (G::H * G::W), p = pix - b * (G::H * G::W);
-  const int ih = p / G::W, iw = p - ih * G::W;
-  float4 s = zero4();
-  for (int kh = (ih + G::PT) % G::S; kh < G::KH; kh += G::S) {
-    const int th = ih + G::PT - kh;
-    if (th < 0) break;
-    const int oh = th / G::S;
-    if (oh >= G::OH) continue;
-    for (int kw = (iw + G::PL) % G::S; kw < G::KW; kw += G::S) {
-      const int tw = iw + G::PL - kw;
-      if (tw < 0) break;
-      const int ow = tw / G::S;
-      if (ow >= G::OW) continue;
-      const float4 v = ld4(dcol + ((b * G::OH + oh) * G::OW + ow) * G::K + (kh * G::KW + kw) * G::CI + ci);
-      s.x = __fadd_rn(s.x, v.x);
-      s.y = __fadd_rn(s.y, v.y);
-      s.z = __fadd_rn(s.z, v.z);
-      s.w = __fadd_rn(s.w, v.w);
-    }
-  }
-  const float4 a = ld4(act + (int64_t)i * 4);
-  float4 o;
-  o.x = a.x > 0.0f ? s.x : 0.0f;
-  o.y = a.y > 0.0f ? s.y : 0.0f;
-  o.z = a.z > 0.0f ? s.z : 0.0f;
-  o.w = a.w > 0.0f ? s.w : 0.0f;
-  *reinterpret_cast<float4*>(dx + (int64_t)i * 4) = o;
-}
-
-template <class G>
-__global__ __launch_bounds__(256) void k_col2im(const float* dcol, const float* act, float* dx,
-                                                int total4) {
-  col2im_group<G>(dcol, act, dx, blockIdx.x * 256 + threadIdx.x, total4);
-}
-
 // ------------------------------------------------------------ grouped launches
 // Independent operations of the backward (layer L's weight gradient beside layer
 // L+1's input gradient, a split-K reduce beside the next GEMMs) share ONE launch:
@@ -877,20 +902,6 @@ struct FcHeadOp {
       if (m < B && n < NO) dst[(int64_t)m * NO + n] = acc[e];
     }
   }
-};
-
-template <class G>
-struct Col2imOp {
-  static constexpr int kT = kGroupT;
-  static constexpr int kLds = 0;
-  const float* dcol;
-  const float* act;
-  float* dx;
-  int total4;
-  __device__ __forceinline__ void run(int blk, float*) const {
-    col2im_group<G>(dcol, act, dx, blk * kGroupT + threadIdx.x, total4);
-  }
-  int blocks() const { return (total4 + kGroupT - 1) / kGroupT; }
 };
 
 // TF1 Adam (the arithmetic of dq_adam_tf1) over a contiguous range of the flat
@@ -1024,7 +1035,7 @@ void k_grouped(GroupArgs<Ops...> g, Ops... ops) {
 // Launch context: a dry run only sizes the workspace, so the two can never disagree.
 struct Ctx {
   hipStream_t s;
-  float* ws;       // split-K slabs / conv2 dcol
+  float* ws;       // split-K slabs
   bool dry;
   size_t need;
   size_t take(size_t n) {        // carve a private workspace region (grouped ops run together)
@@ -1170,13 +1181,17 @@ struct FwdOps {
 // partials, net 1 (target, head run earlier: conv1..conv3 into a1) finishing with
 // its fc1 slabs (if fc1_1) in net 0's fc1 launch and its fused head beside net 0's:
 // 5 launches.  The logits are summed by dq_c51_loss_fused.
-void forward_fused(Ctx& c0, Ctx& c1, const FwdOps& f0, const FwdOps& f1, bool fc1_1) {
+void forward_fused(Ctx& c0, Ctx& c1, const FwdOps& f0, const FwdOps& f1, bool fc1_1,
+                   bool conv3_1 = false) {
   const size_t n0 = FwdOps::fused_ws_floats(f0.B, f0.p->n_out);
   const size_t n1 = FwdOps::fused_ws_floats(f1.B, f1.p->n_out);
   c0.need = n0 > c0.need ? n0 : c0.need;
   c1.need = n1 > c1.need ? n1 : c1.need;
   if (c0.dry) return;
-  group(c0, f0.conv1<false>());      // single-round launches: fetch early
+  if (conv3_1)                       // net 1's conv3 (head_from = 5) beside net 0's conv1
+    group(c0, f0.conv1<false>(), f1.conv3());
+  else
+    group(c0, f0.conv1<false>());    // single-round launches: fetch early
   group(c0, f0.conv2<false>());
   group(c0, f0.conv3<false>());
   if (fc1_1)
@@ -1228,6 +1243,19 @@ void forward_head(Ctx& c, const FwdOps& f) {
   group(c, f.fc1());
 }
 
+// conv2's input gradient as its 4 sub-pixel classes (SubPix): da1 straight from da2,
+// masked by a1 > 0, in one grouped launch of 8-wave tiles (K = 2 x 2 taps x 64 = 256)
+#ifndef DQ_SP_LATE
+#define DQ_SP_LATE true
+#endif
+template <int PY, int PX>
+auto subpix_op(const dq_cnn_params* p, const dq_cnn_acts* a, dq_cnn_acts* d, int B) {
+  using SP = SubPix<Conv2, PY, PX>;
+  return gemm_op<1, 1, 8, DQ_SP_LATE>(SubPixDy<Conv2, PY, PX>{d->a2}, SubPixW<Conv2, PY, PX>{p->conv2_w},
+                          EpiMaskPix<SP, Conv2::CI>{d->a1, a->a1}, B * SP::NY * SP::NX, Conv2::CI,
+                          SP::K, SP::K);
+}
+
 // Backward of one layer: part 1 = weight/bias gradient, part 0 = input gradient.
 // Layers 0..4 = fc2, fc1, conv3, conv2, conv1 (conv1 has no input gradient).
 // Same tiles and split factors as the grouped schedule below: bitwise identical.
@@ -1263,18 +1291,10 @@ bool backward_layer(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int 
       gemm<1, 1, 16>(c, DyT<64>{d->a2}, Im2colT<Conv2>{a->a1},
                      EpiGrad{g->conv2_w, g->conv2_b, Conv2::K}, 64, Conv2::K + 1, B * 121, kSplitConvW);
       return true;
-    case 3 * 2 + 0: {  // da1 = col2im(da2 W2) * (a1 > 0)
-      const size_t dcol = (size_t)B * 121 * Conv2::K;
-      c.need = dcol > c.need ? dcol : c.need;
-      gemm<4, 4, 1>(c, RowK{d->a2, 64}, ColK{p->conv2_w, Conv2::K}, EpiStore{c.ws, Conv2::K},
-                    B * 121, Conv2::K, 64);
-      if (!c.dry) {
-        const int total4 = B * 441 * 32 / 4;
-        hipLaunchKernelGGL((k_col2im<Conv2>), dim3((total4 + 255) / 256), dim3(256), 0, c.s, c.ws,
-                           a->a1, d->a1, total4);
-      }
+    case 3 * 2 + 0:   // da1 = conv2^T(da2) * (a1 > 0), by sub-pixel class
+      group(c, subpix_op<0, 0>(p, a, d, B), subpix_op<0, 1>(p, a, d, B),
+            subpix_op<1, 0>(p, a, d, B), subpix_op<1, 1>(p, a, d, B));
       return true;
-    }
     case 4 * 2 + 1:   // conv1: dW1|db1 = da1^T [im2col(x) | 1]   (no input gradient needed)
       gemm<1, 1, 16>(c, DyT<32>{d->a1}, Im2colT<Conv1>{x}, EpiGrad{g->conv1_w, g->conv1_b, Conv1::K},
                      32, Conv1::K + 1, B * 441, kSplitConv1W);
@@ -1284,14 +1304,17 @@ bool backward_layer(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int 
   }
 }
 
-// Backward in 7 grouped launches (13 kernels' worth of work):
-//   1: dh                      (fc2 input grad)
-//   2: dW fc2     | da3        (fc1 input grad)
-//   3: dW fc1     | da2        (conv3 input grad)              [+ Adam fc2]
-//   4: dW conv3 slabs | dcol   (conv2 input grad, dense part)  [+ Adam fc1, 1st third]
-//   5: sum conv3 slabs | dW conv2 slabs | da1 = col2im(dcol)   [+ Adam fc1, 2nd third]
-//   6: sum conv2 slabs | dW conv1 slabs                        [+ Adam fc1, 3rd third]
-//   7: sum conv1 slabs                                         [+ Adam conv2, conv3]
+// Backward in 7 grouped launches (numbered 0..6 below):
+//   0: dh                      (fc2 input grad)
+//   1: dW fc2     | da3        (fc1 input grad)
+//   2: dW fc1     | da2        (conv3 input grad)              [+ Adam fc2]
+//   3: dW conv3 slabs | da1    (conv2 input grad, 4 sub-pixel GEMMs) [+ Adam fc1, 1st third]
+//   4: sum conv3 slabs | dW conv2 slabs                        [+ Adam fc1, 2nd third]
+//   5: sum conv2 slabs | dW conv1 slabs                        [+ Adam fc1, 3rd third]
+//   6: sum conv1 slabs                                         [+ Adam conv2, conv3]
+// or, kHeadFrom = 5, in 6 (the Rainbow fast path starts at 1, dh coming from the loss):
+//   4: sum conv3 slabs | dW conv2 slabs | dW conv1 slabs       [+ Adam fc1, 2nd third]
+//   5: sum conv2 slabs | sum conv1 slabs               [+ Adam fc1, 3rd third, conv3]
 // With kAdam the TF1 Adam step is spread as bracketed: float4 AdamOps over ranges
 // whose gradients are final and whose weights have had their last read; conv1's
 // split-K sum applies it in its epilogue (and advances the beta powers).  The
@@ -1301,7 +1324,8 @@ bool backward_layer(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int 
 // (same tiles, same summation order), so the two are bitwise identical.
 // kHeadFrom: the launch of the head network's conv1 (3: conv1..conv3 and the fc1
 // slabs in launches 3..6; 4: conv1..conv3 in launches 4..6, its fc1 slabs left to
-// forward_fused).  Riders are numbered from launch `first`: rider i rides in launch
+// forward_fused; 5: conv1, conv2 in launches 4, 5 of the six-launch schedule, conv3
+// and the fc1 slabs left to forward_fused).  Riders are numbered from launch `first`: rider i rides in launch
 // first + i.
 template <bool kAdam, int kHeadFrom = 3>
 void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int B,
@@ -1318,7 +1342,6 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
   const int ch1 = split_chunk(K1, kSplitConv1W, W16::BKT), nz1 = (K1 + ch1 - 1) / ch1;
   const size_t o3 = c.take((size_t)nz3 * 64 * (Conv3::K + 1));
   const size_t o2 = c.take((size_t)nz3 * 64 * (Conv2::K + 1));
-  const size_t od = c.take((size_t)K3 * Conv2::K);
   const size_t o1 = c.take((size_t)nz1 * 32 * (Conv1::K + 1));
   float* ws = c.ws;
   if (c.dry) return;
@@ -1336,13 +1359,14 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
                                  EpiMask{d->a2, a->a2, 64}, K3, 64, Conv3::K, Conv3::K);
   auto dW_c3 = gemm_op<1, 1, 16>(DyT<64>{d->a3}, Im2colT<Conv3>{a->a2},
                                  EpiPartial{ws + o3, 64, Conv3::K + 1}, 64, Conv3::K + 1, K3, ch3);
-  auto dcol = gemm_op<4, 4, 1>(RowK{d->a2, 64}, ColK{p->conv2_w, Conv2::K},
-                               EpiStore{ws + od, Conv2::K}, K3, Conv2::K, 64, 64);
+  auto sp00 = subpix_op<0, 0>(p, a, d, B);
+  auto sp01 = subpix_op<0, 1>(p, a, d, B);
+  auto sp10 = subpix_op<1, 0>(p, a, d, B);
+  auto sp11 = subpix_op<1, 1>(p, a, d, B);
   auto sum_c3 = ReduceOp<EpiGrad>{ws + o3, nz3, 64, Conv3::K + 1,
                                   EpiGrad{g->conv3_w, g->conv3_b, Conv3::K}};
   auto dW_c2 = gemm_op<1, 1, 16>(DyT<64>{d->a2}, Im2colT<Conv2>{a->a1},
                                  EpiPartial{ws + o2, 64, Conv2::K + 1}, 64, Conv2::K + 1, K3, ch3);
-  auto da1 = Col2imOp<Conv2>{ws + od, a->a1, d->a1, B * 441 * 32 / 4};
   auto sum_c2 = ReduceOp<EpiGrad>{ws + o2, nz3, 64, Conv2::K + 1,
                                   EpiGrad{g->conv2_w, g->conv2_b, Conv2::K}};
   auto dW_c1 = gemm_op<1, 1, 16>(DyT<32>{d->a1}, Im2colT<Conv1>{x},
@@ -1373,25 +1397,47 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
       const int64_t third = ((f3 - f0) / 3) & ~(int64_t)3;
       float* f1 = f0 + third;
       float* f2 = f1 + third;
+      if constexpr (kHeadFrom == 5) {
+        // five launches: conv2's input gradient by sub-pixel class needs only da2, so
+        // conv1's weight-gradient slabs join launch 4 and the three split-K sums end
+        // the backward in launch 5, conv2 and conv1 applying Adam in their epilogues
+        auto sum_c2a = ReduceOp<decltype(GE::make(0, 0, 0, 0, 0, opt, 0))>{
+            ws + o2, nz3, 64, Conv2::K + 1,
+            GE::make(g->conv2_w, g->conv2_b, Conv2::K, p->conv2_w, p->conv2_b, opt, 0)};
+        if (in(0)) group_r(c, rd(0), dX_fc2);
+        if (in(1)) group_r(c, rd(1), dW_fc2, dX_fc1);
+        if (in(2)) group_r(c, rd(2), dW_fc1, dX_c3, part(p->fc2_w, p->fc2_b + NO));
+        if (in(3)) group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11, part(f0, f1));
+        if (head) {
+          if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, dW_c1, part(f1, f2), head->conv1());
+          if (in(5))
+            group_r(c, rd(5), sum_c2a, sum_c1, part(f2, f3), part(p->conv3_w, p->fc1_w),
+                    head->conv2());
+        } else {
+          if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, dW_c1, part(f1, f2));
+          if (in(5)) group_r(c, rd(5), sum_c2a, sum_c1, part(f2, f3), part(p->conv3_w, p->fc1_w));
+        }
+        return;
+      }
       if (in(0)) group_r(c, rd(0), dX_fc2);
       if (in(1)) group_r(c, rd(1), dW_fc2, dX_fc1);
       if (in(2)) group_r(c, rd(2), dW_fc1, dX_c3, part(p->fc2_w, p->fc2_b + NO));
       if (head) {
 if constexpr (kHeadFrom == 4) {
-          if (in(3)) group_r(c, rd(3), dW_c3, dcol, part(f0, f1));
-          if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, da1, part(f1, f2), head->conv1());
+          if (in(3)) group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11, part(f0, f1));
+          if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, part(f1, f2), head->conv1());
           if (in(5)) group_r(c, rd(5), sum_c2, dW_c1, part(f2, f3), head->conv2());
           if (in(6)) group_r(c, rd(6), sum_c1, part(p->conv2_w, p->fc1_w), head->conv3<DQ_B6_LATE>());
         } else {
-          if (in(3)) group_r(c, rd(3), dW_c3, dcol, part(f0, f1), head->conv1());
-          if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, da1, part(f1, f2), head->conv2());
+          if (in(3)) group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11, part(f0, f1), head->conv1());
+          if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, part(f1, f2), head->conv2());
           if (in(5)) group_r(c, rd(5), sum_c2, dW_c1, part(f2, f3), head->conv3());
           if (in(6)) group_r(c, rd(6), sum_c1, part(p->conv2_w, p->fc1_w), head->fc1());
         }
         return;
       }
-      if (in(3)) group_r(c, rd(3), dW_c3, dcol, part(f0, f1));
-      if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, da1, part(f1, f2));
+      if (in(3)) group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11, part(f0, f1));
+      if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, part(f1, f2));
       if (in(5)) group_r(c, rd(5), sum_c2, dW_c1, part(f2, f3));
       if (in(6)) group_r(c, rd(6), sum_c1, part(p->conv2_w, p->fc1_w));
       return;
@@ -1400,22 +1446,33 @@ if constexpr (kHeadFrom == 4) {
   if (in(0)) group_r(c, rd(0), dX_fc2);
   if (in(1)) group_r(c, rd(1), dW_fc2, dX_fc1);
   if (in(2)) group_r(c, rd(2), dW_fc1, dX_c3);
+  if constexpr (kHeadFrom == 5) {
+    if (in(3)) group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11);
+    if (head) {
+      if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, dW_c1, head->conv1());
+      if (in(5)) group_r(c, rd(5), sum_c2, sum_c1, head->conv2());
+    } else {
+      if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, dW_c1);
+      if (in(5)) group_r(c, rd(5), sum_c2, sum_c1);
+    }
+    return;
+  }
   if (head) {
     if constexpr (kHeadFrom == 4) {
-      if (in(3)) group_r(c, rd(3), dW_c3, dcol);
-      if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, da1, head->conv1());
+      if (in(3)) group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11);
+      if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, head->conv1());
       if (in(5)) group_r(c, rd(5), sum_c2, dW_c1, head->conv2());
       if (in(6)) group_r(c, rd(6), sum_c1, head->conv3());
     } else {
-      if (in(3)) group_r(c, rd(3), dW_c3, dcol, head->conv1());
-      if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, da1, head->conv2());
+      if (in(3)) group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11, head->conv1());
+      if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, head->conv2());
       if (in(5)) group_r(c, rd(5), sum_c2, dW_c1, head->conv3());
       if (in(6)) group_r(c, rd(6), sum_c1, head->fc1());
     }
     return;
   }
-  if (in(3)) group_r(c, rd(3), dW_c3, dcol);
-  if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, da1);
+  if (in(3)) group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11);
+  if (in(4)) group_r(c, rd(4), sum_c3, dW_c2);
   if (in(5)) group_r(c, rd(5), sum_c2, dW_c1);
   if (in(6)) group_r(c, rd(6), sum_c1);
 }
@@ -1503,7 +1560,7 @@ int dq_cnn_forward_fused(const dq_cnn_params* p0, const float* x0, dq_cnn_acts* 
   DQ_CHECK_ARG(ws0 != ws1, "the two networks need separate workspaces");
   Ctx c0{(hipStream_t)stream, ws0, false, 0}, c1{(hipStream_t)stream, ws1, false, 0};
   forward_fused(c0, c1, FwdOps{p0, x0, a0, ws0, batch}, FwdOps{p1, nullptr, a1, ws1, batch},
-                fc1_1 != 0);
+                (fc1_1 & 1) != 0, (fc1_1 & 2) != 0);
   DQ_CHECK_LAUNCH("dq_cnn_forward_fused");
   return DQ_OK;
 }
@@ -1557,7 +1614,7 @@ int dq_cnn_backward_riders(const dq_cnn_params* p, const dq_cnn_params* g, int32
                "at most one rider per grouped launch (7)");
   DQ_CHECK_ARG(0 <= first && first <= last && last <= 7, "groups must satisfy 0 <= first <= last <= 7");
   DQ_CHECK_ARG(!opt || (first <= 1 && last == 7), "the fused optimizer needs the whole backward");
-  DQ_CHECK_ARG(head_from == 3 || head_from == 4, "head_from must be 3 or 4");
+  DQ_CHECK_ARG(head_from >= 3 && head_from <= 5, "head_from must be 3, 4 or 5");
   RiderDesc r[7];
   for (int i = 0; i < n_riders; ++i) {
     memcpy(&r[i], &riders[i], sizeof(RiderDesc));
@@ -1575,14 +1632,20 @@ int dq_cnn_backward_riders(const dq_cnn_params* p, const dq_cnn_params* g, int32
   if (opt) {
     const int rc = check_adam(p, g, opt);
     if (rc != DQ_OK) return rc;
-    if (head_from == 4)
+    if (head_from == 5)
+      backward_grouped<true, 5>(c, p, g, batch, x, a, dout, d, AdamHost{opt}, first, last, r,
+                                n_riders, hp);
+    else if (head_from == 4)
       backward_grouped<true, 4>(c, p, g, batch, x, a, dout, d, AdamHost{opt}, first, last, r,
                                 n_riders, hp);
     else
       backward_grouped<true>(c, p, g, batch, x, a, dout, d, AdamHost{opt}, first, last, r,
                              n_riders, hp);
   } else {
-    if (head_from == 4)
+    if (head_from == 5)
+      backward_grouped<false, 5>(c, p, g, batch, x, a, dout, d, AdamHost{nullptr}, first, last, r,
+                                 n_riders, hp);
+    else if (head_from == 4)
       backward_grouped<false, 4>(c, p, g, batch, x, a, dout, d, AdamHost{nullptr}, first, last, r,
                                  n_riders, hp);
     else

@@ -310,7 +310,10 @@ int dq_cnn_forward_with_tail(const dq_cnn_params* p0, const float* x0, dq_cnn_ac
    x, a, dout, d, g or ws.  head (may be NULL): another network's forward head (e.g. the
    target network on the next batch, which riders gathered) runs in launches 4..7
    (head_from = 3: conv1..conv3 + fc1 slabs) or 5..7 (head_from = 4: conv1..conv3, the fc1
-   slabs then run in dq_cnn_forward_fused).  Rider i rides in launch first + i.  Only
+   slabs then run in dq_cnn_forward_fused).  head_from = 5 selects the five-launch backward
+   (launches 0..5; conv2's input gradient by sub-pixel class, the split-K sums of conv2 and
+   conv1 both in launch 5) with the head's conv1 / conv2 in launches 4 / 5 and its conv3
+   and fc1 slabs left to dq_cnn_forward_fused (fc1_1 = 3).  Rider i rides in launch first + i.  Only
    launches [first, last) are issued (as dq_cnn_backward_groups; riders and head ops of
    other launches are skipped; opt needs [0, 7)).  CNN results are bitwise those of the
    separate calls. */
@@ -322,8 +325,9 @@ int dq_cnn_backward_riders(const dq_cnn_params* p, const dq_cnn_params* g, int32
 /* The Rainbow fast path (rainbow_agent.py:200-305 on the Nature CNN, one launch less in
    the forward and one in the backward than dq_cnn_forward_with_tail + dq_c51_loss +
    dq_cnn_backward_riders(first 0)):
-   dq_cnn_forward_fused: net 0 (online) conv1..fc1 and net 1's (target's) fc1 slabs (if fc1_1;
-   its conv1..conv3 ran earlier, e.g. as head_from = 4 riders of the previous backward), then
+   dq_cnn_forward_fused: net 0 (online) conv1..fc1 and net 1's (target's) fc1 slabs (if fc1_1
+   bit 0; its conv1..conv3 ran earlier, e.g. as head_from = 4 riders of the previous backward;
+   with bit 1 its conv3 runs here too, in net 0's conv1 launch: head_from = 5), then
    ONE launch that sums both nets' fc1 slabs (+ bias, ReLU -> a->h) and stores fc2's 16 k-band
    partial products at ws + dq_cnn_fc2_parts_offset(batch) ([16][B][n_out]).  The logits are
    never stored by the CNN: dq_c51_loss_fused sums the partials in band order and adds the

@@ -11,7 +11,7 @@ def name_of(n):
   if n.startswith('k_grouped'):
     ops = []
     for m in re.finditer(r'(GemmOp<(\d+), (\d+), (\d+), (\w+)(?:<[^>]*(?:<[^>]*>)?[^>]*>)?, (\w+)'
-                         r'(?:<[^>]*(?:<[^>]*>)?[^>]*>)?, (\w+)|ReduceOp<(\w+)|Col2imOp|AdamOp|RiderOp'
+                         r'(?:<[^>]*(?:<[^>]*>)?[^>]*>)?, (\w+)|ReduceOp<(\w+)|SubPix|AdamOp|RiderOp'
                          r'|FcHeadOp)', n):
       if m.group(1).startswith('GemmOp'):
         ops.append('G%s%s%s:%s/%s/%s' % (m.group(2), m.group(3), m.group(4), m.group(5),
