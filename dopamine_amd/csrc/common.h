@@ -58,6 +58,12 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o));
+  return v;
+}
+
 // ---- TF1 ApplyAdam, shared by the optimizer kernels and the fused CNN epilogues.
 // state = {beta1^t, beta2^t} x 2 slots: step t reads slot t % 2 and writes the
 // next powers into the other slot (one thread per step does that).

@@ -38,7 +38,7 @@ struct LogitsParts {
   const float* part;   // [np][B * NO]
   const float* bias;   // [NO]
   int64_t stride;      // B * NO
-  int np, NO;
+  int np, NO;          // np <= 16: straight-line loads, all in flight before the first add
   __device__ __forceinline__ float get(int64_t i) const {
     float v[16];
 #pragma unroll
@@ -47,7 +47,6 @@ struct LogitsParts {
 #pragma unroll
     for (int z = 1; z < 16; ++z)
       if (z < np) x = __fadd_rn(x, v[z]);
-    for (int z = 16; z < np; ++z) x = __fadd_rn(x, part[(int64_t)z * stride + i]);
     return __fadd_rn(x, bias[i % NO]);
   }
 };
@@ -73,6 +72,50 @@ struct C51Extra {
 // The fused path (x.w2) also forms d h from the chosen action's N logit
 // gradients; its W2 rows are fetched into LDS at the start, under the chain.
 
+// Wave-wide reductions on DPP row rotations (no LDS round trips, unlike __shfl_xor's
+// ds_bpermute chain): each 16-lane row reduces by row_ror 8, 4, 2, 1, then lanes 0, 16,
+// 32, 48 combine as (r0 op r1) op (r2 op r3) -- one value, the same in every lane.
+template <int kCtrl>
+__device__ __forceinline__ float dpp_ror(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), kCtrl, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float rl(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ float fast_sum(float v) {
+  v = __fadd_rn(v, dpp_ror<0x128>(v));
+  v = __fadd_rn(v, dpp_ror<0x124>(v));
+  v = __fadd_rn(v, dpp_ror<0x122>(v));
+  v = __fadd_rn(v, dpp_ror<0x121>(v));
+  return __fadd_rn(__fadd_rn(rl(v, 0), rl(v, 16)), __fadd_rn(rl(v, 32), rl(v, 48)));
+}
+__device__ __forceinline__ float fast_max(float v) {
+  v = fmaxf(v, dpp_ror<0x128>(v));
+  v = fmaxf(v, dpp_ror<0x124>(v));
+  v = fmaxf(v, dpp_ror<0x122>(v));
+  v = fmaxf(v, dpp_ror<0x121>(v));
+  return fmaxf(fmaxf(rl(v, 0), rl(v, 16)), fmaxf(rl(v, 32), rl(v, 48)));
+}
+__device__ __forceinline__ float fast_min(float v) {
+  v = fminf(v, dpp_ror<0x128>(v));
+  v = fminf(v, dpp_ror<0x124>(v));
+  v = fminf(v, dpp_ror<0x122>(v));
+  v = fminf(v, dpp_ror<0x121>(v));
+  return fminf(fminf(rl(v, 0), rl(v, 16)), fminf(rl(v, 32), rl(v, 48)));
+}
+
+#ifdef DQ_C51_PROF
+__device__ long long g_c51_t[256][8];
+__device__ long long g_c51_w[256][16];
+__device__ long long g_c51_w2[256][16];
+#define C51_T(k) if (threadIdx.x == 0) g_c51_t[blockIdx.x][k] = wall_clock64()
+#define C51_W2() if ((threadIdx.x & 63) == 0) g_c51_w2[blockIdx.x][threadIdx.x >> 6] = wall_clock64()
+#define C51_W() if ((threadIdx.x & 63) == 0) g_c51_w[blockIdx.x][threadIdx.x >> 6] = wall_clock64()
+#else
+#define C51_T(k)
+#define C51_W()
+#define C51_W2()
+#endif
 template <class LS>
 __global__ __launch_bounds__(1024) void k_c51(C51Args a, LS ol, LS tl, C51Extra x) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -87,20 +130,30 @@ __global__ __launch_bounds__(1024) void k_c51(C51Args a, LS ol, LS tl, C51Extra 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = T >> 6;
   const bool on = lane < N;
   const float ninf = -__builtin_inff();
+  C51_T(0);
   // every ordinary global load of the chain is issued here, before any LDS-DMA
   // (hipcc drains vmcnt to 0 at the first use of a plain load issued behind one)
   const float z = on ? a.support[lane] : 0.0f;
   const int ab = a.act[b];
   const float rew_b = a.rew[b], term_b = (float)a.term[b];
   const float vmin = a.support[0], vmax = a.support[N - 1], z1 = a.support[1];
-  const float pr_t = (a.probs && (int)threadIdx.x < a.B) ? a.probs[threadIdx.x] : 0.0f;
+  const float pr_t = a.probs ? a.probs[min((int)threadIdx.x, a.B - 1)] : 0.0f;
   const float pr_b = a.probs ? a.probs[b] : 0.0f;
-  const float hv = (x.w2 && (int)threadIdx.x < x.H) ? x.h[(int64_t)b * x.H + threadIdx.x] : 0.0f;
-  // the chosen online logit row, issued with the target rows (wave 0 uses it last)
-  const float y = (wave == 0 && on) ? ol.get(((int64_t)b * A + ab) * N + lane) : ninf;
+  const float hv = x.w2 ? x.h[(int64_t)b * x.H + min((int)threadIdx.x, x.H - 1)] : 0.0f;
+  // the chosen online logit row (wave 0 uses it last) and the first target row of each
+  // wave (nw <= A): loaded by every lane at clamped indices, so both rows' loads sit in one
+  // basic block and are all in flight before the first wait
+  const int lc = min(lane, N - 1);
+  const float x0 = tl.get(((int64_t)b * A + wave) * N + lc);   // (not behind act[b])
+  float y = ninf;
+  if (wave == 0) {            // (the vector-memory issue of 16-band rows is what costs)
+    const float y0 = ol.get(((int64_t)b * A + ab) * N + lc);
+    y = on ? y0 : ninf;
+  }
   float xv[4];
+  xv[0] = on ? x0 : ninf;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
+  for (int r = 1; r < 4; ++r) {
     const int act = wave + r * nw;
     xv[r] = (act < A && on) ? tl.get(((int64_t)b * A + act) * N + lane) : ninf;
   }
@@ -110,8 +163,8 @@ __global__ __launch_bounds__(1024) void k_c51(C51Args a, LS ol, LS tl, C51Extra 
   {
     const float dz = __fsub_rn(z1, vmin);
     const float gt = __fmul_rn(a.cg, __fsub_rn(1.0f, term_b));
-    for (int j = wave; j < N; j += nw) {
-      const float zj = a.support[j];
+    for (int j = __builtin_amdgcn_readfirstlane(wave); j < N; j += nw) {
+      const float zj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(z), j));
       const float tzj = fminf(fmaxf(__fadd_rn(rew_b, __fmul_rn(gt, zj)), vmin), vmax);
       if (on) {
         float c = __fsub_rn(1.0f, __fdiv_rn(fabsf(__fsub_rn(tzj, z)), dz));
@@ -119,31 +172,60 @@ __global__ __launch_bounds__(1024) void k_c51(C51Args a, LS ol, LS tl, C51Extra 
       }
     }
   }
+  C51_W2();
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int act = wave + r * nw;
     if (act >= A) break;
     const float v = xv[r];
     if (x.tl_out && on) x.tl_out[((int64_t)b * A + act) * N + lane] = v;
-    const float mx = wave_max(v);
+    const float mx = fast_max(v);
     const float e = on ? expf(__fsub_rn(v, mx)) : 0.0f;
-    const float p = __fdiv_rn(e, wave_sum(e));
-    const float q = wave_sum(on ? __fmul_rn(z, p) : 0.0f);
+    const float p = __fdiv_rn(e, fast_sum(e));
+    const float q = fast_sum(on ? __fmul_rn(z, p) : 0.0f);
     if (on) s_p[act * N + lane] = p;
     if (lane == 0) s_q[act] = q;
+  }
+  C51_T(1);
+  C51_W();
+  // PER importance weights (rb:277-280): w_b = r(p_b) / max_i r(p_i), r(p) = 1 / sqrt(p + eps).
+  // r rounds monotonically (non-increasing), so max_i r(p_i) = r(min_i p_i) exactly: each
+  // wave's min joins the barrier that completes s_p and s_q.  Formed here, before the
+  // LDS-DMA below, so no wait on a plain load can drain it.
+  if (a.probs) {
+    float pm = pr_t;
+    for (int i = threadIdx.x + T; i < a.B; i += T) pm = fminf(pm, a.probs[i]);
+    pm = fast_min(pm);
+    if (lane == 0) s_red[wave] = pm;
+  }
+  // the chosen online row's softmax terms (wave 0), likewise before the LDS-DMA
+  float sh = 0.0f, ey = 0.0f, lse = 0.0f, py = 0.0f;
+  if (wave == 0) {
+    const float my = fast_max(y);
+    sh = on ? __fsub_rn(y, my) : 0.0f;
+    ey = on ? expf(sh) : 0.0f;
+    const float sy = fast_sum(ey);
+    lse = logf(sy);
+    py = __fdiv_rn(ey, sy);
   }
   if (x.ol_out)
     for (int act = wave; act < A; act += nw) {
       const int64_t i = ((int64_t)b * A + act) * N + lane;
       if (on) x.ol_out[i] = act == ab && wave == 0 ? y : ol.get(i);
     }
+  // s_p, s_q, s_c, s_red complete.  A bare barrier: __syncthreads' release fence would
+  // also wait for vmcnt(0), i.e. for the whole LDS-DMA just issued
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  C51_T(2);
   // fused d h: this sample's N contiguous W2 rows (N x H floats) stream into LDS by
   // LDS-DMA (global_load_lds, 1 KB per wave instruction, no registers), landing under
-  // the rest of the loss chain
-  if (x.w2) {
+  // the rest of the loss chain.  Issued by waves 1.. (wave 0 runs the chain) after the
+  // barrier, so neither the chain nor the barrier waits behind the issue.
+  if (x.w2 && (wave > 0 || nw == 1)) {
     const int bytes = N * x.H * 4, nq = (bytes + 1023) >> 10;
+    const int w0 = nw > 1 ? wave - 1 : 0, nwd = nw > 1 ? nw - 1 : 1;
     const char* src = reinterpret_cast<const char*>(x.w2 + (int64_t)ab * N * x.H);
-    for (int q = wave; q < nq; q += nw) {
+    for (int q = w0; q < nq; q += nwd) {
       const int off = min(q * 1024 + lane * 16, bytes - 16);   // the tail re-reads in-bounds bytes
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + off),
                                        (__attribute__((address_space(3))) void*)(
@@ -151,20 +233,14 @@ __global__ __launch_bounds__(1024) void k_c51(C51Args a, LS ol, LS tl, C51Extra 
                                        16, 0, 0);
     }
   }
-  __syncthreads();            // s_p, s_q, s_z complete
-  // PER importance weight (rb:277-280) from the probabilities loaded above
   float w = 1.0f;
   if (a.probs) {
-    float m = (int)threadIdx.x < a.B ? __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(pr_t, 1e-10f))) : 0.0f;
-    for (int i = threadIdx.x + T; i < a.B; i += T)
-      m = fmaxf(m, __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(a.probs[i], 1e-10f))));
-    m = wave_max(m);
-    if (lane == 0) s_red[wave] = m;
-    __syncthreads();
-    m = s_red[0];
-    for (int i = 1; i < nw; ++i) m = fmaxf(m, s_red[i]);
+    float pm = s_red[0];
+    for (int i = 1; i < nw; ++i) pm = fminf(pm, s_red[i]);
+    const float m = __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(pm, 1e-10f)));
     w = __fdiv_rn(__fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(pr_b, 1e-10f))), m);
   }
+  C51_T(3);
   const float gscale = __fmul_rn(w, __fdiv_rn(1.0f, (float)a.B));
   for (int act = wave; act < A; act += nw) {
     if (act == ab) continue;
@@ -172,23 +248,31 @@ __global__ __launch_bounds__(1024) void k_c51(C51Args a, LS ol, LS tl, C51Extra 
   }
   // greedy target action (first max) and Tz, redundantly per wave (no barrier)
   int astar = 0;
-  float best = s_q[0];
-  for (int act = 1; act < A; ++act)
-    if (s_q[act] > best) {
-      best = s_q[act];
+  const float qv = lane < A ? s_q[lane] : 0.0f;   // one LDS read, then lane reads (A <= 64)
+  float best = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qv), 0));
+  for (int act = 1; act < A; ++act) {
+    const float qa = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qv), act));
+    if (qa > best) {
+      best = qa;
       astar = act;
     }
+  }
   const float* pst = s_p + astar * N;
   if (wave == 0) {
     float proj = 0.0f;        // sum_j c(i, j) p_j in j order (rb:340-494)
-    if (on)
-      for (int j = 0; j < N; ++j) proj = __fadd_rn(proj, __fmul_rn(s_c[j * kWave + lane], pst[j]));
-    const float my = wave_max(y);
-    const float sh = on ? __fsub_rn(y, my) : 0.0f;
-    const float ey = on ? expf(sh) : 0.0f;
-    const float sy = wave_sum(ey);
-    const float loss = wave_sum(on ? __fmul_rn(proj, __fsub_rn(logf(sy), sh)) : 0.0f);
-    const float gr = on ? __fmul_rn(gscale, __fsub_rn(__fdiv_rn(ey, sy), proj)) : 0.0f;
+    if (on) {
+      int j = 0;
+      for (; j + 8 <= N; j += 8) {      // 8 terms' LDS reads in flight, then summed in j order
+        float t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = __fmul_rn(s_c[(j + u) * kWave + lane], pst[j + u]);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) proj = __fadd_rn(proj, t[u]);
+      }
+      for (; j < N; ++j) proj = __fadd_rn(proj, __fmul_rn(s_c[j * kWave + lane], pst[j]));
+    }
+    const float loss = fast_sum(on ? __fmul_rn(proj, __fsub_rn(lse, sh)) : 0.0f);
+    const float gr = on ? __fmul_rn(gscale, __fsub_rn(py, proj)) : 0.0f;
     if (on) {
       a.grad[((int64_t)b * A + ab) * N + lane] = gr;
       s_g[lane] = gr;
@@ -198,17 +282,38 @@ __global__ __launch_bounds__(1024) void k_c51(C51Args a, LS ol, LS tl, C51Extra 
       if (a.prio_out) a.prio_out[b] = __fsqrt_rn(__fadd_rn(loss, 1e-10f));
     }
   }
+  C51_T(4);
   if (!x.w2) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's LDS-DMA has landed
   __syncthreads();
+  C51_T(5);
   // d h[b][j] = (h[b][j] > 0) * sum_i g_i W2[ab*N + i][j], i in order
   for (int j = threadIdx.x; j < x.H; j += T) {
     const float m = j == (int)threadIdx.x ? hv : x.h[(int64_t)b * x.H + j];
     float acc = 0.0f;
-    for (int i = 0; i < N; ++i) acc = __fadd_rn(acc, __fmul_rn(s_g[i], s_w[i * x.H + j]));
+    int i = 0;
+    for (; i + 8 <= N; i += 8) {
+      float t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = __fmul_rn(s_g[i + u], s_w[(i + u) * x.H + j]);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc = __fadd_rn(acc, t[u]);
+    }
+    for (; i < N; ++i) acc = __fadd_rn(acc, __fmul_rn(s_g[i], s_w[i * x.H + j]));
     x.dh[(int64_t)b * x.H + j] = m > 0.0f ? acc : 0.0f;
   }
+  C51_T(6);
 }
+#ifdef DQ_C51_PROF
+extern "C" int dq_debug_c51_times(long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_c51_t), sizeof(g_c51_t)) == hipSuccess ? 0 : -1;
+}
+extern "C" int dq_debug_c51_wave_times(long long* out) {
+  if (hipMemcpyFromSymbol(out + 256 * 16, HIP_SYMBOL(g_c51_w2), sizeof(g_c51_w2)) != hipSuccess)
+    return -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_c51_w), sizeof(g_c51_w)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 // dynamic LDS of k_c51 (bytes), with the fused path's W2 rows when they fit the prefetch
 static size_t c51_lds(int A, int N, int H) {
@@ -501,7 +606,7 @@ int dq_c51_loss_fused(const float* online_parts, const float* online_bias,
   DQ_CHECK_ARG(online_parts && online_bias && target_parts && target_bias && actions && rewards &&
                    terminals && support && grad_logits,
                "null argument");
-  DQ_CHECK_ARG(n_parts >= 1, "n_parts must be >= 1");
+  DQ_CHECK_ARG(n_parts >= 1 && n_parts <= 16, "n_parts must be in [1, 16]");
   DQ_CHECK_ARG(num_atoms >= 2 && num_atoms <= 64, "num_atoms must be in [2, 64]");
   DQ_CHECK_ARG(batch >= 1 && num_actions >= 1 && num_actions <= 256, "bad batch / num_actions");
   DQ_CHECK_ARG(!fc2_w || (h && dh && hidden >= 1), "d h needs h, dh and hidden");
