@@ -118,6 +118,9 @@ class DQNAgent(object):
     self._device = _device_of(tf_device, device)
     self._seed = seed
     self._pg = process_group
+    self._pg_conv = None           # a second communicator for the conv bucket (see _split_step)
+    self._fc_pending = None        # event: the previous step's fc all-reduce + update are done
+    self._defer_fc = False         # set by train_gradient_steps (learner-only loop)
     self.use_hip_graph = use_hip_graph
     self.pipeline = pipeline
     self.use_hip_cnn = use_hip_cnn
@@ -292,13 +295,15 @@ class DQNAgent(object):
       return self._fused_loss(t, c)
     return self._online_loss(t, self._ptgt[c])
 
-  def _forward_ride(self, c):
-    """The online forward of slot c with the target network's tail (ride mode)."""
+  def _forward_ride(self, c, part=None):
+    """The online forward of slot c with the target network's tail (ride mode).
+    part: 'convs' / 'fcs' -- the fused path's conv / fc launches only."""
     from dopamine_amd import cnn
     if self._fused():
       cnn.forward_fused(self._hip['online'], self._pbuf[c]['state'], self._hip['target'][c],
-                        conv3_b=self._head_from() == 5)
+                        conv3_b=self._head_from() == 5, part=part)
       return
+    assert part is None
     on, tg = cnn.forward_with_tail(self._hip['online'], self._pbuf[c]['state'], self._hip['target'][c])
     self._online_ready = on
     self._ptgt[c] = self._target_dict(tg)
@@ -392,12 +397,22 @@ class DQNAgent(object):
   def _split_allreduce(self):
     return self._pg is not None and self._hip is not None and not self._fused_opt()
 
-  def _grad_step_head(self, c, k, pipe=None):
+  def _head_splits(self):
+    """The N > 1 head graph splits before fc1's forward (fused Rainbow path), so the
+    previous step's fc all-reduce + update may still run under the conv launches."""
+    return self._fused() and self._rides()
+
+  def _grad_step_head(self, c, k, pipe=None, part=None):
+    """part None: the whole head; 'a': up to the conv forward; 'b': the rest."""
     pipe = self.pipeline if pipe is None else pipe
-    if not pipe:
-      self._prefetch(c)
+    if part != 'b':
+      if not pipe:
+        self._prefetch(c)
+      if part == 'a':
+        self._forward_ride(c, part='convs')
+        return
     if self._rides():
-      self._forward_ride(c)
+      self._forward_ride(c, part='fcs' if part == 'b' else None)
     elif self._pairs():
       self._forward_pair(c)
     y, g = self._loss(self._pbuf[c], c)
@@ -446,18 +461,45 @@ class DQNAgent(object):
     o = fp.offsets['fc1_w'][0]
     return fp.grad[o:], fp.grad[:o]           # fc1 + fc2 (final after the head), convs
 
-  def _split_step(self, head, tail, opt, k=0):
+  def _join_fc(self):
+    """The main stream waits for a deferred fc all-reduce + update (_split_step)."""
+    if self._fc_pending is not None:
+      torch.cuda.current_stream(self._device).wait_event(self._fc_pending)
+      self._fc_pending = None
+
+  def _conv_group(self):
+    """A second communicator over the same ranks: its all-reduce is not queued behind
+    the fc bucket's on the first one's internal stream.  Created on first use, which
+    every rank reaches at the same step."""
+    if self._pg_conv is None:
+      import torch.distributed as dist
+      self._pg_conv = dist.new_group(ranks=dist.get_process_group_ranks(self._pg),
+                                     backend=dist.get_backend(self._pg))
+    return self._pg_conv
+
+  def _split_step(self, head_a, head_b, tail, opt, k=0):
     """head | tail on the main stream with the fc bucket's all-reduce on the comm
     stream beside the tail; with TF1 Adam the fc parameters' update follows their
     all-reduce on the comm stream (hidden under the conv bucket's all-reduce) and
     only the conv parameters' update (which advances the beta powers) is left
-    after the join: same arithmetic, split in two launches (dq_adam_tf1_part)."""
+    after the join: same arithmetic, split in two launches (dq_adam_tf1_part).
+    In the learner-only loop (_defer_fc, fused Rainbow head split in head_a | head_b)
+    the join moves to the next step, between its conv and fc forward launches: the
+    fc all-reduce then runs under this step's tail AND the next step's convs, and
+    the conv bucket goes over a second communicator so it does not wait behind it.
+    Every launch keeps its inputs: the next step's convs read no fc parameter, its
+    fc launches wait for the update, and Adam's beta-power slots alternate (the fc
+    part reads slot k while the conv part writes slot 1 - k)."""
     main = torch.cuda.current_stream(self._device)
     fc, conv = self._grad_buckets()
     split_opt = isinstance(self._opt, ops.TF1Adam)
+    defer = self._defer_fc and split_opt and head_a is not None
     grad = self.online_convnet.fp.grad
     o = grad.numel() - fc.numel()
-    head()
+    if head_a is not None:
+      head_a()
+    self._join_fc()
+    head_b()
     ev = torch.cuda.Event()
     ev.record(main)
     self._comm.wait_event(ev)
@@ -466,8 +508,13 @@ class DQNAgent(object):
       if split_opt:
         self._opt.step_part(grad, o, grad.numel(), slot=k, bump=False)
     tail()
-    parallel.allreduce_mean_(conv, self._pg)
-    main.wait_stream(self._comm)
+    if defer:
+      parallel.allreduce_mean_(conv, self._conv_group())
+      self._fc_pending = torch.cuda.Event()
+      self._fc_pending.record(self._comm)
+    else:
+      parallel.allreduce_mean_(conv, self._pg)
+      main.wait_stream(self._comm)
     if split_opt:
       self._opt.step_part(grad, 0, o, slot=k, bump=True)
     else:
@@ -522,9 +569,14 @@ class DQNAgent(object):
     graphs = self._graph_sets.get(pipe)
     if self._split_allreduce():
       if graphs is not None:
-        self._split_step(*[g.replay for g in graphs[0][k]], k=k)
+        self._split_step(*[None if g is None else g.replay for g in graphs[0][k]], k=k)
+      elif self._head_splits():
+        self._split_step(lambda: self._grad_step_head(c, k, pipe, 'a'),
+                         lambda: self._grad_step_head(c, k, pipe, 'b'),
+                         lambda: self._grad_step_tail(c, k, pipe),
+                         lambda: self._device_opt_step(k), k=k)
       else:
-        self._split_step(lambda: self._grad_step_head(c, k, pipe),
+        self._split_step(None, lambda: self._grad_step_head(c, k, pipe),
                          lambda: self._grad_step_tail(c, k, pipe),
                          lambda: self._device_opt_step(k), k=k)
         self._eager_steps[pipe] += 1
@@ -564,13 +616,21 @@ class DQNAgent(object):
     if self._split_allreduce():
       for k in (0, 1):
         c = k
-        parts = [torch.cuda.CUDAGraph() for _ in range(3)]
-        fns = (lambda: self._grad_step_head(c, k, pipe), lambda: self._grad_step_tail(c, k, pipe),
-               lambda: self._device_opt_step(k))
-        for gr, fn in zip(parts, fns):
-          with torch.cuda.graph(gr, pool=pool):
-            fn()
-          pool = gr.pool()
+        if self._head_splits():
+          fns = (lambda: self._grad_step_head(c, k, pipe, 'a'),
+                 lambda: self._grad_step_head(c, k, pipe, 'b'))
+        else:
+          fns = (None, lambda: self._grad_step_head(c, k, pipe))
+        fns += (lambda: self._grad_step_tail(c, k, pipe), lambda: self._device_opt_step(k))
+        parts = []
+        for fn in fns:
+          gr = None
+          if fn is not None:
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr, pool=pool):
+              fn()
+            pool = gr.pool()
+          parts.append(gr)
         graphs.append(parts)
       self._graph_pool = pool
       self._graph_sets[pipe] = (graphs, [])
@@ -594,6 +654,7 @@ class DQNAgent(object):
     self._graph_sets[pipe] = (graphs, graphs_opt)
 
   def _sync_target(self):
+    self._join_fc()
     ops.sync_copy(self.target_convnet.fp.flat, self.online_convnet.fp.flat)
     if self.pipeline and self._has_prefetch and self._rides():   # the prefetched head is stale
       self._hip['target'][self._slot].forward_head(self._pbuf[self._slot]['next_state'])
@@ -697,6 +758,14 @@ class DQNAgent(object):
     once per chunk); the steps, their order, RNG use and target syncs are exactly
     those of the per-call loop (tests/test_gpu_agent.py)."""
     n = int(n)
+    self._defer_fc = True
+    try:
+      self._train_gradient_steps(n)
+    finally:
+      self._defer_fc = False
+      self._join_fc()
+
+  def _train_gradient_steps(self, n):
     while n > 0:
       K = self._UNROLL
       if n >= K and self._chunk_ok():

@@ -1182,18 +1182,21 @@ struct FwdOps {
 // its fc1 slabs (if fc1_1) in net 0's fc1 launch and its fused head beside net 0's:
 // 5 launches.  The logits are summed by dq_c51_loss_fused.
 void forward_fused(Ctx& c0, Ctx& c1, const FwdOps& f0, const FwdOps& f1, bool fc1_1,
-                   bool conv3_1 = false) {
+                   bool conv3_1 = false, bool convs = true, bool fcs = true) {
   const size_t n0 = FwdOps::fused_ws_floats(f0.B, f0.p->n_out);
   const size_t n1 = FwdOps::fused_ws_floats(f1.B, f1.p->n_out);
   c0.need = n0 > c0.need ? n0 : c0.need;
   c1.need = n1 > c1.need ? n1 : c1.need;
   if (c0.dry) return;
-  if (conv3_1)                       // net 1's conv3 (head_from = 5) beside net 0's conv1
-    group(c0, f0.conv1<false>(), f1.conv3());
-  else
-    group(c0, f0.conv1<false>());    // single-round launches: fetch early
-  group(c0, f0.conv2<false>());
-  group(c0, f0.conv3<false>());
+  if (convs) {
+    if (conv3_1)                     // net 1's conv3 (head_from = 5) beside net 0's conv1
+      group(c0, f0.conv1<false>(), f1.conv3());
+    else
+      group(c0, f0.conv1<false>());  // single-round launches: fetch early
+    group(c0, f0.conv2<false>());
+    group(c0, f0.conv3<false>());
+  }
+  if (!fcs) return;
   if (fc1_1)
     group(c0, f0.fc1<DQ_F4_LATE>(), f1.fc1<DQ_F4_LATE>());
   else
@@ -1559,8 +1562,9 @@ int dq_cnn_forward_fused(const dq_cnn_params* p0, const float* x0, dq_cnn_acts* 
                "the Nature CNN takes 84x84x4 NHWC input");
   DQ_CHECK_ARG(ws0 != ws1, "the two networks need separate workspaces");
   Ctx c0{(hipStream_t)stream, ws0, false, 0}, c1{(hipStream_t)stream, ws1, false, 0};
+  DQ_CHECK_ARG((fc1_1 & 12) != 12, "flags 4 (convs only) and 8 (fc layers only) exclude each other");
   forward_fused(c0, c1, FwdOps{p0, x0, a0, ws0, batch}, FwdOps{p1, nullptr, a1, ws1, batch},
-                (fc1_1 & 1) != 0, (fc1_1 & 2) != 0);
+                (fc1_1 & 1) != 0, (fc1_1 & 2) != 0, (fc1_1 & 8) == 0, (fc1_1 & 4) == 0);
   DQ_CHECK_LAUNCH("dq_cnn_forward_fused");
   return DQ_OK;
 }

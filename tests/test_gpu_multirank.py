@@ -5,7 +5,9 @@ ranks sharing cuda:0 over gloo (which all-reduces CUDA tensors).
 * identical seeds on both ranks: the mean gradient equals each rank's own
   ((g + g) / 2 is exact in fp32), so after K steps the parameters must equal a
   single-process agent's BIT FOR BIT -- this pins the whole N > 1 schedule;
-* different seeds: the replicas stay bit-identical (checksum broadcast)."""
+* different seeds: the replicas stay bit-identical (checksum broadcast);
+* the learner-only loop (train_gradient_steps), whose fc all-reduce + update is
+  joined in the next step, between its conv and fc launches: bitwise the same."""
 import os
 import socket
 
@@ -35,15 +37,18 @@ def _agent(pg, seed):
   return agent
 
 
-def _run(agent):
-  for _ in range(STEPS):
-    for _ in range(agent.update_period):
-      agent._train_step()
+def _run(agent, loop=False):
+  if loop:
+    agent.train_gradient_steps(STEPS)
+  else:
+    for _ in range(STEPS):
+      for _ in range(agent.update_period):
+        agent._train_step()
   torch.cuda.synchronize()
   return agent.online_convnet.fp.flat.detach().cpu().clone()
 
 
-def _worker(rank, world, port, same_seed, q):
+def _worker(rank, world, port, same_seed, q, loop=False):
   import sys
   sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
   import torch.distributed as dist
@@ -53,7 +58,7 @@ def _worker(rank, world, port, same_seed, q):
   dist.init_process_group('gloo', rank=rank, world_size=world)
   from dopamine_amd import parallel
   agent = _agent(dist.group.WORLD, 0 if same_seed else rank)
-  flat = _run(agent)
+  flat = _run(agent, loop)
   ok = parallel.replicas_in_sync(agent.online_convnet.fp.flat)
   if rank == 0:
     q.put((ok, flat.numpy()))
@@ -69,11 +74,11 @@ def _free_port():
   return p
 
 
-def _two_ranks(same_seed):
+def _two_ranks(same_seed, loop=False):
   ctx = mp.get_context('spawn')
   q = ctx.Queue()
   port = _free_port()
-  procs = [ctx.Process(target=_worker, args=(r, 2, port, same_seed, q)) for r in range(2)]
+  procs = [ctx.Process(target=_worker, args=(r, 2, port, same_seed, q, loop)) for r in range(2)]
   for p in procs:
     p.start()
   ok, flat = q.get(timeout=400)
@@ -95,3 +100,11 @@ def test_two_ranks_same_seed_equal_single_learner_bitwise():
 def test_two_ranks_different_seeds_stay_in_sync():
   ok, _ = _two_ranks(same_seed=False)
   assert ok
+
+
+@pytest.mark.timeout(600)
+def test_two_ranks_learner_loop_equal_single_learner_bitwise():
+  ok, flat = _two_ranks(same_seed=True, loop=True)
+  assert ok
+  single = _run(_agent(None, 0)).numpy()
+  assert np.array_equal(flat, single)
