@@ -233,7 +233,7 @@ def forward_fused(a, xa, b, fc1_b=True, conv3_b=False, part=None):
   """The Rainbow fast path's forward (dq_cnn_forward_fused): ``a`` (online) on
   ``xa`` through fc1, ``b`` (target; conv1..conv3 already run, e.g. riding in the
   previous backward with head_from=4) from its fc1 slabs (if ``fc1_b``; with
-  ``conv3_b`` its conv3 too, beside ``a``'s conv1: head_from=5), then one
+  ``conv3_b`` its conv3 too, beside ``a``'s conv3: head_from=5), then one
   launch summing both nets' fc1 slabs and forming fc2's 16 k-band partials.
   Neither net's logits are stored: ``ops.c51_loss_fused`` sums the partials
   (bitwise the logits of ``forward``).  part='convs' / 'fcs': only the three conv

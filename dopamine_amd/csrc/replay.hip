@@ -46,7 +46,7 @@ namespace dq {
 constexpr int kTreeT = 1024;   // block of the block-parallel sum-tree kernels
 
 __global__ __launch_bounds__(kTreeT) void k_per_sample(ReplayView v, int B, int32_t* out) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kPerSampleLds];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kPerSampleParLds];
   per_sample_par<kTreeT>(v, B, out, lds);
 }
 

@@ -600,6 +600,11 @@ __device__ inline void sumtree_set_par(const ReplayView& v, const SetArgs& a, vo
   double* s_delta = (double*)lds;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   dq_replay_meta* meta = v.meta;
+  // the first chunk's (index, value) pairs load with the control block (clamped, no
+  // branch), so the tree loads wait on one memory round, not two
+  const int64_t l0 = a.n > 0 ? (lane < a.n ? lane : a.n - 1) : 0;
+  const int32_t pre_i = (a.indices && a.n > 0) ? a.indices[l0] : 0;
+  const float pre_v = a.n > 0 ? a.values[l0] : 0.0f;
   if (meta->status != 0) return;
   const int depth = v.depth;
   const int64_t base = meta->add_count;
@@ -610,8 +615,13 @@ __device__ inline void sumtree_set_par(const ReplayView& v, const SetArgs& a, vo
     int64_t idx = 0;
     float val = 0.0f;
     if (lane < m) {
-      idx = a.indices ? (int64_t)a.indices[c0 + lane] : pymod(base + c0 + lane, v.C);
-      val = a.values[c0 + lane];
+      if (c0 == 0) {
+        idx = a.indices ? (int64_t)pre_i : pymod(base + lane, v.C);
+        val = pre_v;
+      } else {
+        idx = a.indices ? (int64_t)a.indices[c0 + lane] : pymod(base + c0 + lane, v.C);
+        val = a.values[c0 + lane];
+      }
     }
     // the reference raises at the first negative value, after applying the earlier ones
     const bool badi = lane < m && (idx < 0 || idx >= ((int64_t)1 << depth));
@@ -684,18 +694,32 @@ __device__ inline void sumtree_set_par(const ReplayView& v, const SetArgs& a, vo
 }
 
 // Prioritized stratified sampling (prioritized_replay_buffer.py:152-170 /
-// sum_tree.py:99-139) with T threads: 32 lanes per stratum descend the tree 5
-// levels per round -- lane j of the group loads the left-child sum of subtree node
-// j (breadth-first), then the group walks the 5 levels through shuffles: 4 round
-// trips instead of 20 for a 2^20-leaf tree.  The retry loop for invalid draws is
-// the reference's sequential one (thread 0).
+// sum_tree.py:99-139) with T threads.  The tree's top kTopLevels levels (2047 nodes,
+// 16 KB) are read by the whole block in the same memory round as the control block,
+// and every stratum walks its first 10 levels in LDS; below them 32 lanes per
+// stratum descend 5 levels per round -- lane j of the group loads the left-child
+// sum of subtree node j (breadth-first), then the group walks the 5 levels through
+// shuffles: for a 2^20-leaf tree 2 dependent rounds instead of 4 (or 20).  The
+// retry loop for invalid draws is the reference's sequential one (thread 0).
+constexpr int kTopLevels = 11;
+constexpr int kPerSampleParLds = kPerSampleLds + ((1 << kTopLevels) - 1) * 8;
+
 template <int T>
 __device__ inline void per_sample_par(const ReplayView& v, int B, int32_t* out, void* lds) {
   static_assert(T % 32 == 0, "32-lane groups");
+  static_assert(kPerSampleLds % 8 == 0, "s_top alignment");
   int64_t* s_idx = (int64_t*)lds;
   uint8_t* s_ok = (uint8_t*)(s_idx + kMaxBatch);
+  double* s_top = (double*)((uint8_t*)lds + kPerSampleLds);
   const int t = threadIdx.x, g = t >> 5, j = t & 31;
   dq_replay_meta* meta = v.meta;
+  // the top levels first: their loads do not wait for the control block's
+  const int ktop = v.depth + 1 < kTopLevels ? v.depth + 1 : kTopLevels;
+  const int ntop = (1 << ktop) - 1;
+  constexpr int kTopR = ((1 << kTopLevels) - 1 + T - 1) / T;
+  double top[kTopR];
+#pragma unroll
+  for (int r = 0; r < kTopR; ++r) top[r] = v.tree[min(t + r * T, ntop - 1)];
   const int64_t add_count = meta->add_count;
   const int64_t pos0 = meta->tape_pos;
   const int64_t len = meta->tape_len;
@@ -714,6 +738,10 @@ __device__ inline void per_sample_par(const ReplayView& v, int B, int32_t* out, 
     for (int i = t; i < B; i += T) out[i] = 0;
     return;
   }
+#pragma unroll
+  for (int r = 0; r < kTopR; ++r)
+    if (t + r * T < ntop) s_top[t + r * T] = top[r];
+  __syncthreads();
   // subtree node j of the group: level offset l (0..4), position p within it
   const int l = 31 - __clz(j + 1), p = j + 1 - (1 << l);
   const double step = 1.0 / (double)B;        // np.linspace(0, 1, B + 1)
@@ -728,7 +756,16 @@ __device__ inline void per_sample_par(const ReplayView& v, int B, int32_t* out, 
       q = __dmul_rn(__dadd_rn(lo, __dmul_rn(__dsub_rn(hi, lo), u)), total);   // uniform * total
     }
     int64_t node = 0;                          // index at level d
-    for (int d = 0; d < v.depth; d += 5) {
+    for (int d = 0; d < ktop - 1; ++d) {       // children within the staged levels
+      const double lf = s_top[(2 << d) - 1 + 2 * node];
+      if (q < lf) {
+        node = 2 * node;
+      } else {
+        node = 2 * node + 1;
+        q = __dsub_rn(q, lf);
+      }
+    }
+    for (int d = ktop - 1; d < v.depth; d += 5) {
       const int lv = d + l + 1;                // level of the left child this lane fetches
       double left = 0.0;
       if (mine && j < 31 && lv <= v.depth)
@@ -807,7 +844,7 @@ struct RiderDesc {
 };
 static_assert(sizeof(RiderDesc) <= sizeof(dq_rider), "dq_rider too small");
 
-constexpr int kRiderLds = kSumtreeParLds > kPerSampleLds ? kSumtreeParLds : kPerSampleLds;
+constexpr int kRiderLds = kSumtreeParLds > kPerSampleParLds ? kSumtreeParLds : kPerSampleParLds;
 
 // Runs rider r as block blk of a launch with T >= 256 threads per block.
 template <int T>

@@ -327,7 +327,7 @@ int dq_cnn_backward_riders(const dq_cnn_params* p, const dq_cnn_params* g, int32
    dq_cnn_backward_riders(first 0)):
    dq_cnn_forward_fused: net 0 (online) conv1..fc1 and net 1's (target's) fc1 slabs (if fc1_1
    bit 0; its conv1..conv3 ran earlier, e.g. as head_from = 4 riders of the previous backward;
-   with bit 1 its conv3 runs here too, in net 0's conv1 launch: head_from = 5; bit 2: only the
+   with bit 1 its conv3 runs here too, in net 0's conv3 launch: head_from = 5; bit 2: only the
    three conv launches, bit 3: only the fc launches -- a data-parallel learner waits for the
    previous step's fc update in between), then
    ONE launch that sums both nets' fc1 slabs (+ bias, ReLU -> a->h) and stores fc2's 16 k-band
