@@ -1411,9 +1411,14 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
       };
       float* f0 = p->fc1_w;
       float* f3 = p->fc2_w;                          // fc1_w .. fc1_b (+ pad)
-      const int64_t third = ((f3 - f0) / 3) & ~(int64_t)3;
-      float* f1 = f0 + third;
-      float* f2 = f1 + third;
+#ifndef DQ_FC1_A      // fc1's Adam split points, in 24ths of the range
+#define DQ_FC1_A 8
+#endif
+#ifndef DQ_FC1_B
+#define DQ_FC1_B 16
+#endif
+      float* f1 = f0 + (((f3 - f0) * DQ_FC1_A / 24) & ~(int64_t)3);
+      float* f2 = f0 + (((f3 - f0) * DQ_FC1_B / 24) & ~(int64_t)3);
       if constexpr (kHeadFrom == 5) {
         // five launches: conv2's input gradient by sub-pixel class needs only da2, so
         // conv1's weight-gradient slabs join launch 4 and the three split-K sums end
