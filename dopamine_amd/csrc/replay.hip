@@ -72,7 +72,8 @@ __global__ __launch_bounds__(256) void k_gather_f32(ReplayView v, GatherOut g) {
   const int r = slot - b * 2 * S;
   const int which = r / S;
   const int k = r - which * S;
-  if (blockIdx.x == 0 && which == 0 && k == 0 && threadIdx.x < 64) write_scalars_wave(v, g, b);
+  if (blockIdx.x == 0 && which == 0 && k == 0 && threadIdx.x < 64)
+    write_scalars_wave(v, g, b, pymod((int64_t)g.indices[b], v.C));
   float* dst_base = (float*)(which ? g.next_state : g.state);
   if (!dst_base) return;
   const int64_t f = pymod(stack_base(v, g, b, which) - S + 1 + k, v.C);
@@ -95,7 +96,7 @@ __global__ __launch_bounds__(256) void k_gather_f32(ReplayView v, GatherOut g) {
 
 template <int R>
 __global__ __launch_bounds__(256) void k_gather_nhwc4(ReplayView v, GatherOut g) {
-  gather_nhwc4_body<R>(v, g, blockIdx.x, blockIdx.y, threadIdx.x);
+  gather_nhwc4_body<R, true>(v, g, blockIdx.x, blockIdx.y, threadIdx.x);
 }
 
 __device__ __forceinline__ int64_t frame_of(const ReplayView& v, const GatherOut& g, int slot,
@@ -116,7 +117,8 @@ __global__ __launch_bounds__(256) void k_gather_raw(ReplayView v, GatherOut g) {
   int b, which, k;
   const int slot = blockIdx.y;
   const int64_t f = frame_of(v, g, slot, &b, &which, &k);
-  if (blockIdx.x == 0 && threadIdx.x < 64 && which == 0 && k == 0) write_scalars_wave(v, g, b);
+  if (blockIdx.x == 0 && threadIdx.x < 64 && which == 0 && k == 0)
+    write_scalars_wave(v, g, b, pymod((int64_t)g.indices[b], v.C));
   uint8_t* dst_base = (uint8_t*)(which ? g.next_state : g.state);
   if (!dst_base) return;
   const uint8_t* src = v.frames + f * v.obs_bytes;

@@ -314,9 +314,9 @@ __device__ __forceinline__ int64_t stack_base(const ReplayView& v, const GatherO
 // usual L = n together with the trajectory and re-read only when a terminal
 // cuts it short, so the wave waits on two dependent loads (index, then
 // everything else), not three.
-__device__ inline void write_scalars_wave(const ReplayView& v, const GatherOut& g, int b) {
+__device__ inline void write_scalars_wave(const ReplayView& v, const GatherOut& g, int b,
+                                          int64_t idx) {
   const int lane = threadIdx.x & 63;
-  const int64_t idx = pymod((int64_t)g.indices[b], v.C);
   float p = 0.0f;
   bool t = false;
   // independent of L: issued with the trajectory
@@ -395,18 +395,26 @@ __device__ __forceinline__ float4 u8x4_to_f32_255(uint32_t w) {
 // pixels) of each of the 4 frames -- all 4R loads in flight together -- and
 // writes 4 pixels x 4 channels = 64 contiguous bytes per lane per store.
 // (bx, slot) = the block's coordinates in the (column blocks, 2B) grid; tid in [0, 256).
-template <int R>
+// kLateScalars: the scalars wave issues its frame loads first (standalone kernel: 6.5 ->
+// 5.6 us at B = 32).  Riders keep the early form: the late one's live frame registers
+// raise the grouped launch's VGPR count (-1% per learner step, measured).
+template <int R, bool kLateScalars = false>
 __device__ __forceinline__ void gather_nhwc4_body(const ReplayView& v, const GatherOut& g, int bx,
                                                   int slot, int tid) {
   const int b = slot >> 1, which = slot & 1;
-  if (bx == 0 && which == 0 && tid < 64) write_scalars_wave(v, g, b);
+  // one wave per sample also writes the scalars: after issuing its frame loads, so its
+  // scalar loads share their memory round (the kernel waits for its slowest wave)
+  const bool scal = bx == 0 && which == 0 && tid < 64;
+  if (!kLateScalars && scal) write_scalars_wave(v, g, b, pymod((int64_t)g.indices[b], v.C));
   float* dst_base = (float*)(which ? g.next_state : g.state);
-  if (!dst_base) return;
   const int64_t nd = v.obs_bytes >> 2;
   const int lane = tid & 63;
   // this wave's R x 64 dwords of each of the 4 frames
   const int64_t w0 = ((int64_t)bx * 256 + (tid & ~63)) * R;
-  if (w0 >= nd) return;
+  if (!dst_base || w0 >= nd) {
+    if (kLateScalars && scal) write_scalars_wave(v, g, b, pymod((int64_t)g.indices[b], v.C));
+    return;
+  }
   // next_state's stack ends at idx + L (L = n-step length, crb:517-531).  Its
   // frames are loaded for the usual L = n together with the trajectory's
   // terminal bytes and re-loaded only when a terminal makes L < n (wave-uniform
@@ -433,6 +441,7 @@ __device__ __forceinline__ void gather_nhwc4_body(const ReplayView& v, const Gat
     if (base != spec) load(base);
   } else {
     load(idx);
+    if (kLateScalars && scal) write_scalars_wave(v, g, b, idx);
   }
   // store j of chunk r: lane l writes pixel 64j + l of the chunk (its 4 channels =
   // 16 B), so every store instruction covers 1 KiB contiguous; the bytes come from
