@@ -123,8 +123,8 @@ SIGNATURES = {
                                ctypes.POINTER(Rider), _I32, ctypes.POINTER(AdamArgs),
                                ctypes.POINTER(CnnNet), _I32, _I32, _I32, _P],
     'dq_cnn_forward_fused': [ctypes.POINTER(CnnParams), _P, ctypes.POINTER(CnnActs), _P,
-                             ctypes.POINTER(CnnParams), ctypes.POINTER(CnnActs), _P, _I32, _I32,
-                             _P],
+                             ctypes.POINTER(CnnParams), _P, ctypes.POINTER(CnnActs), _P, _I32,
+                             _I32, _P],
     'dq_cnn_fc2_parts_offset': [_I32],
     'dq_c51_loss_fused': [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _I32, _I32, _I32, _F, _P, _P,
                           _P, _P, _P, _P, _I32, _P, _P, _P],

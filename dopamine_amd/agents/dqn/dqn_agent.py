@@ -300,8 +300,10 @@ class DQNAgent(object):
     part: 'convs' / 'fcs' -- the fused path's conv / fc launches only."""
     from dopamine_amd import cnn
     if self._fused():
+      hf = self._head_from()
       cnn.forward_fused(self._hip['online'], self._pbuf[c]['state'], self._hip['target'][c],
-                        conv3_b=self._head_from() == 5, part=part)
+                        conv3_b=hf >= 5, conv2_b=hf >= 6, part=part,
+                        xb=self._pbuf[c]['next_state'] if hf == 7 else None)
       return
     assert part is None
     on, tg = cnn.forward_with_tail(self._hip['online'], self._pbuf[c]['state'], self._hip['target'][c])
@@ -313,8 +315,11 @@ class DQNAgent(object):
 
   def _head_from(self):
     """The backward's schedule: 7 launches with the target head from launch 3, or
-    (fused) 5 launches from launch 1, the target's conv3 left to forward_fused."""
-    return 5 if self._fused() else 3
+    (fused) 5 launches from launch 1 with the target's conv1 in the last one and its
+    conv2 / conv3 beside the online conv2 / conv3 of the next forward (measured: +1.4%
+    over conv1, conv2 in the backward's launches 4, 5 (head_from 5); -0.7% with conv1
+    in the next forward too (7))."""
+    return 6 if self._fused() else 3
 
   def _pairs(self):
     return self.pair_forward and self._hip is not None and not self._rides()

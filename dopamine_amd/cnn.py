@@ -229,7 +229,7 @@ def fc2_parts(net):
   return net.ws[off:off + n].view(16, net.B, net.n_out)
 
 
-def forward_fused(a, xa, b, fc1_b=True, conv3_b=False, part=None):
+def forward_fused(a, xa, b, fc1_b=True, conv3_b=False, part=None, conv2_b=False, xb=None):
   """The Rainbow fast path's forward (dq_cnn_forward_fused): ``a`` (online) on
   ``xa`` through fc1, ``b`` (target; conv1..conv3 already run, e.g. riding in the
   previous backward with head_from=4) from its fc1 slabs (if ``fc1_b``; with
@@ -237,14 +237,18 @@ def forward_fused(a, xa, b, fc1_b=True, conv3_b=False, part=None):
   launch summing both nets' fc1 slabs and forming fc2's 16 k-band partials.
   Neither net's logits are stored: ``ops.c51_loss_fused`` sums the partials
   (bitwise the logits of ``forward``).  part='convs' / 'fcs': only the three conv
-  launches / only the fc launches (the same launches in two calls).  Returns the two
+  launches / only the fc launches (the same launches in two calls).  conv2_b / xb:
+  ``b``'s conv2 beside ``a``'s conv2 (head_from=6) / ``b``'s conv1 on ``xb`` beside
+  ``a``'s conv1 (head_from=7: no target head in the backward).  Returns the two
   partial views."""
   assert a.B == b.B and a is not b
   xa = a._nhwc(xa)
   a._x = xa
   _lib.check(_lib.lib.dq_cnn_forward_fused(
       ctypes.byref(a._p), xa.data_ptr(), ctypes.byref(a._a), a.ws.data_ptr(),
-      ctypes.byref(b._p), ctypes.byref(b._a), b.ws.data_ptr(), a.B,
-      int(bool(fc1_b)) | 2 * int(bool(conv3_b)) | {None: 0, 'convs': 4, 'fcs': 8}[part],
+      ctypes.byref(b._p), None if xb is None else b._nhwc(xb).data_ptr(), ctypes.byref(b._a),
+      b.ws.data_ptr(), a.B,
+      int(bool(fc1_b)) | 2 * int(bool(conv3_b)) | {None: 0, 'convs': 4, 'fcs': 8}[part] |
+      16 * int(bool(conv2_b)) | 32 * int(xb is not None),
       a._stream(xa)), 'dq_cnn_forward_fused')
   return fc2_parts(a), fc2_parts(b)

@@ -1182,7 +1182,8 @@ struct FwdOps {
 // its fc1 slabs (if fc1_1) in net 0's fc1 launch and its fused head beside net 0's:
 // 5 launches.  The logits are summed by dq_c51_loss_fused.
 void forward_fused(Ctx& c0, Ctx& c1, const FwdOps& f0, const FwdOps& f1, bool fc1_1,
-                   bool conv3_1 = false, bool convs = true, bool fcs = true) {
+                   bool conv3_1 = false, bool convs = true, bool fcs = true,
+                   bool conv2_1 = false, bool conv1_1 = false) {
   const size_t n0 = FwdOps::fused_ws_floats(f0.B, f0.p->n_out);
   const size_t n1 = FwdOps::fused_ws_floats(f1.B, f1.p->n_out);
   c0.need = n0 > c0.need ? n0 : c0.need;
@@ -1197,11 +1198,18 @@ void forward_fused(Ctx& c0, Ctx& c1, const FwdOps& f0, const FwdOps& f1, bool fc
 #ifndef DQ_F1_LATE
 #define DQ_F1_LATE false
 #endif
-    if (conv3_1 && DQ_T3_AT == 1)
+#ifndef DQ_F2_LATE       // the conv2 launch with the target's conv2: late fetch, +0.9%
+#define DQ_F2_LATE true
+#endif
+    if (conv1_1)                     // net 1's conv1 (head_from = 7) beside net 0's conv1
+      group(c0, f0.conv1<DQ_F1_LATE>(), f1.conv1());
+    else if (conv3_1 && DQ_T3_AT == 1)
       group(c0, f0.conv1<DQ_F1_LATE>(), f1.conv3());
     else
       group(c0, f0.conv1<false>());  // single-round launches: fetch early
-    if (conv3_1 && DQ_T3_AT == 2)
+    if (conv2_1)                     // net 1's conv2 (head_from = 6) beside net 0's conv2
+      group(c0, f0.conv2<DQ_F2_LATE>(), f1.conv2());
+    else if (conv3_1 && DQ_T3_AT == 2)
       group(c0, f0.conv2<DQ_F1_LATE>(), f1.conv3());
     else
       group(c0, f0.conv2<false>());
@@ -1419,7 +1427,7 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
 #endif
       float* f1 = f0 + (((f3 - f0) * DQ_FC1_A / 24) & ~(int64_t)3);
       float* f2 = f0 + (((f3 - f0) * DQ_FC1_B / 24) & ~(int64_t)3);
-      if constexpr (kHeadFrom == 5) {
+      if constexpr (kHeadFrom >= 5) {
         // five launches: conv2's input gradient by sub-pixel class needs only da2, so
         // conv1's weight-gradient slabs join launch 4 and the three split-K sums end
         // the backward in launch 5, conv2 and conv1 applying Adam in their epilogues
@@ -1430,11 +1438,16 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
         if (in(1)) group_r(c, rd(1), dW_fc2, dX_fc1);
         if (in(2)) group_r(c, rd(2), dW_fc1, dX_c3, part(p->fc2_w, p->fc2_b + NO));
         if (in(3)) group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11, part(f0, f1));
-        if (head) {
+        if (head && kHeadFrom == 5) {
           if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, dW_c1, part(f1, f2), head->conv1());
           if (in(5))
             group_r(c, rd(5), sum_c2a, sum_c1, part(f2, f3), part(p->conv3_w, p->fc1_w),
                     head->conv2());
+        } else if (head) {   // 6: only conv1 here, conv2 and conv3 in the next forward
+          if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, dW_c1, part(f1, f2));
+          if (in(5))
+            group_r(c, rd(5), sum_c2a, sum_c1, part(f2, f3), part(p->conv3_w, p->fc1_w),
+                    head->conv1());
         } else {
           if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, dW_c1, part(f1, f2));
           if (in(5)) group_r(c, rd(5), sum_c2a, sum_c1, part(f2, f3), part(p->conv3_w, p->fc1_w));
@@ -1468,11 +1481,14 @@ if constexpr (kHeadFrom == 4) {
   if (in(0)) group_r(c, rd(0), dX_fc2);
   if (in(1)) group_r(c, rd(1), dW_fc2, dX_fc1);
   if (in(2)) group_r(c, rd(2), dW_fc1, dX_c3);
-  if constexpr (kHeadFrom == 5) {
+  if constexpr (kHeadFrom >= 5) {
     if (in(3)) group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11);
-    if (head) {
+    if (head && kHeadFrom == 5) {
       if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, dW_c1, head->conv1());
       if (in(5)) group_r(c, rd(5), sum_c2, sum_c1, head->conv2());
+    } else if (head) {
+      if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, dW_c1);
+      if (in(5)) group_r(c, rd(5), sum_c2, sum_c1, head->conv1());
     } else {
       if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, dW_c1);
       if (in(5)) group_r(c, rd(5), sum_c2, sum_c1);
@@ -1574,16 +1590,18 @@ int dq_cnn_forward_with_tail(const dq_cnn_params* p0, const float* x0, dq_cnn_ac
 }
 
 int dq_cnn_forward_fused(const dq_cnn_params* p0, const float* x0, dq_cnn_acts* a0, float* ws0,
-                         const dq_cnn_params* p1, dq_cnn_acts* a1, float* ws1, int32_t batch,
-                         int32_t fc1_1, void* stream) {
+                         const dq_cnn_params* p1, const float* x1, dq_cnn_acts* a1, float* ws1,
+                         int32_t batch, int32_t fc1_1, void* stream) {
   DQ_CHECK_ARG(p0 && a0 && x0 && ws0 && p1 && a1 && ws1 && batch >= 1, "null argument");
   DQ_CHECK_ARG(p0->in_channels == 4 && p1->in_channels == 4 && p0->n_out >= 1 && p1->n_out >= 1,
                "the Nature CNN takes 84x84x4 NHWC input");
   DQ_CHECK_ARG(ws0 != ws1, "the two networks need separate workspaces");
   Ctx c0{(hipStream_t)stream, ws0, false, 0}, c1{(hipStream_t)stream, ws1, false, 0};
   DQ_CHECK_ARG((fc1_1 & 12) != 12, "flags 4 (convs only) and 8 (fc layers only) exclude each other");
-  forward_fused(c0, c1, FwdOps{p0, x0, a0, ws0, batch}, FwdOps{p1, nullptr, a1, ws1, batch},
-                (fc1_1 & 1) != 0, (fc1_1 & 2) != 0, (fc1_1 & 8) == 0, (fc1_1 & 4) == 0);
+  DQ_CHECK_ARG(!(fc1_1 & 32) || x1, "flag 32 (net 1's conv1) needs x1");
+  forward_fused(c0, c1, FwdOps{p0, x0, a0, ws0, batch}, FwdOps{p1, x1, a1, ws1, batch},
+                (fc1_1 & 1) != 0, (fc1_1 & 2) != 0, (fc1_1 & 8) == 0, (fc1_1 & 4) == 0,
+                (fc1_1 & 16) != 0, (fc1_1 & 32) != 0);
   DQ_CHECK_LAUNCH("dq_cnn_forward_fused");
   return DQ_OK;
 }
@@ -1637,7 +1655,7 @@ int dq_cnn_backward_riders(const dq_cnn_params* p, const dq_cnn_params* g, int32
                "at most one rider per grouped launch (7)");
   DQ_CHECK_ARG(0 <= first && first <= last && last <= 7, "groups must satisfy 0 <= first <= last <= 7");
   DQ_CHECK_ARG(!opt || (first <= 1 && last == 7), "the fused optimizer needs the whole backward");
-  DQ_CHECK_ARG(head_from >= 3 && head_from <= 5, "head_from must be 3, 4 or 5");
+  DQ_CHECK_ARG(head_from >= 3 && head_from <= 7, "head_from must be in [3, 7]");
   RiderDesc r[7];
   for (int i = 0; i < n_riders; ++i) {
     memcpy(&r[i], &riders[i], sizeof(RiderDesc));
@@ -1655,7 +1673,13 @@ int dq_cnn_backward_riders(const dq_cnn_params* p, const dq_cnn_params* g, int32
   if (opt) {
     const int rc = check_adam(p, g, opt);
     if (rc != DQ_OK) return rc;
-    if (head_from == 5)
+    if (head_from == 7)       // the whole target head runs in the next forward
+      backward_grouped<true, 5>(c, p, g, batch, x, a, dout, d, AdamHost{opt}, first, last, r,
+                                n_riders, nullptr);
+    else if (head_from == 6)
+      backward_grouped<true, 6>(c, p, g, batch, x, a, dout, d, AdamHost{opt}, first, last, r,
+                                n_riders, hp);
+    else if (head_from == 5)
       backward_grouped<true, 5>(c, p, g, batch, x, a, dout, d, AdamHost{opt}, first, last, r,
                                 n_riders, hp);
     else if (head_from == 4)
@@ -1665,7 +1689,13 @@ int dq_cnn_backward_riders(const dq_cnn_params* p, const dq_cnn_params* g, int32
       backward_grouped<true>(c, p, g, batch, x, a, dout, d, AdamHost{opt}, first, last, r,
                              n_riders, hp);
   } else {
-    if (head_from == 5)
+    if (head_from == 7)
+      backward_grouped<false, 5>(c, p, g, batch, x, a, dout, d, AdamHost{nullptr}, first, last, r,
+                                 n_riders, nullptr);
+    else if (head_from == 6)
+      backward_grouped<false, 6>(c, p, g, batch, x, a, dout, d, AdamHost{nullptr}, first, last, r,
+                                 n_riders, hp);
+    else if (head_from == 5)
       backward_grouped<false, 5>(c, p, g, batch, x, a, dout, d, AdamHost{nullptr}, first, last, r,
                                  n_riders, hp);
     else if (head_from == 4)

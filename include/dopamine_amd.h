@@ -313,7 +313,9 @@ int dq_cnn_forward_with_tail(const dq_cnn_params* p0, const float* x0, dq_cnn_ac
    slabs then run in dq_cnn_forward_fused).  head_from = 5 selects the five-launch backward
    (launches 0..5; conv2's input gradient by sub-pixel class, the split-K sums of conv2 and
    conv1 both in launch 5) with the head's conv1 / conv2 in launches 4 / 5 and its conv3
-   and fc1 slabs left to dq_cnn_forward_fused (fc1_1 = 3).  Rider i rides in launch first + i.  Only
+   and fc1 slabs left to dq_cnn_forward_fused (fc1_1 = 3); head_from = 6: the head's conv1 in
+   launch 5 only, its conv2 too left to dq_cnn_forward_fused (fc1_1 = 19, the Rainbow agent's
+   default); 7: no head here at all (fc1_1 = 51 with x1 = the head's input).  Rider i rides in launch first + i.  Only
    launches [first, last) are issued (as dq_cnn_backward_groups; riders and head ops of
    other launches are skipped; opt needs [0, 7)).  CNN results are bitwise those of the
    separate calls. */
@@ -327,7 +329,9 @@ int dq_cnn_backward_riders(const dq_cnn_params* p, const dq_cnn_params* g, int32
    dq_cnn_backward_riders(first 0)):
    dq_cnn_forward_fused: net 0 (online) conv1..fc1 and net 1's (target's) fc1 slabs (if fc1_1
    bit 0; its conv1..conv3 ran earlier, e.g. as head_from = 4 riders of the previous backward;
-   with bit 1 its conv3 runs here too, in net 0's conv3 launch: head_from = 5; bit 2: only the
+   with bit 1 its conv3 runs here too, in net 0's conv3 launch: head_from = 5; bit 4 (16): its
+   conv2 in net 0's conv2 launch (head_from = 6); bit 5 (32): its conv1 on x1 in net 0's conv1
+   launch (head_from = 7; x1 may be NULL otherwise); bit 2: only the
    three conv launches, bit 3: only the fc launches -- a data-parallel learner waits for the
    previous step's fc update in between), then
    ONE launch that sums both nets' fc1 slabs (+ bias, ReLU -> a->h) and stores fc2's 16 k-band
@@ -337,8 +341,8 @@ int dq_cnn_backward_riders(const dq_cnn_params* p, const dq_cnn_params* g, int32
    (dq_cnn_backward_riders with first = 1, riders numbered from it): dq_c51_loss_fused also
    writes d h. */
 int dq_cnn_forward_fused(const dq_cnn_params* p0, const float* x0, dq_cnn_acts* a0, float* ws0,
-                         const dq_cnn_params* p1, dq_cnn_acts* a1, float* ws1, int32_t batch,
-                         int32_t fc1_1, void* stream);
+                         const dq_cnn_params* p1, const float* x1, dq_cnn_acts* a1, float* ws1,
+                         int32_t batch, int32_t fc1_1, void* stream);
 size_t dq_cnn_fc2_parts_offset(int32_t batch);
 /* one layer of the backward: layer 0..4 = fc2, fc1, conv3, conv2, conv1; part 1 = weight and
    bias gradient, part 0 = input gradient (not for conv1).  dW(L) depends only on dX(L-1),

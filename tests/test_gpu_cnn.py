@@ -197,12 +197,18 @@ def test_fused_forward_and_c51_equal_separate_path(B, A):
   _close(g7, ref_g, rtol=2e-5)
   # the five-launch schedule (head_from = 5): the same gradient bit for bit, the target
   # head's conv1/conv2 riding in launches 4/5 and its conv3 + fc1 slabs in forward_fused
+  # (head_from 6 / 7: its conv2 / conv1 too beside the online net's in forward_fused)
   nx2 = torch.rand(B, 84, 84, 4, device='cuda')
   ref_t2 = HipNatureCNN(tg, B).forward(nx2).clone()
-  on.fp.grad.fill_(float('nan'))
-  ho.backward(got['grad'].view(B, -1), groups=(1, 7), head=(ht, nx2), head_from=5)
-  forward_fused(ho, x, ht, conv3_b=True)
-  ops.c51_loss_fused(ho, ht, act, rew, term, sup, 0.970299, probs=probs, logits_out=True)
-  torch.cuda.synchronize()
-  assert torch.equal(torch.cat([v.reshape(-1) for v in on.fp.grad_views]), g7)
-  assert torch.equal(ht.acts['out'], ref_t2) and torch.equal(ho.acts['out'], ref_o)
+  dh0 = ho.dacts['h'].clone()      # the backward's input; each pass's loss rewrites it
+  for hf in (5, 6, 7):
+    ho.dacts['h'].copy_(dh0)
+    on.fp.grad.fill_(float('nan'))
+    for t in (ht.acts['a1'], ht.acts['a2'], ht.acts['a3'], ht.acts['out']):
+      t.fill_(float('nan'))
+    ho.backward(got['grad'].view(B, -1), groups=(1, 7), head=(ht, nx2), head_from=hf)
+    forward_fused(ho, x, ht, conv3_b=True, conv2_b=hf >= 6, xb=nx2 if hf == 7 else None)
+    ops.c51_loss_fused(ho, ht, act, rew, term, sup, 0.970299, probs=probs, logits_out=True)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.cat([v.reshape(-1) for v in on.fp.grad_views]), g7), hf
+    assert torch.equal(ht.acts['out'], ref_t2) and torch.equal(ho.acts['out'], ref_o), hf
