@@ -1437,17 +1437,27 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
         if (in(0)) group_r(c, rd(0), dX_fc2);
         if (in(1)) group_r(c, rd(1), dW_fc2, dX_fc1);
         if (in(2)) group_r(c, rd(2), dW_fc1, dX_c3, part(p->fc2_w, p->fc2_b + NO));
+        if (kHeadFrom == 6) {
+          // 6: conv2's weight-gradient slabs (they need only da2) beside conv3's in
+          // launch 3 (+0.9%), the head's conv1 in launch 5, its conv2 and conv3 in the
+          // next forward
+          if (in(3)) group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11, dW_c2, part(f0, f1));
+          if (in(4)) group_r(c, rd(4), sum_c3, dW_c1, part(f1, f2));
+          if (in(5)) {
+            if (head)
+              group_r(c, rd(5), sum_c2a, sum_c1, part(f2, f3), part(p->conv3_w, p->fc1_w),
+                      head->conv1());
+            else
+              group_r(c, rd(5), sum_c2a, sum_c1, part(f2, f3), part(p->conv3_w, p->fc1_w));
+          }
+          return;
+        }
         if (in(3)) group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11, part(f0, f1));
-        if (head && kHeadFrom == 5) {
+        if (head) {
           if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, dW_c1, part(f1, f2), head->conv1());
           if (in(5))
             group_r(c, rd(5), sum_c2a, sum_c1, part(f2, f3), part(p->conv3_w, p->fc1_w),
                     head->conv2());
-        } else if (head) {   // 6: only conv1 here, conv2 and conv3 in the next forward
-          if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, dW_c1, part(f1, f2));
-          if (in(5))
-            group_r(c, rd(5), sum_c2a, sum_c1, part(f2, f3), part(p->conv3_w, p->fc1_w),
-                    head->conv1());
         } else {
           if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, dW_c1, part(f1, f2));
           if (in(5)) group_r(c, rd(5), sum_c2a, sum_c1, part(f2, f3), part(p->conv3_w, p->fc1_w));
@@ -1482,13 +1492,21 @@ if constexpr (kHeadFrom == 4) {
   if (in(1)) group_r(c, rd(1), dW_fc2, dX_fc1);
   if (in(2)) group_r(c, rd(2), dW_fc1, dX_c3);
   if constexpr (kHeadFrom >= 5) {
+    if (kHeadFrom == 6) {            // as the Adam form: conv2's dW slabs in launch 3
+      if (in(3)) group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11, dW_c2);
+      if (in(4)) group_r(c, rd(4), sum_c3, dW_c1);
+      if (in(5)) {
+        if (head)
+          group_r(c, rd(5), sum_c2, sum_c1, head->conv1());
+        else
+          group_r(c, rd(5), sum_c2, sum_c1);
+      }
+      return;
+    }
     if (in(3)) group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11);
-    if (head && kHeadFrom == 5) {
+    if (head) {
       if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, dW_c1, head->conv1());
       if (in(5)) group_r(c, rd(5), sum_c2, sum_c1, head->conv2());
-    } else if (head) {
-      if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, dW_c1);
-      if (in(5)) group_r(c, rd(5), sum_c2, sum_c1, head->conv1());
     } else {
       if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, dW_c1);
       if (in(5)) group_r(c, rd(5), sum_c2, sum_c1);
