@@ -66,6 +66,20 @@ def fill_synthetic(mem, A, seed):
   del frames
 
 
+def build_agent(actions, capacity, batch, device, pg=None, **kw):
+  """The benchmarked learner: Rainbow as rainbow.gin binds it (n = 3, Adam 6.25e-5 /
+  1.5e-4, target period 8000, update period 4, PER), on the device's 1M buffer.
+  Every rank builds the same networks (seed 0; rank 0's are broadcast anyway)."""
+  from dopamine_amd.agents.optimizers import AdamOptimizer
+  from dopamine_amd.agents.rainbow.rainbow_agent import RainbowAgent
+  return RainbowAgent(num_actions=actions, update_horizon=3, gamma=0.99,
+                      replay_scheme='prioritized', min_replay_history=20000, update_period=4,
+                      target_update_period=8000,
+                      optimizer=AdamOptimizer(learning_rate=0.0000625, epsilon=0.00015),
+                      replay_capacity=capacity, batch_size=batch, device=device, seed=0,
+                      process_group=pg, **kw)
+
+
 def time_gather(agent, iters):
   """Average duration of the gather kernel, HIP events on the launch stream,
   back-to-back launches captured in a HIP graph (no host launch gaps)."""
@@ -155,16 +169,39 @@ def gather_traffic(batch):
     return None, None
 
 
+def host_cores():
+  """CPUs this process may run on: the affinity mask, capped by a cgroup CPU quota."""
+  n = len(os.sched_getaffinity(0))
+  try:
+    quota, period = open('/sys/fs/cgroup/cpu.max').read().split()[:2]
+    if quota != 'max':
+      n = min(n, max(1, -(-int(quota) // int(period))))
+  except (OSError, ValueError):
+    pass
+  return n
+
+
+def cpu_model():
+  try:
+    for line in open('/proc/cpuinfo'):
+      if line.startswith('model name'):
+        return line.split(':', 1)[1].strip()
+  except OSError:
+    pass
+  return platform.processor() or platform.machine()
+
+
 def cpu_baseline(seconds, A, batch):
   from oracle.cpu_step import CpuRainbowStep
-  threads = min(16, os.cpu_count() or 1)
+  threads = host_cores()
   torch.set_num_threads(threads)
   step = CpuRainbowStep(capacity=1_000_000, batch_size=batch, num_actions=A)
   rate, k, dt = step.time(seconds=seconds)
   return {'value': round(rate, 3), 'unit': 'gradient-steps/s', 'cores': threads, 'kind': 'port',
           'sample': '%d Rainbow steps (%.1f s): oracle numpy PER sampler on a 1M buffer + torch-CPU '
-                    'Nature-CNN fwd/bwd + oracle C51 loss + oracle TF1 Adam; host %s' %
-                    (k, dt, platform.processor() or platform.machine())}
+                    'Nature-CNN fwd/bwd (%d threads) + oracle C51 loss + oracle TF1 Adam; host: %s, '
+                    '%d CPUs available to this process (affinity/cgroup), %d online' %
+                    (k, dt, threads, cpu_model(), threads, os.cpu_count() or 0)}
 
 
 def main():
@@ -187,18 +224,10 @@ def main():
     else:
       dist.init_process_group('nccl', device_id=dev)
     pg = dist.group.WORLD
-  from dopamine_amd.agents.optimizers import AdamOptimizer
-  from dopamine_amd.agents.rainbow.rainbow_agent import RainbowAgent
-
-  agent = RainbowAgent(num_actions=args.actions, update_horizon=3, gamma=0.99,
-                       replay_scheme='prioritized', min_replay_history=20000, update_period=4,
-                       target_update_period=8000,
-                       optimizer=AdamOptimizer(learning_rate=0.0000625, epsilon=0.00015),
-                       replay_capacity=args.capacity, batch_size=args.batch,
-                       use_hip_graph=not args.no_graph, device=dev, seed=1000 * rank,
-                       process_group=pg,
-                       **({} if args.fuse_opt is None else {'fuse_optimizer': bool(args.fuse_opt)}),
-                       **({} if args.ride is None else {'ride_replay': bool(args.ride)}))
+  agent = build_agent(args.actions, args.capacity, args.batch, dev, pg=pg,
+                      use_hip_graph=not args.no_graph,
+                      **({} if args.fuse_opt is None else {'fuse_optimizer': bool(args.fuse_opt)}),
+                      **({} if args.ride is None else {'ride_replay': bool(args.ride)}))
   import random
   random.seed(0 + rank)
   fill_synthetic(agent._replay.memory, args.actions, seed=1 + rank)
@@ -212,6 +241,13 @@ def main():
     else:   # the same calls, consecutive steps replayed K per HIP graph (learner-only loop)
       agent.train_gradient_steps(n)
 
+  # untimed: run until every graph the timed loop replays is captured (both step
+  # parities, the 4-step chunk graphs of both starting parities), whatever --warmup
+  # is, so a short timed window holds only steady-state steps; then the warmup
+  prime = 0
+  while not agent.graphs_primed() and prime < 200:
+    grad_steps(5)
+    prime += 5
   grad_steps(args.warmup)
   torch.cuda.synchronize()
   if pg is not None:
@@ -245,7 +281,7 @@ def main():
     line = {
         'metric': 'gradient-steps/sec (Rainbow, batch=32, 1M-transition buffer)',
         'value': round(value, 2), 'unit': 'gradient-steps/s', 'n_gpus': world,
-        'steps': args.steps, 'warmup': args.warmup,
+        'steps': args.steps, 'warmup': args.warmup, 'prime_steps': prime,
         'ms_per_step': round(1e3 * elapsed / args.steps, 4), 'higher_is_better': True,
         'scaling': 'weak', 'vs_baseline': None, 'dtype': 'fp32', 'data': 'synthetic',
         'config': {'workload': 'Rainbow/C51 Asterix (9 actions), prioritized sum-tree replay, '

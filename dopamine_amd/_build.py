@@ -11,10 +11,31 @@ ARCH = os.environ.get('DQ_OFFLOAD_ARCH', 'gfx950')
 
 
 def build(verbose=False, out=None, sources=None):
-  """Compile the HIP sources into libdopamine_amd.so next to this file."""
+  """Compile the HIP sources into libdopamine_amd.so next to this file: one hipcc per
+  translation unit, in parallel, then one link."""
   out = out or LIB_PATH
-  cmd = ['hipcc', '--offload-arch=' + ARCH, '-O3', '-fPIC', '-shared', '-std=c++17',
-         '-ffp-contract=off', '-Wall', '-I', os.path.join(_HERE, 'csrc'), '-o', out] + (sources or SOURCES)
+  flags = ['--offload-arch=' + ARCH, '-O3', '-fPIC', '-std=c++17', '-ffp-contract=off', '-Wall',
+           '-I', os.path.join(_HERE, 'csrc')]
+  objs, procs = [], []
+  bdir = os.path.join(_HERE, 'build')
+  os.makedirs(bdir, exist_ok=True)
+  csrc = os.path.join(_HERE, 'csrc')
+  headers = [os.path.join(csrc, f) for f in os.listdir(csrc) if f.endswith('.h')] + [HEADER]
+  newest_h = max(os.path.getmtime(h) for h in headers)
+  for src in sources or SOURCES:
+    obj = os.path.join(bdir, '%s.%s.o' % (os.path.basename(out), os.path.splitext(os.path.basename(src))[0]))
+    objs.append(obj)
+    if (os.path.exists(obj) and os.path.exists(out) and
+        os.path.getmtime(obj) >= max(os.path.getmtime(src), newest_h)):
+      continue                       # object up to date (incremental rebuild)
+    cmd = ['hipcc'] + flags + ['-c', '-o', obj, src]
+    if verbose:
+      print(' '.join(cmd))
+    procs.append((subprocess.Popen(cmd), cmd))
+  for p, cmd in procs:
+    if p.wait() != 0:
+      raise subprocess.CalledProcessError(p.returncode, cmd)
+  cmd = ['hipcc', '--offload-arch=' + ARCH, '-shared', '-fPIC', '-o', out] + objs
   if verbose:
     print(' '.join(cmd))
   subprocess.run(cmd, check=True)

@@ -12,6 +12,7 @@ ABI_VERSION = 1
 OK = 0
 ST_OK, ST_EMPTY_TREE, ST_MAX_ATTEMPTS, ST_TAPE_EXHAUSTED, ST_NEG_PRIORITY, ST_TOO_FEW, ST_BAD_INDEX = range(7)
 LAYOUT_RAW, LAYOUT_F32_NORM, LAYOUT_F32_NHWC = 0, 1, 2
+SUMTREE_QUERY, SUMTREE_RANDOM, SUMTREE_STRATIFIED = 0, 1, 2
 
 
 class Meta(ctypes.Structure):
@@ -84,10 +85,13 @@ SIGNATURES = {
     'dq_sumtree_depth': [_I64],
     'dq_replay_create': [ctypes.POINTER(Config), ctypes.POINTER(Storage), ctypes.POINTER(_P)],
     'dq_replay_destroy': [_P],
+    'dq_sumtree_create': [_I64, _P, _P, _P, _I64, ctypes.POINTER(_P)],
     'dq_replay_add': [_P, _I64, _P, _P, _P, _P, _P, _P],
     'dq_replay_sample_indices': [_P, _I32, _P, _P],
     'dq_replay_gather': [_P, _P, _I32, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     'dq_sumtree_set': [_P, _P, _P, _I64, _P],
+    'dq_sumtree_set_f64': [_P, _P, _P, _I64, _P],
+    'dq_sumtree_sample': [_P, _I32, _I32, _P, _P, _P],
     'dq_sumtree_get': [_P, _P, _I64, _P, _P],
     'dq_sumtree_rebuild': [_P, _P],
     'dq_replay_set_meta': [_P, _I64, _D, _P],

@@ -144,6 +144,7 @@ class DQNAgent(object):
     self._head = None              # (target net, input) whose forward head rides in the backward
     self._tail_head = None         # ... in the N > 1 tail graph
     self._sess = sess
+    self._trace = None             # enable_trace(): per-step copies for the parity tests
 
     state_shape = (1,) + self.observation_shape + (stack_size,)
     self.state = np.zeros(state_shape)
@@ -155,9 +156,62 @@ class DQNAgent(object):
                                        segments=self.online_convnet.fp.segments())
       self._side = torch.cuda.Stream(self._device)
       self._comm = torch.cuda.Stream(self._device)
+      if self._pg is not None:
+        self._broadcast_replica()
     self._observation = None
     self._last_observation = None
     self.last_loss = None
+
+  def _replica_tensors(self):
+    """Everything a replica's updates depend on: parameters and optimizer state."""
+    ts = [self.online_convnet.fp.flat, self.target_convnet.fp.flat]
+    ts += [v for k, v in sorted(vars(self._opt).items())
+           if isinstance(v, torch.Tensor) and v.data_ptr() != self.online_convnet.fp.flat.data_ptr()]
+    return ts
+
+  def _broadcast_replica(self):
+    """Data-parallel replicas start from group rank 0's networks and optimizer state
+    (whatever seed each rank was built with), so the identical all-reduced updates
+    keep them bit-identical (parallel.replicas_in_sync)."""
+    import torch.distributed as dist
+    src = dist.get_process_group_ranks(self._pg)[0]
+    for t in self._replica_tensors():
+      dist.broadcast(t, src=src, group=self._pg)
+    torch.cuda.synchronize(self._device)
+
+  # ---------------------------------------------------------------- tracing
+  # Parity tests compare every step of the bench path (graph replays, chunks) with a
+  # float64 CPU restatement.  enable_trace() (before the first step, so captured graphs
+  # include it) makes each step copy its batch, network outputs, loss outputs and flat
+  # gradient into ring slot j of self._trace: chunk step j -> slot j (< _UNROLL), a
+  # single-step graph or eager step of parity k -> slot _UNROLL + k.  Copies only: the
+  # step's own kernels and arithmetic are those of the untraced path.
+  def enable_trace(self):
+    assert not self._graph_sets, 'enable_trace() must precede the first gradient step'
+    self._trace = {}
+
+  def _trace_outputs(self, c):
+    """name -> device tensor of step slot c's results (subclasses add theirs)."""
+    t = self._pbuf[c]
+    d = {k: t[k] for k in ('indices', 'action', 'reward', 'terminal', 'next_action',
+                           'next_reward', 'state', 'next_state', 'sampling_probabilities')
+         if k in t}
+    d['loss'] = self._loss_out['loss']
+    d['grad_out'] = self._loss_out['grad']
+    d['grad'] = self.online_convnet.fp.grad
+    if self._hip is not None:
+      d['online_out'] = self._hip['online'].acts['out']
+      d['target_out'] = self._hip['target'][c].acts['out']
+    return d
+
+  def _trace_step(self, slot, c):
+    if self._trace is None:
+      return
+    n = self._UNROLL + 2
+    for k, v in self._trace_outputs(c).items():
+      if k not in self._trace:
+        self._trace[k] = torch.zeros((n,) + tuple(v.shape), dtype=v.dtype, device=v.device)
+      self._trace[k][slot].copy_(v)
 
   # ------------------------------------------------------------ graph parts
   def _build_replay_buffer(self, use_staging):
@@ -594,6 +648,7 @@ class DQNAgent(object):
       self._grad_step(c, k, pipe)
       self._allreduce_grads()
       self._device_opt_step(k)
+      self._trace_step(self._UNROLL + k, c)
       self._eager_steps[pipe] += 1
     self._opt_steps += 1
     self._replay._out = self._pbuf[c]
@@ -647,6 +702,7 @@ class DQNAgent(object):
         self._grad_step(c, k, pipe)
         if self._pg is None:
           self._device_opt_step(k)
+          self._trace_step(self._UNROLL + k, c)
       pool = g.pool()
       graphs.append(g)
       if self._pg is not None:
@@ -787,6 +843,18 @@ class DQNAgent(object):
         self._train_step()
       n -= 1
 
+  def graphs_primed(self):
+    """True once every HIP graph the learner loop replays is captured: the per-step
+    graphs and, where chunking applies (single replica), the chunk graphs of both
+    starting parities."""
+    if not self.use_hip_graph:
+      return True
+    if self._graph_sets.get(True) is None:
+      return False
+    if self._pg is not None or self._hip is None or not self.pipeline:
+      return True
+    return all(('chunk', self._UNROLL, k) in self._graph_sets for k in (0, 1))
+
   def _chunk_ok(self):
     K, U = self._UNROLL, self.update_period
     t0 = self.training_steps
@@ -817,6 +885,7 @@ class DQNAgent(object):
           k = (k0 + j) % 2
           self._grad_step(k, k, True)
           self._device_opt_step(k)
+          self._trace_step(j, k)
       self._graph_pool = g.pool()
       self._graph_sets[key] = g
     for _ in range(K):
@@ -882,10 +951,14 @@ class DQNAgent(object):
       except OSError:
         pass
     self._replay.save(checkpoint_dir, iteration_number)
-    return {'state': self.state, 'training_steps': self.training_steps}
+    # _opt_steps: TF1 Adam's beta powers are double-buffered by step parity
+    return {'state': self.state, 'training_steps': self.training_steps,
+            '_opt_steps': self._opt_steps}
 
   def unbundle(self, checkpoint_dir, iteration_number, bundle_dictionary):
     """dqn_agent.py:512-551."""
+    self._discard_prefetch()          # the buffer (and its RNG use) is replaced below
+    self._replay.memory.sync_rng(raise_errors=False)
     try:
       self._replay.load(checkpoint_dir, iteration_number)
     except (FileNotFoundError, NotImplementedError):

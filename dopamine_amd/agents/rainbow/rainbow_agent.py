@@ -139,8 +139,13 @@ class RainbowAgent(dqn_agent.DQNAgent):
     out = ops.c51_loss_fused(self._hip['online'], self._hip['target'][c], t['action'], t['reward'],
                              t['terminal'], self._support, self.cumulative_gamma,
                              probs=t['sampling_probabilities'] if prioritized else None,
-                             out=self._loss_out)
+                             out=self._loss_out, logits_out=self._trace is not None)
     return None, out['grad']
+
+  def _trace_outputs(self, c):
+    d = super()._trace_outputs(c)
+    d['priorities'] = self._loss_out['priorities']
+    return d
 
   def _post_loss(self, t):
     if self._replay_scheme == 'prioritized':

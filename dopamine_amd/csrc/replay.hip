@@ -21,6 +21,7 @@ struct dq_replay {
   dq_replay_config cfg;
   dq_replay_storage st;
   int depth;
+  bool tree_only;   // dq_sumtree_create: a standalone SumTree (no transition store)
   dq::ReplayView view() const {
     dq::ReplayView v;
     v.C = cfg.capacity;
@@ -52,6 +53,54 @@ __global__ __launch_bounds__(kTreeT) void k_per_sample(ReplayView v, int B, int3
 
 __global__ __launch_bounds__(64) void k_uniform_sample(ReplayView v, int B, int32_t* out) {
   uniform_sample_body(v, B, out);
+}
+
+// SumTree.sample / stratified_sample (sum_tree.py:99-166) on the flat heap, one
+// lane per query: DQ_SUMTREE_QUERY uses the caller's query values, DQ_SUMTREE_RANDOM
+// one random.random() per query (two tape words each, in order), DQ_SUMTREE_STRATIFIED
+// random.uniform(i/n, (i+1)/n) per stratum -- the same float64 steps as the PER
+// sampler's first phase (per_sample_body), without the validity rule.
+__global__ __launch_bounds__(256) void k_sumtree_sample(ReplayView v, int mode, int n,
+                                                        const double* query, int64_t* out) {
+  dq_replay_meta* meta = v.meta;
+  const int64_t pos = meta->tape_pos;
+  const bool random = mode != DQ_SUMTREE_QUERY;
+  const double total = v.tree[0];
+  bool fail = meta->status != 0;
+  if (!fail && total == 0.0) {
+    if (threadIdx.x == 0) latch(meta, DQ_ST_EMPTY_TREE, 0, 0.0);
+    fail = true;
+  }
+  if (!fail && random && pos + 2 * (int64_t)n > meta->tape_len) {
+    if (threadIdx.x == 0) latch(meta, DQ_ST_TAPE_EXHAUSTED, 0, 0.0);
+    fail = true;
+  }
+  const double step = 1.0 / (double)n;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    int64_t node = 0;
+    if (!fail) {
+      double q;
+      if (!random) {
+        q = query[i];
+      } else {
+        const double u = res53(v.tape[pos + 2 * i], v.tape[pos + 2 * i + 1]);
+        if (mode == DQ_SUMTREE_RANDOM) {
+          q = u;
+        } else {
+          const double lo = __dmul_rn((double)i, step);
+          const double hi = (i + 1 == n) ? 1.0 : __dmul_rn((double)(i + 1), step);
+          q = __dadd_rn(lo, __dmul_rn(__dsub_rn(hi, lo), u));
+        }
+      }
+      node = descend(v.tree, v.depth, __dmul_rn(q, total));
+    }
+    out[i] = node;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && !fail && random) {
+    meta->reserved[0] = pos;
+    meta->tape_pos = pos + 2 * (int64_t)n;
+  }
 }
 
 // Undo the tape consumption of the most recent sample (its indices are discarded):
@@ -224,6 +273,30 @@ int dq_replay_create(const dq_replay_config* cfg, const dq_replay_storage* st, d
   h->cfg = *cfg;
   h->st = *st;
   h->depth = dq_sumtree_depth(cfg->capacity);
+  h->tree_only = false;
+  *out = h;
+  return DQ_OK;
+}
+
+int dq_sumtree_create(int64_t capacity, double* tree, dq_replay_meta* meta, uint32_t* tape,
+                      int64_t tape_capacity, dq_replay** out) {
+  DQ_CHECK_ARG(out && tree && meta, "null argument");
+  DQ_CHECK_ARG(capacity > 0, "Sum tree capacity should be positive.");
+  DQ_CHECK_ARG(capacity < ((int64_t)1 << 31), "capacity must fit int32 indices");
+  dq_replay* h = new (std::nothrow) dq_replay;
+  DQ_CHECK_ARG(h, "out of host memory");
+  memset(&h->cfg, 0, sizeof(h->cfg));
+  memset(&h->st, 0, sizeof(h->st));
+  h->cfg.capacity = capacity;
+  h->cfg.stack_size = 1;
+  h->cfg.update_horizon = 1;
+  h->cfg.prioritized = 1;
+  h->st.tree = tree;
+  h->st.meta = meta;
+  h->st.tape = tape;
+  h->st.tape_capacity = tape ? tape_capacity : 0;
+  h->depth = dq_sumtree_depth(capacity);
+  h->tree_only = true;
   *out = h;
   return DQ_OK;
 }
@@ -237,6 +310,7 @@ int dq_replay_add(dq_replay* h, int64_t n, const uint8_t* frames, const int32_t*
                   const float* rewards, const uint8_t* terminals, const float* priorities,
                   void* stream) {
   DQ_CHECK_ARG(h && n >= 0, "bad handle/count");
+  DQ_CHECK_ARG(!h->tree_only, "a standalone sum tree has no transition store");
   if (n == 0) return DQ_OK;
   DQ_CHECK_ARG(frames && actions && rewards && terminals, "null transition array");
   DQ_CHECK_ARG(!h->cfg.prioritized || priorities, "prioritized add needs priorities");
@@ -259,6 +333,7 @@ int dq_replay_add(dq_replay* h, int64_t n, const uint8_t* frames, const int32_t*
 
 int dq_replay_sample_indices(dq_replay* h, int32_t batch, int32_t* indices_out, void* stream) {
   DQ_CHECK_ARG(h && indices_out, "null argument");
+  DQ_CHECK_ARG(!h->tree_only, "a standalone sum tree has no transition store");
   DQ_CHECK_ARG(batch >= 1 && batch <= kMaxBatch, "batch must be in [1, 1024]");
   DQ_CHECK_ARG(h->st.tape, "RNG tape not attached");
   hipStream_t s = (hipStream_t)stream;
@@ -276,6 +351,7 @@ int dq_replay_gather(dq_replay* h, const int32_t* indices, int32_t batch, int32_
                      uint8_t* terminal_out, int32_t* indices_out, float* probs_out,
                      void* stream) {
   DQ_CHECK_ARG(h && indices && batch >= 1, "bad arguments");
+  DQ_CHECK_ARG(!h->tree_only, "a standalone sum tree has no transition store");
   DQ_CHECK_ARG(!probs_out || h->cfg.prioritized, "probs requested from a uniform buffer");
   GatherOut g{indices, state_out, next_state_out, action_out, reward_out, next_action_out,
               next_reward_out, terminal_out, indices_out, probs_out};
@@ -316,6 +392,33 @@ int dq_sumtree_set(dq_replay* h, const int32_t* indices, const float* priorities
   SetArgs a{indices, priorities, n};
   hipLaunchKernelGGL(k_sumtree_set, dim3(1), dim3(kTreeT), 0, (hipStream_t)stream, h->view(), a);
   DQ_CHECK_LAUNCH("k_sumtree_set");
+  return DQ_OK;
+}
+
+int dq_sumtree_set_f64(dq_replay* h, const int32_t* indices, const double* values, int64_t n,
+                       void* stream) {
+  DQ_CHECK_ARG(h && h->cfg.prioritized, "sum tree needs a prioritized buffer");
+  DQ_CHECK_ARG(indices && values && n >= 0, "bad arguments");
+  DQ_CHECK_ARG(h->depth < 63, "tree too deep");
+  if (n == 0) return DQ_OK;
+  SetArgs a{indices, nullptr, n, values};
+  hipLaunchKernelGGL(k_sumtree_set, dim3(1), dim3(kTreeT), 0, (hipStream_t)stream, h->view(), a);
+  DQ_CHECK_LAUNCH("k_sumtree_set");
+  return DQ_OK;
+}
+
+int dq_sumtree_sample(dq_replay* h, int32_t mode, int32_t n, const double* query_values,
+                      int64_t* out, void* stream) {
+  DQ_CHECK_ARG(h && h->cfg.prioritized && out, "bad arguments");
+  DQ_CHECK_ARG(n >= 1 && n <= (1 << 20), "query count must be in [1, 2^20]");
+  DQ_CHECK_ARG(mode == DQ_SUMTREE_QUERY || mode == DQ_SUMTREE_RANDOM ||
+               mode == DQ_SUMTREE_STRATIFIED, "unknown sum-tree sample mode");
+  DQ_CHECK_ARG(mode != DQ_SUMTREE_QUERY || query_values, "query mode needs query values");
+  DQ_CHECK_ARG(mode == DQ_SUMTREE_QUERY || h->st.tape, "RNG tape not attached");
+  DQ_CHECK_ARG(h->depth < 63, "tree too deep");
+  hipLaunchKernelGGL(k_sumtree_sample, dim3(1), dim3(256), 0, (hipStream_t)stream, h->view(),
+                     (int)mode, (int)n, query_values, out);
+  DQ_CHECK_LAUNCH("k_sumtree_sample");
   return DQ_OK;
 }
 
@@ -397,6 +500,7 @@ int dq_replay_record_sumtree_set(dq_replay* h, const int32_t* indices, const flo
 
 int dq_replay_record_sample(dq_replay* h, int32_t batch, int32_t* indices_out, dq_rider* out) {
   DQ_CHECK_ARG(h && indices_out, "null argument");
+  DQ_CHECK_ARG(!h->tree_only, "a standalone sum tree has no transition store");
   DQ_CHECK_ARG(batch >= 1 && batch <= kMaxBatch, "batch must be in [1, 1024]");
   DQ_CHECK_ARG(h->st.tape, "RNG tape not attached");
   RiderDesc r{};
@@ -412,6 +516,7 @@ int dq_replay_record_gather_nhwc(dq_replay* h, const int32_t* indices, int32_t b
                                  float* next_reward_out, uint8_t* terminal_out,
                                  int32_t* indices_out, float* probs_out, dq_rider* out) {
   DQ_CHECK_ARG(h && indices && batch >= 1 && batch <= kMaxBatch, "bad arguments");
+  DQ_CHECK_ARG(!h->tree_only, "a standalone sum tree has no transition store");
   DQ_CHECK_ARG(!probs_out || h->cfg.prioritized, "probs requested from a uniform buffer");
   DQ_CHECK_ARG(h->cfg.obs_is_u8, "F32_NHWC layout needs uint8 observations");
   DQ_CHECK_ARG(h->cfg.stack_size == 4, "F32_NHWC layout needs stack_size == 4");

@@ -479,85 +479,10 @@ constexpr int kNhwcR = 1;
 // ---------------------------------------------------------------------------
 struct SetArgs {
   const int32_t* indices;  // NULL => (add_count + i) mod C
-  const float* values;
+  const float* values;     // float32 priorities (set_priority, _add) ...
   int64_t n;
+  const double* values64;  // ... or, if non-null, float64 values (a standalone SumTree.set)
 };
-
-constexpr int kSumtreeSetLds = kWave * (kWave + 1) * 8 + kWave * 8 + kWave * 4 + kWave * kWave;
-
-__device__ inline void sumtree_set_body(const ReplayView& v, const SetArgs& a, void* lds) {
-  double (*s_cur)[kWave + 1] = (double (*)[kWave + 1])lds;
-  int64_t* s_idx = (int64_t*)(s_cur + kWave);
-  float* s_val = (float*)(s_idx + kWave);
-  int8_t (*s_next)[kWave] = (int8_t (*)[kWave])(s_val + kWave);  // [level][i] -> next update sharing the node
-  const int lane = threadIdx.x;
-  dq_replay_meta* meta = v.meta;
-  if (meta->status != 0) return;
-  const int depth = v.depth;
-  const int64_t base = meta->add_count;
-  double maxrec = meta->max_recorded_priority;
-  bool stop = false;
-  for (int64_t c0 = 0; c0 < a.n && !stop; c0 += kWave) {
-    const int m = (int)((a.n - c0) < kWave ? (a.n - c0) : kWave);
-    if (lane < m) {
-      s_idx[lane] = a.indices ? (int64_t)a.indices[c0 + lane] : pymod(base + c0 + lane, v.C);
-      s_val[lane] = a.values[c0 + lane];
-    }
-    __syncthreads();
-    // the reference raises at the first negative value, after applying the earlier ones
-    const bool badi = lane < m && (s_idx[lane] < 0 || s_idx[lane] >= ((int64_t)1 << depth));
-    const uint64_t negm = __ballot(lane < m && (s_val[lane] < 0.0f || badi));
-    int me = m;
-    if (negm) {
-      me = __ffsll((unsigned long long)negm) - 1;
-      stop = true;
-    }
-    for (int i = 0; i < me; ++i) {  // max(value, max_rec) with Python's argument order
-      const double x = (double)s_val[i];
-      maxrec = (maxrec > x) ? maxrec : x;
-    }
-    // next-same table: levels 0..D(i,j) share a node between updates i < j
-    for (int d = 0; d <= depth; ++d)
-      if (lane < me) s_next[d][lane] = -1;
-    __syncthreads();
-    if (lane < me) {
-      int covered = -1;
-      for (int j = lane + 1; j < me && covered < depth; ++j) {
-        const uint64_t x = (uint64_t)(s_idx[lane] ^ s_idx[j]);
-        const int D = x ? depth - (64 - __clzll(x)) : depth;
-        for (int d = covered + 1; d <= D; ++d) s_next[d][lane] = (int8_t)j;
-        if (D > covered) covered = D;
-      }
-    }
-    __syncthreads();
-    const bool mine = lane <= depth;
-    const int shift = depth - lane;
-    const int64_t loff = ((int64_t)1 << (mine ? lane : 0)) - 1;
-    if (mine)
-      for (int i = 0; i < me; ++i) s_cur[lane][i] = v.tree[loff + (s_idx[i] >> shift)];
-    __syncthreads();
-    for (int i = 0; i < me; ++i) {
-      const double cur = mine ? s_cur[lane][i] : 0.0;
-      const double dl = __dsub_rn((double)s_val[i], cur);  // meaningful on the leaf lane
-      const double delta = __shfl(dl, depth);
-      if (mine) {
-        const double x = __dadd_rn(cur, delta);
-        const int j = s_next[lane][i];
-        if (j >= 0)
-          s_cur[lane][j] = x;
-        else
-          v.tree[loff + (s_idx[i] >> shift)] = x;
-      }
-    }
-    __syncthreads();
-    if (stop && lane == 0) {
-      const bool oob = s_idx[me] < 0 || s_idx[me] >= ((int64_t)1 << depth);
-      latch(meta, oob ? DQ_ST_BAD_INDEX : DQ_ST_NEG_PRIORITY, (int)(c0 + me),
-            oob ? (double)s_idx[me] : (double)s_val[me]);
-    }
-  }
-  if (lane == 0) meta->max_recorded_priority = maxrec;
-}
 
 // ---------------------------------------------------------------------------
 // Block-parallel forms of the two single-wave chains above (same float64
@@ -565,8 +490,10 @@ __device__ inline void sumtree_set_body(const ReplayView& v, const SetArgs& a, v
 // block of T threads: the riders get a whole 1024-thread block anyway.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int readlane_i(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
-__device__ __forceinline__ float readlane_f(float x, int l) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
+__device__ __forceinline__ double readlane_d(double x, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(x), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(x), l);
+  return __hiloint2double(hi, lo);
 }
 
 // Ordered chain of float64 adds per tree node: update i (lane i) hits node n_i,
@@ -574,11 +501,11 @@ __device__ __forceinline__ float readlane_f(float x, int l) {
 // before update i (the tree value, or after_prev), after_i = before_i + delta_i --
 // resolved in rounds along the prev links, each round one shuffle.
 __device__ __forceinline__ double node_chain(bool act, int prev, double tree_val, double& delta,
-                                             bool leaf, float val) {
+                                             bool leaf, double val) {
   bool done = act && prev < 0;
   double before = tree_val, after = 0.0;
   if (done) {
-    if (leaf) delta = __dsub_rn((double)val, before);
+    if (leaf) delta = __dsub_rn(val, before);
     after = __dadd_rn(before, delta);
   }
   while (__ballot(act && !done)) {
@@ -587,7 +514,7 @@ __device__ __forceinline__ double node_chain(bool act, int prev, double tree_val
     const int dp = __shfl((int)done, src);
     if (act && !done && dp) {
       before = ap;
-      if (leaf) delta = __dsub_rn((double)val, before);
+      if (leaf) delta = __dsub_rn(val, before);
       after = __dadd_rn(before, delta);
       done = true;
     }
@@ -613,7 +540,7 @@ __device__ inline void sumtree_set_par(const ReplayView& v, const SetArgs& a, vo
   // branch), so the tree loads wait on one memory round, not two
   const int64_t l0 = a.n > 0 ? (lane < a.n ? lane : a.n - 1) : 0;
   const int32_t pre_i = (a.indices && a.n > 0) ? a.indices[l0] : 0;
-  const float pre_v = a.n > 0 ? a.values[l0] : 0.0f;
+  const double pre_v = a.n > 0 ? (a.values64 ? a.values64[l0] : (double)a.values[l0]) : 0.0;
   if (meta->status != 0) return;
   const int depth = v.depth;
   const int64_t base = meta->add_count;
@@ -622,19 +549,19 @@ __device__ inline void sumtree_set_par(const ReplayView& v, const SetArgs& a, vo
   for (int64_t c0 = 0; c0 < a.n && !stop; c0 += kWave) {
     const int m = (int)((a.n - c0) < kWave ? (a.n - c0) : kWave);
     int64_t idx = 0;
-    float val = 0.0f;
+    double val = 0.0;
     if (lane < m) {
       if (c0 == 0) {
         idx = a.indices ? (int64_t)pre_i : pymod(base + lane, v.C);
         val = pre_v;
       } else {
         idx = a.indices ? (int64_t)a.indices[c0 + lane] : pymod(base + c0 + lane, v.C);
-        val = a.values[c0 + lane];
+        val = a.values64 ? a.values64[c0 + lane] : (double)a.values[c0 + lane];
       }
     }
     // the reference raises at the first negative value, after applying the earlier ones
     const bool badi = lane < m && (idx < 0 || idx >= ((int64_t)1 << depth));
-    const uint64_t negm = __ballot(lane < m && (val < 0.0f || badi));
+    const uint64_t negm = __ballot(lane < m && (val < 0.0 || badi));
     int me = m;
     if (negm) {
       me = __ffsll((unsigned long long)negm) - 1;
@@ -643,7 +570,7 @@ __device__ inline void sumtree_set_par(const ReplayView& v, const SetArgs& a, vo
     const bool act = lane < me;
     if (wave == 0)
       for (int i = 0; i < me; ++i) {   // max(value, max_rec) with Python's argument order
-        const double x = (double)readlane_f(val, i);
+        const double x = readlane_d(val, i);
         maxrec = (maxrec > x) ? maxrec : x;
       }
     const int node_leaf = act ? (int)idx : 0;
@@ -690,11 +617,11 @@ __device__ inline void sumtree_set_par(const ReplayView& v, const SetArgs& a, vo
     }
     if (stop) {                        // the first bad update: a bad index, else its value
       const int64_t bi = (int64_t)readlane_i((int)idx, me);   // indices are int32
-      const float bv = readlane_f(val, me);
+      const double bv = readlane_d(val, me);
       const bool oob = bi < 0 || bi >= ((int64_t)1 << depth);
       if (threadIdx.x == 0)
         latch(meta, oob ? DQ_ST_BAD_INDEX : DQ_ST_NEG_PRIORITY, (int)(c0 + me),
-              oob ? (double)bi : (double)bv);
+              oob ? (double)bi : bv);
     }
     __threadfence_block();
     __syncthreads();                   // the next chunk reads what this one stored

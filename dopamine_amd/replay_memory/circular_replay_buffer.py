@@ -29,6 +29,36 @@ STORE_FILENAME_PREFIX = '$store$_'
 CHECKPOINT_DURATION = 4
 
 
+class _ReferenceSumTree(object):
+  """Target of a reference-written ``sum_tree`` pickle (dopamine.replay_memory.sum_tree.
+  SumTree): only its fields (``nodes``, ``max_recorded_priority``) are restored."""
+
+
+class _CheckpointUnpickler(pickle.Unpickler):
+  """Unpickles replay checkpoint members with a class whitelist: the reference's and
+  this package's sum-tree snapshots and numpy's array / scalar reconstructors.
+  Anything else (a callable a crafted file could name) is refused."""
+
+  _ALLOWED = {
+      ('dopamine.replay_memory.sum_tree', 'SumTree'): _ReferenceSumTree,
+      ('numpy', 'ndarray'): np.ndarray,
+      ('numpy', 'dtype'): np.dtype,
+  }
+
+  def find_class(self, module, name):
+    key = (module, name)
+    if key in self._ALLOWED:
+      return self._ALLOWED[key]
+    if key == ('dopamine_amd.replay_memory.sum_tree', 'SumTreeState'):
+      from dopamine_amd.replay_memory.sum_tree import SumTreeState
+      return SumTreeState
+    if module in ('numpy.core.multiarray', 'numpy._core.multiarray') and name in ('_reconstruct',
+                                                                                  'scalar'):
+      return getattr(np._core.multiarray if hasattr(np, '_core') else np.core.multiarray, name)
+    raise pickle.UnpicklingError('replay checkpoint names {}.{}: not an allowed type'.format(
+        module, name))
+
+
 class NotFoundError(FileNotFoundError):
   """Stands in for ``tf.errors.NotFoundError`` (same constructor), raised by
   ``load`` when a checkpoint file is missing (crb:671-673)."""
@@ -356,8 +386,10 @@ class OutOfGraphReplayBuffer(object):
       self._precheck()
     out = torch.empty((batch_size,), dtype=torch.int32, device=self._device)
     words = self._words_worst_case(batch_size)
+    if self._rng.valid:                # words already used by device sampling come first
+      self._rng.sync(self._stream)
     while True:
-      self._rng.invalidate()
+      self._rng.invalidate()           # a retry (tape ran dry) redraws from the same state
       self._rng.rebuild(words, self._stream)
       _lib.call('dq_replay_sample_indices', self._h, batch_size, _lib.ptr(out), self._stream)
       meta = self._read_meta()
@@ -603,7 +635,8 @@ class OutOfGraphReplayBuffer(object):
 
   def load(self, checkpoint_dir, suffix):
     """crb:659-687.  Raises NotFoundError (nothing loaded) if any file is missing.
-    Pickled members are unpickled: load only checkpoints this code wrote."""
+    Pickled members go through a whitelisting unpickler (_CheckpointUnpickler), so a
+    checkpoint written by the reference loads (its pickled SumTree included)."""
     elems = self._return_checkpointable_elements()
     for attr in elems:
       filename = self._generate_filename(checkpoint_dir, attr, suffix)
@@ -623,7 +656,7 @@ class OutOfGraphReplayBuffer(object):
           elif isinstance(cur, np.ndarray):
             self.__dict__[attr] = np.load(infile, allow_pickle=False)
           else:
-            self.__dict__[attr] = self._restore_value(attr, pickle.load(infile))
+            self.__dict__[attr] = self._restore_value(attr, _CheckpointUnpickler(infile).load())
     for attr, arr in arrays.items():
       t = elems[attr]
       t.copy_(torch.from_numpy(np.ascontiguousarray(arr)).to(dtype=t.dtype))

@@ -58,17 +58,20 @@ class OutOfGraphPrioritizedReplayBuffer(circular_replay_buffer.OutOfGraphReplayB
       return
     assert indices.dtype == np.int32, ('Indices must be integers, '
                                        'given: {}'.format(indices.dtype))
-    pr = np.asarray(priorities, dtype=np.float32).reshape(-1)
+    # SumTree.set receives each priority as given (float32 from the agent, float64 from
+    # a caller's float array): the float64 entry point stores both exactly
+    given = np.asarray(priorities).reshape(-1)
+    pr = given.astype(np.float64)
     idx = np.asarray(indices).reshape(-1)
     bad = np.nonzero(pr < 0.0)[0]
     upto = int(bad[0]) if len(bad) else len(idx)
     if upto:
       d_i = torch.from_numpy(np.ascontiguousarray(idx[:upto])).to(self._device)
       d_p = torch.from_numpy(np.ascontiguousarray(pr[:upto])).to(self._device)
-      _lib.call('dq_sumtree_set', self._h, _lib.ptr(d_i), _lib.ptr(d_p), upto, self._stream)
+      _lib.call('dq_sumtree_set_f64', self._h, _lib.ptr(d_i), _lib.ptr(d_p), upto, self._stream)
       torch.cuda.current_stream(self._device).synchronize()
     if len(bad):
-      raise ValueError('Sum tree values should be nonnegative. Got {}'.format(pr[upto]))
+      raise ValueError('Sum tree values should be nonnegative. Got {}'.format(given[upto]))
 
   def get_priority(self, indices):
     """prb:216-235."""
@@ -101,6 +104,8 @@ class OutOfGraphPrioritizedReplayBuffer(circular_replay_buffer.OutOfGraphReplayB
 
   def _restore_value(self, attr, value):
     if attr == 'sum_tree':
+      if isinstance(value, circular_replay_buffer._ReferenceSumTree):   # written by the reference
+        value = SumTreeState(value.nodes, value.max_recorded_priority)
       if not isinstance(value, SumTreeState):
         raise ValueError('sum_tree checkpoint holds {}, expected SumTreeState'.format(type(value)))
       flat = np.concatenate([np.asarray(n, np.float64) for n in value.nodes])

@@ -41,6 +41,11 @@ extern "C" {
 #define DQ_ST_TOO_FEW 5           /* circular_replay_buffer.py:457-460 */
 #define DQ_ST_BAD_INDEX 6         /* leaf index outside the tree (numpy IndexError in sum_tree.py:196) */
 
+/* dq_sumtree_sample modes */
+#define DQ_SUMTREE_QUERY 0        /* SumTree.sample(query_value) for given values (sum_tree.py:99-141) */
+#define DQ_SUMTREE_RANDOM 1       /* SumTree.sample() with random.random() (sum_tree.py:123) */
+#define DQ_SUMTREE_STRATIFIED 2   /* SumTree.stratified_sample(n) (sum_tree.py:143-166) */
+
 /* gather output layouts */
 #define DQ_LAYOUT_RAW 0           /* (B, stack, obs_bytes) bytes, stack-major (moveaxis on host = reference NHWC) */
 #define DQ_LAYOUT_F32_NORM 1      /* (B, stack, H*W) float32 = uint8 / 255 (atari_lib.py:96-97), NCHW */
@@ -93,6 +98,13 @@ int dq_sumtree_depth(int64_t capacity);
  * OutOfGraphPrioritizedReplayBuffer.__init__ (prioritized_replay_buffer.py:43-97). */
 int dq_replay_create(const dq_replay_config* cfg, const dq_replay_storage* st, dq_replay** out);
 int dq_replay_destroy(dq_replay* h);
+/* SumTree.__init__ (sum_tree.py:65-89) as a standalone object: a handle over a caller-owned
+ * float64 heap of 2^(depth+1)-1 nodes, depth = ceil(log2 capacity) (0 for capacity 1),
+ * a control block and an optional RNG tape.  Valid with dq_sumtree_set[_f64]/get/sample/
+ * rebuild, dq_replay_set_meta/set_tape/read_meta and dq_replay_destroy; the transition
+ * calls (add, sample_indices, gather, riders) reject it. */
+int dq_sumtree_create(int64_t capacity, double* tree, dq_replay_meta* meta, uint32_t* tape,
+                      int64_t tape_capacity, dq_replay** out);
 
 /* add() / _add() for n consecutive transitions at the cursor
  * (circular_replay_buffer.py:234-287, prioritized_replay_buffer.py:117-140).
@@ -120,6 +132,17 @@ int dq_replay_gather(dq_replay* h, const int32_t* indices, int32_t batch, int32_
  * ordered, delta-propagating float64 updates, duplicates honoured. */
 int dq_sumtree_set(dq_replay* h, const int32_t* indices, const float* priorities, int64_t n,
                    void* stream);
+/* SumTree.set with float64 values (sum_tree.py:178-205; a standalone tree is
+ * set with Python floats, not the buffer's float32 priorities). */
+int dq_sumtree_set_f64(dq_replay* h, const int32_t* indices, const double* values, int64_t n,
+                       void* stream);
+/* SumTree.sample(query_value) / sample() / stratified_sample(n) (sum_tree.py:99-166):
+ * n leaf indices into out (int64).  RANDOM / STRATIFIED consume 2n tape words (the
+ * Python `random` stream: random.random() per sample, random.uniform per stratum).
+ * An empty tree latches DQ_ST_EMPTY_TREE (sum_tree.py:116-117, 159-160); the
+ * query_value range check (sum_tree.py:119-120) is the host's. */
+int dq_sumtree_sample(dq_replay* h, int32_t mode, int32_t n, const double* query_values,
+                      int64_t* out, void* stream);
 /* get_priority (prioritized_replay_buffer.py:216-235). */
 int dq_sumtree_get(dq_replay* h, const int32_t* indices, int64_t n, float* out, void* stream);
 /* Bulk (re)build of internal nodes from the leaves (parents = sum of children).

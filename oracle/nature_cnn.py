@@ -1,0 +1,84 @@
+"""float64 Nature-CNN on the flat parameter layout -- TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/`` may import this module.  A torch-CPU float64 restatement of the
+reference's networks (atari_lib.py:85-105 NatureDQNNetwork, :108-144
+RainbowNetwork, :147-199 ImplicitQuantileNetwork) with TF's SAME padding and
+TF's (h, w, c) flatten order, reading the same flat fp32 parameter buffer the
+device kernels use (``dopamine_amd.agents.networks.FlatParams`` offsets: conv
+filters stored (out, kh, kw, in), FC (out, in)).  Gradients come from torch
+autograd in float64; they are returned in the same flat layout.
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+
+class Params64(object):
+  """float64 leaf tensors (torch layout) of a flat fp32/fp64 buffer."""
+
+  def __init__(self, flat, offsets):
+    flat = torch.as_tensor(np.asarray(flat), dtype=torch.float64)
+    self.offsets = offsets
+    self.numel = flat.numel()
+    self.t = {}
+    for name, (o, shape) in offsets.items():
+      n = int(np.prod(shape))
+      v = flat[o:o + n]
+      if len(shape) == 4:
+        out_c, in_c, kh, kw = shape
+        v = v.view(out_c, kh, kw, in_c).permute(0, 3, 1, 2)
+      else:
+        v = v.view(shape)
+      self.t[name] = v.clone().requires_grad_(True)
+
+  def __getitem__(self, name):
+    return self.t[name]
+
+  def flat_grad(self):
+    """The autograd gradients in the flat (out, kh, kw, in) / (out, in) layout."""
+    g = torch.zeros(self.numel, dtype=torch.float64)
+    for name, (o, shape) in self.offsets.items():
+      x = self.t[name].grad
+      if x is None:
+        continue
+      if len(shape) == 4:
+        x = x.permute(0, 2, 3, 1)
+      g[o:o + x.numel()] = x.reshape(-1)
+    return g.numpy()
+
+
+def torso(P, x_nhwc):
+  """x (B, 84, 84, stack) float64, already /255 -> (B, 7744) in TF's flatten order."""
+  x = x_nhwc.permute(0, 3, 1, 2)
+  x = F.relu(F.conv2d(F.pad(x, (2, 2, 2, 2)), P['conv1_w'], P['conv1_b'], stride=4))   # SAME 84->21
+  x = F.relu(F.conv2d(F.pad(x, (1, 2, 1, 2)), P['conv2_w'], P['conv2_b'], stride=2))   # SAME 21->11
+  x = F.relu(F.conv2d(F.pad(x, (1, 1, 1, 1)), P['conv3_w'], P['conv3_b'], stride=1))   # SAME 11->11
+  return x.permute(0, 2, 3, 1).reshape(x.shape[0], -1)
+
+
+def forward(P, x_nhwc):
+  """NatureDQN q-values (B, A) or Rainbow logits (B, A*N): fc1 + ReLU, fc2."""
+  h = F.relu(F.linear(torso(P, x_nhwc), P['fc1_w'], P['fc1_b']))
+  return F.linear(h, P['fc2_w'], P['fc2_b'])
+
+
+def iqn_forward(P, x_nhwc, taus):
+  """ImplicitQuantileNetwork (atari_lib.py:147-199): taus (N*B,) rows ordered
+  q*B + b; returns quantile values (N*B, A)."""
+  state = torso(P, x_nhwc)
+  B = state.shape[0]
+  nq = taus.shape[0] // B
+  E = P['emb_w'].shape[1]
+  tiled = state.repeat(nq, 1)
+  i_pi = torch.arange(1, E + 1, dtype=torch.float64) * math.pi
+  emb = torch.cos(taus.reshape(-1, 1) * i_pi)
+  emb = F.relu(F.linear(emb, P['emb_w'], P['emb_b']))
+  h = F.relu(F.linear(tiled * emb, P['fc1_w'], P['fc1_b']))
+  return F.linear(h, P['fc2_w'], P['fc2_b'])
+
+
+def to_input(x_float32_nhwc):
+  """The network input the reference computes in fp32 (uint8 / 255.), as float64."""
+  return torch.as_tensor(np.asarray(x_float32_nhwc), dtype=torch.float32).double()

@@ -199,12 +199,50 @@ def gen_checkpoint(m):
                       **{n: np.asarray(v) for n, v in zip(names, batch)})
 
 
+def gen_checkpoint_per(m):
+  """A prioritized checkpoint written by the reference's save (crb:612-657 via
+  prb:36-252): the `sum_tree` member is the reference's pickled SumTree object.  Plus
+  what the reference samples after loading it (random.seed(17)).  The test loads it
+  through a restricted unpickler (classes whitelisted, nothing else executes)."""
+  import shutil
+  prb = m['prioritized_replay_buffer']
+  tf = sys.modules['tensorflow']
+  tf.gfile = types.SimpleNamespace(Exists=os.path.exists, Open=open, Remove=os.remove)
+  tf.errors = types.SimpleNamespace(NotFoundError=FileNotFoundError)
+  kw = dict(observation_shape=(6, 6), stack_size=4, replay_capacity=40, batch_size=4,
+            update_horizon=3, gamma=0.9)
+  mem = prb.OutOfGraphPrioritizedReplayBuffer(**kw)
+  rs = np.random.RandomState(6)
+  for i in range(61):
+    mem.add(rs.randint(0, 256, (6, 6)).astype(np.uint8), int(rs.randint(0, 5)),
+            float(rs.randn()), bool(i % 11 == 10), np.float32(rs.uniform(0.1, 2.0)))
+  mem.set_priority(np.array([5, 9, 5, 30], np.int32), np.array([0.3, 2.5, 0.7, 1.1], np.float32))
+  d = os.path.join(OUT, 'ckpt_per')
+  shutil.rmtree(d, ignore_errors=True)
+  os.makedirs(d)
+  mem.save(d, 3)
+  fresh = prb.OutOfGraphPrioritizedReplayBuffer(**kw)
+  fresh.load(d, 3)
+  random.seed(17)
+  batch = fresh.sample_transition_batch(batch_size=4)
+  names = [e.name for e in fresh.get_transition_elements(4)]
+  out = {n: np.asarray(v) for n, v in zip(names, batch)}
+  out['nodes'] = np.concatenate(fresh.sum_tree.nodes)
+  out['maxrec'] = np.float64(fresh.sum_tree.max_recorded_priority)
+  out['rng_state'] = _pystate_words()
+  np.savez_compressed(os.path.join(OUT, 'ckpt_per_expected.npz'), **out)
+
+
 if __name__ == '__main__':
   mods = _load_reference()
+  if sys.argv[1:] == ['ckpt_per']:
+    gen_checkpoint_per(mods)
+    sys.exit(0)
   gen_sumtree(mods)
   gen_replay(mods, prioritized=False)
   gen_replay(mods, prioritized=True)
   gen_checkpoint(mods)
+  gen_checkpoint_per(mods)
   for f in sorted(os.listdir(OUT)):
     if f.endswith('.npz'):
       print(f, os.path.getsize(os.path.join(OUT, f)))

@@ -22,7 +22,7 @@ STEPS = 12
 CAP = 30000
 
 
-def _agent(pg, seed):
+def _agent(pg, seed, net_seed=0, **kw):
   from dopamine_amd.agents.optimizers import AdamOptimizer
   from dopamine_amd.agents.rainbow.rainbow_agent import RainbowAgent
   import bench
@@ -31,7 +31,7 @@ def _agent(pg, seed):
                        min_replay_history=100, update_period=4, target_update_period=40,
                        optimizer=AdamOptimizer(learning_rate=6.25e-5, epsilon=1.5e-4),
                        replay_capacity=CAP, batch_size=32, device=torch.device('cuda', 0),
-                       seed=0, process_group=pg)
+                       seed=net_seed, process_group=pg, **kw)
   random.seed(seed)
   bench.fill_synthetic(agent._replay.memory, 9, seed=1 + seed)
   return agent
@@ -48,7 +48,7 @@ def _run(agent, loop=False):
   return agent.online_convnet.fp.flat.detach().cpu().clone()
 
 
-def _worker(rank, world, port, same_seed, q, loop=False):
+def _worker(rank, world, port, same_seed, q, loop=False, net_seed_per_rank=False):
   import sys
   sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
   import torch.distributed as dist
@@ -57,9 +57,11 @@ def _worker(rank, world, port, same_seed, q, loop=False):
   torch.cuda.set_device(0)
   dist.init_process_group('gloo', rank=rank, world_size=world)
   from dopamine_amd import parallel
-  agent = _agent(dist.group.WORLD, 0 if same_seed else rank)
+  agent = _agent(dist.group.WORLD, 0 if same_seed else rank,
+                 net_seed=1000 * rank if net_seed_per_rank else 0)
   flat = _run(agent, loop)
   ok = parallel.replicas_in_sync(agent.online_convnet.fp.flat)
+  ok = ok and parallel.replicas_in_sync(agent.target_convnet.fp.flat)
   if rank == 0:
     q.put((ok, flat.numpy()))
   dist.barrier()
@@ -74,11 +76,12 @@ def _free_port():
   return p
 
 
-def _two_ranks(same_seed, loop=False):
+def _two_ranks(same_seed, loop=False, net_seed_per_rank=False):
   ctx = mp.get_context('spawn')
   q = ctx.Queue()
   port = _free_port()
-  procs = [ctx.Process(target=_worker, args=(r, 2, port, same_seed, q, loop)) for r in range(2)]
+  procs = [ctx.Process(target=_worker, args=(r, 2, port, same_seed, q, loop, net_seed_per_rank))
+           for r in range(2)]
   for p in procs:
     p.start()
   ok, flat = q.get(timeout=400)
@@ -108,3 +111,56 @@ def test_two_ranks_learner_loop_equal_single_learner_bitwise():
   assert ok
   single = _run(_agent(None, 0)).numpy()
   assert np.array_equal(flat, single)
+
+
+def _mean_gradient_reference(loop=False):
+  """Both ranks' learners in ONE process, no collective: each _train_step computes
+  its own gradient (the optimizer deferred), the two flat gradients are averaged
+  ((gA + gB) * 0.5, what gloo's sum + scale gives), and the TF1 Adam step is applied
+  to that mean on both replicas; target syncs run after the update, as in
+  _train_step.  SURVEY 8(e): the multi-GPU gradient = the mean of the ranks'
+  single-GPU gradients on their own minibatches (PER weights per rank)."""
+  from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
+  import random
+  agents = []
+  for r in range(2):
+    ag = _agent(None, r, use_hip_graph=False, fuse_optimizer=False)
+    ag._replay.memory._rng.stream = random.Random(r)   # each rank's own `random`, as its process
+    agents.append(ag)
+  steps = []
+  for ag in agents:
+    ag._device_opt_step = lambda k, ag=ag: steps.append((ag, k))
+    ag._sync_target = lambda ag=ag: steps.append((ag, 'sync'))
+  for _ in range(STEPS * agents[0].update_period):
+    steps.clear()
+    for ag in agents:
+      ag._train_step()
+    opt = [(ag, k) for ag, k in steps if k != 'sync']
+    if opt:
+      assert len(opt) == 2 and opt[0][1] == opt[1][1]
+      g = (agents[0].online_convnet.fp.grad + agents[1].online_convnet.fp.grad) * 0.5
+      for ag, k in opt:
+        ag.online_convnet.fp.grad.copy_(g)
+        ag._opt.step(ag.online_convnet.fp.grad, slot=k)
+    for ag, k in steps:
+      if k == 'sync':
+        DQNAgent._sync_target(ag)
+  torch.cuda.synchronize()
+  a, b = (ag.online_convnet.fp.flat.cpu().numpy() for ag in agents)
+  assert np.array_equal(a, b)
+  return a
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize('loop', [False, True])
+def test_two_ranks_different_data_equal_mean_gradient_reference(loop):
+  """Different buffers AND different network seeds per rank (rank 0's networks are
+  broadcast at construction): after 12 steps the parameters equal -- bit for bit --
+  a single process applying TF1 Adam to the mean of the two ranks' gradients.  An
+  unreduced, double-counted or mis-ordered all-reduce changes the result."""
+  ok, flat = _two_ranks(same_seed=False, loop=loop, net_seed_per_rank=True)
+  assert ok
+  ref = _mean_gradient_reference(loop)
+  assert np.array_equal(flat, ref)
+  lone = _run(_agent(None, 0)).numpy()        # rank 0 alone differs: the reduction did something
+  assert not np.array_equal(flat, lone)

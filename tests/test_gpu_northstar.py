@@ -1,0 +1,260 @@
+"""The north-star parity check on the EXACT benchmarked path.
+
+BASELINE.json north_star: "Q-values/losses within 1e-5 fp32 of the reference CPU
+path on identical sampled minibatches (bit-exact sampled indices for a fixed seed)".
+
+The agent is built as bench.py builds it -- 1M-transition buffer, B = 32, HIP
+graphs, riders, the fused Rainbow head, the fused TF1 optimizer -- and driven by
+``train_gradient_steps`` (one single-step graph replay, then 4-step chunk graphs),
+with ``enable_trace()`` copying every step's batch, network outputs, loss outputs and
+flat gradient aside.  In lockstep, a float64 CPU restatement runs the same steps from
+the same snapshot (parameters, optimizer state, sum tree, Python/numpy RNG state):
+
+* indices and the RNG state: the oracle sampler (oracle/replay.py, pinned to the
+  reference's own outputs) must draw the same indices, bit for bit;
+* the gathered batch: bit for bit (stacks, n-step rewards, terminals, probabilities);
+* network outputs (Rainbow logits / DQN Q-values, online on s and target on s'):
+  float64 Nature-CNN (oracle/nature_cnn.py) -- max |err| <= 1e-5 * max |ref|;
+* per-sample losses: max |err| <= 1e-5 * max |ref|; Rainbow's new priorities
+  sqrt(CE + 1e-10): |err| <= 1e-5 * |ref| elementwise (fp64 c51 / Huber oracle);
+* the flat gradient: per parameter tensor, max |err| <= GRAD_TOL * max |ref|;
+* after each chunk, the parameters vs the float64 optimizer trajectory (TF1 Adam /
+  centered RMSProp in float64 from the same state): |err| <= PARAM_ATOL.
+The oracle's sum tree takes the device's float32 priorities after they are checked,
+so the next step samples from the same tree (identical minibatches).  Measured errors
+are printed as one JSON line ("northstar_errors") for DESIGN.md.
+"""
+import json
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import learner as OL
+from oracle import nature_cnn as ONC
+from oracle import replay as OR
+
+pytestmark = pytest.mark.gpu
+
+Q_TOL = 1e-5         # north_star: Q-values / logits and losses
+GRAD_TOL = 1e-5      # flat gradient, per tensor, relative to the tensor's max |g|
+PARAM_ATOL = 5e-8    # parameters after fp32 updates vs the float64 trajectory (|w| ~ 0.05)
+CHUNKS = 3
+
+
+class DeviceFrames(object):
+  """The oracle's ``observation`` array backed by the device frame store: rows are
+  fetched on demand (the synthetic 1M-frame store is 7 GB and lives in HBM)."""
+
+  def __init__(self, frames, shape):
+    self.f, self.shape = frames, tuple(shape)
+
+  def __getitem__(self, idx):
+    ii = torch.as_tensor(np.asarray(idx, np.int64).reshape(-1), device=self.f.device)
+    return self.f[ii].cpu().numpy().reshape((-1,) + self.shape)
+
+
+def _oracle_replay(agent, prioritized):
+  mem = agent._replay.memory
+  C, B = mem._replay_capacity, agent._batch_size
+  cls = OR.PrioritizedOracle if prioritized else OR.ReplayOracle
+  orc = cls((84, 84), 4, C, B, update_horizon=agent.update_horizon, gamma=agent.gamma)
+  orc.observation = DeviceFrames(mem._frames, (84, 84))
+  orc.action = mem._actions.cpu().numpy()
+  orc.reward = mem._rewards.cpu().numpy()
+  orc.terminal = mem._terminals.cpu().numpy()
+  orc.add_count = int(mem.add_count)
+  orc.invalid_range = OR.invalid_range(orc.cursor(), C, 4, agent.update_horizon)
+  if prioritized:
+    orc.sum_tree.nodes = mem._tree.cpu().numpy().copy()
+    orc.sum_tree.max_recorded_priority = mem.sum_tree.max_recorded_priority
+    py = random.Random()
+    py.setstate(random.getstate())
+    orc.py_rng = py
+  else:
+    rs = np.random.RandomState()
+    rs.set_state(np.random.get_state())
+    orc.np_rng = rs
+  return orc
+
+
+def _rel(got, ref):
+  got, ref = np.asarray(got, np.float64), np.asarray(ref, np.float64)
+  return float(np.abs(got - ref).max() / max(np.abs(ref).max(), 1e-30))
+
+
+class _Adam64(object):
+  def __init__(self, opt, k0):
+    f = lambda x: np.float64(np.float32(x))
+    self.lr, self.b1, self.b2, self.eps = f(opt.lr), f(opt.b1), f(opt.b2), f(opt.eps)
+    self.m = opt.m.cpu().double().numpy().copy()
+    self.v = opt.v.cpu().double().numpy().copy()
+    st = opt.state.cpu().double().numpy()
+    self.b1p, self.b2p = st[2 * k0], st[2 * k0 + 1]
+
+  def step(self, w, g):
+    alpha = self.lr * np.sqrt(1 - self.b2p) / (1 - self.b1p)
+    self.m += (g - self.m) * (1 - self.b1)
+    self.v += (g * g - self.v) * (1 - self.b2)
+    w -= alpha * self.m / (np.sqrt(self.v) + self.eps)
+    self.b1p *= self.b1
+    self.b2p *= self.b2
+
+
+class _RMSProp64(object):
+  def __init__(self, opt, k0):
+    f = lambda x: np.float64(np.float32(x))
+    self.lr, self.rho, self.mu, self.eps = f(opt.lr), f(opt.decay), f(opt.mu), f(opt.eps)
+    self.ms = opt.ms.cpu().double().numpy().copy()
+    self.mg = opt.mg.cpu().double().numpy().copy()
+    self.mom = opt.mom.cpu().double().numpy().copy()
+
+  def step(self, w, g):
+    self.ms += (g * g - self.ms) * (1 - self.rho)
+    self.mg += (g - self.mg) * (1 - self.rho)
+    self.mom = self.mom * self.mu + g * self.lr / np.sqrt(self.ms - self.mg * self.mg + self.eps)
+    w -= self.mom
+
+
+def _prime(agent):
+  n = 0
+  while not agent.graphs_primed():
+    agent.train_gradient_steps(5)
+    n += 5
+    assert n < 200, 'graphs never captured'
+  # restart the pipeline at a clean RNG point: the prefetched batch's draws are given
+  # back, so the next step samples again (eagerly) from a known host RNG state
+  agent._discard_prefetch()
+  agent._replay.memory.sync_rng()
+  torch.cuda.synchronize()
+
+
+def _run_lockstep(agent, kind):
+  """Drive the bench path and the float64 oracle in lockstep; returns the errors."""
+  mem = agent._replay.memory
+  prioritized = kind == 'rainbow'
+  B = agent._batch_size
+  A = agent.num_actions
+  offsets = agent.online_convnet.fp.offsets
+  k0 = agent._opt_steps % 2
+  w = agent.online_convnet.fp.flat.cpu().double().numpy().copy()
+  tw = agent.target_convnet.fp.flat.cpu().double().numpy().copy()
+  opt = _Adam64(agent._opt, k0) if kind == 'rainbow' else _RMSProp64(agent._opt, k0)
+  orc = _oracle_replay(agent, prioritized)
+  T64 = ONC.Params64(tw, offsets)
+  cg = np.float64(np.float32(agent.cumulative_gamma))
+  if prioritized:
+    support = agent._support.cpu().double().numpy()
+  errs = dict(logits=0.0, target=0.0, loss=0.0, loss_elementwise=0.0, priorities=0.0, grad={},
+              params=0.0)
+  U = agent._UNROLL
+
+  def step(slot):
+    tr = {k: v[slot].cpu().numpy() for k, v in agent._trace.items()}
+    idx = orc.sample_index_batch(B)
+    np.testing.assert_array_equal(tr['indices'], idx)
+    b = orc.sample_transition_batch(B, indices=idx)
+    st, act, rew, nst, nact, nrew, term = b[:7]
+    for name, ref in (('action', act), ('reward', rew), ('terminal', term),
+                      ('next_action', nact), ('next_reward', nrew)):
+      np.testing.assert_array_equal(tr[name], ref, err_msg=name)
+    if prioritized:
+      np.testing.assert_array_equal(tr['sampling_probabilities'], b[8])
+    x = np.moveaxis(st, -1, 1).astype(np.float32) / np.float32(255)
+    nx = np.moveaxis(nst, -1, 1).astype(np.float32) / np.float32(255)
+    np.testing.assert_array_equal(tr['state'], x)            # NCHW view of the NHWC batch
+    np.testing.assert_array_equal(tr['next_state'], nx)
+    P = ONC.Params64(w, offsets)
+    out = ONC.forward(P, ONC.to_input(np.moveaxis(x, 1, -1)))
+    with torch.no_grad():
+      tout = ONC.forward(T64, ONC.to_input(np.moveaxis(nx, 1, -1)))
+    errs['logits'] = max(errs['logits'], _rel(tr['online_out'], out.detach().numpy()))
+    errs['target'] = max(errs['target'], _rel(tr['target_out'], tout.numpy()))
+    if prioritized:
+      N = support.shape[0]
+      ref = OL.c51_loss(out.detach().numpy().reshape(B, A, N), tout.numpy().reshape(B, A, N),
+                        act, rew, term, support, cg, b[8], dtype=np.float64)
+      errs['priorities'] = max(errs['priorities'],
+                               float((np.abs(tr['priorities'] - ref['priorities']) /
+                                      np.abs(ref['priorities'])).max()))
+      gout = ref['grad'].reshape(B, A * N)
+    else:
+      ref = OL.dqn_huber(out.detach().numpy(), tout.numpy(), act, rew, term, cg, dtype=np.float64)
+      gout = ref['grad']
+    # the loss vector relative to its scale (a Huber loss of a near-zero TD error is
+    # 0.5 e^2: its elementwise relative error is that of e, amplified -- reported too)
+    errs['loss'] = max(errs['loss'], _rel(tr['loss'], ref['loss']))
+    errs['loss_elementwise'] = max(errs['loss_elementwise'], float(
+        (np.abs(tr['loss'] - ref['loss']) / np.maximum(np.abs(ref['loss']), 1e-30)).max()))
+    out.backward(torch.from_numpy(gout))
+    g = P.flat_grad()
+    for name, (o, shape) in offsets.items():
+      n = int(np.prod(shape))
+      e = _rel(tr['grad'][o:o + n], g[o:o + n])
+      errs['grad'][name] = max(errs['grad'].get(name, 0.0), e)
+    opt.step(w, g)
+    if prioritized:   # the next step samples the tree the device wrote
+      orc.set_priority(np.asarray(idx, np.int32), tr['priorities'].astype(np.float32))
+
+  eager0 = dict(agent._eager_steps)
+  agent.train_gradient_steps(1)                 # the single-step graph of parity k0
+  torch.cuda.synchronize()
+  step(U + k0)
+  for _ in range(CHUNKS):
+    assert agent._chunk_ok()
+    agent.train_gradient_steps(U)               # ONE chunk-graph replay
+    torch.cuda.synchronize()
+    for j in range(U):
+      step(j)
+    gw = agent.online_convnet.fp.flat.cpu().double().numpy()
+    errs['params'] = max(errs['params'], float(np.abs(gw - w).max()))
+  assert agent._eager_steps == eager0, 'a step ran eagerly: not the bench path'
+  # the host RNG stream ends where the oracle's sequential draws leave it
+  agent._discard_prefetch()
+  mem.sync_rng()
+  if prioritized:
+    assert random.getstate() == orc.py_rng.getstate()
+  else:
+    a, b = np.random.get_state(), orc.np_rng.get_state()
+    assert np.array_equal(a[1], b[1]) and a[2] == b[2]
+  return errs
+
+
+def _check(errs, kind):
+  print(json.dumps({'northstar_errors': kind, **errs}), flush=True)
+  assert errs['logits'] <= Q_TOL, errs
+  assert errs['target'] <= Q_TOL, errs
+  assert errs['loss'] <= Q_TOL, errs
+  assert errs['priorities'] <= Q_TOL, errs
+  assert max(errs['grad'].values()) <= GRAD_TOL, errs
+  assert errs['params'] <= PARAM_ATOL, errs
+
+
+@pytest.mark.timeout(600)
+def test_rainbow_bench_path_matches_float64_oracle():
+  """Config 3 exactly as bench.py runs it: Rainbow/C51, PER, n = 3, 1M buffer, B = 32."""
+  import bench
+  torch.cuda.set_device(0)
+  agent = bench.build_agent(9, 1_000_000, 32, torch.device('cuda', 0))
+  agent.enable_trace()
+  random.seed(0)
+  bench.fill_synthetic(agent._replay.memory, 9, seed=1)
+  _prime(agent)
+  _check(_run_lockstep(agent, 'rainbow'), 'rainbow')
+
+
+@pytest.mark.timeout(600)
+def test_dqn_pong_bench_path_matches_float64_oracle():
+  """Config 2: DQN on Pong's 6 actions, uniform replay (numpy's legacy stream), n = 1,
+  TF1 centered RMSProp, 1M buffer, B = 32, the same graph / chunk path."""
+  import bench
+  from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
+  torch.cuda.set_device(0)
+  agent = DQNAgent(num_actions=6, replay_capacity=1_000_000, batch_size=32,
+                   device=torch.device('cuda', 0))
+  agent.enable_trace()
+  np.random.seed(0)
+  bench.fill_synthetic(agent._replay.memory, 6, seed=2)
+  _prime(agent)
+  _check(_run_lockstep(agent, 'dqn'), 'dqn')
