@@ -67,6 +67,19 @@ class CnnNet(ctypes.Structure):
               ('ws', ctypes.c_void_p)]
 
 
+class IqnHead(ctypes.Structure):
+  _fields_ = [('embed_dim', ctypes.c_int32), ('num_actions', ctypes.c_int32)] + [
+      (n, ctypes.c_void_p) for n in ('emb_w', 'emb_b', 'fc1_w', 'fc1_b', 'fc2_w', 'fc2_b')]
+
+
+class IqnActs(ctypes.Structure):
+  _fields_ = [(n, ctypes.c_void_p) for n in ('cos', 'emb', 'x', 'h', 'q')]
+
+
+class IqnGrads(ctypes.Structure):
+  _fields_ = [(n, ctypes.c_void_p) for n in ('dh', 'dpre', 'dtl')]
+
+
 class Rider(ctypes.Structure):
   """dq_rider: a recorded replay operation (opaque)."""
   _fields_ = [('words', ctypes.c_int64 * 40)]
@@ -139,8 +152,18 @@ SIGNATURES = {
                               ctypes.POINTER(CnnActs), _P, ctypes.POINTER(CnnActs), _P, _I32, _I32,
                               _P],
     'dq_cnn_workspace_floats': [_I32, _I32],
+    'dq_cnn_forward_torso': [ctypes.POINTER(CnnParams), _I32, _P, ctypes.POINTER(CnnActs), _P, _P],
+    'dq_cnn_backward_torso': [ctypes.POINTER(CnnParams), ctypes.POINTER(CnnParams), _I32, _P,
+                              ctypes.POINTER(CnnActs), ctypes.POINTER(CnnActs), _P, _P],
+    'dq_iqn_head_forward': [ctypes.POINTER(IqnHead), _I32, _I32, _P, _P, ctypes.POINTER(IqnActs),
+                            _P, _P],
+    'dq_iqn_head_backward': [ctypes.POINTER(IqnHead), ctypes.POINTER(IqnHead), _I32, _I32, _P,
+                             ctypes.POINTER(IqnActs), _P, ctypes.POINTER(IqnGrads), _P, _P, _P],
+    'dq_iqn_workspace_floats': [_I32, _I32, _I32, _I32],
+    'dq_uniform_draw': [_P, ctypes.c_uint64, _I64, _P, _P],
 }
 RESTYPES = {'dq_last_error': ctypes.c_char_p, 'dq_cnn_workspace_floats': ctypes.c_size_t,
+            'dq_iqn_workspace_floats': ctypes.c_size_t,
             'dq_cnn_fc2_parts_offset': ctypes.c_size_t}
 
 

@@ -202,6 +202,9 @@ class DQNAgent(object):
     if self._hip is not None:
       d['online_out'] = self._hip['online'].acts['out']
       d['target_out'] = self._hip['target'][c].acts['out']
+    elif getattr(self, '_last_online_out', None) is not None and 'q' in (self._ptgt[c] or {}):
+      d['online_out'] = self._last_online_out       # the PyTorch-network path (e.g. CartPole)
+      d['target_out'] = self._ptgt[c]['q']
     return d
 
   def _trace_step(self, slot, c):
@@ -276,6 +279,7 @@ class DQNAgent(object):
   def _online_loss(self, t, tgt):
     """dqn_agent.py:283-322."""
     q = self._online_forward(t['state'])
+    self._last_online_out = q
     out = ops.dqn_huber_loss(q.detach(), tgt['q'], t['action'], t['reward'], t['terminal'],
                              self.cumulative_gamma, out=self._loss_out)
     return q, out['grad']

@@ -1,11 +1,18 @@
 """IQN agent (reference implicit_quantile_agent.py:36-321).
 
-Online net on s with N tau samples, target net on s' with N' samples, greedy
-next action from the mean of K target (or online, double_dqn) quantiles; the
+Online net on s with N tau samples, target net on s' with N' samples, greedy next
+action from the mean of K target (or online, double_dqn) quantiles; the
 quantile-Huber loss and its gradient are one HIP kernel (``dq_iqn_loss``).
-Tau samples come from torch's device RNG (the reference's tf.random_uniform
-stream cannot be reproduced without TF: parity is on given taus).
+
+With the Atari geometry the ImplicitQuantileNetwork runs on the HIP kernels
+(dopamine_amd/iqn.py): the Nature-CNN torso on nature_cnn.hip and the quantile head
+(cosine embedding, Hadamard product, FC 7744 -> 512 -> A and their backward) on the
+fp32 matrix cores (iqn.hip).  The target net's N' and K quantile rows share one torso
+pass and one head pass (R = (N' + K) * B rows).  Tau samples come from a device
+counter-based generator (TF's tf.random_uniform stream cannot be reproduced without
+TF: parity is on given taus), so a captured HIP graph draws what eager calls draw.
 """
+import numpy as np
 import torch
 
 from dopamine_amd import ops
@@ -46,10 +53,33 @@ class ImplicitQuantileAgent(rainbow_agent.RainbowAgent):
     return self.network(self.num_actions, quantile_embedding_dim=self.quantile_embedding_dim,
                         stack_size=self.stack_size, device=self._device, seed=seed)
 
+  def _build_networks(self):
+    super()._build_networks()
+    self._iqn = None
+    if (self.use_hip_cnn and self.network is networks.ImplicitQuantileNetwork and
+        self.observation_shape == (84, 84) and self.stack_size == 4):
+      from dopamine_amd.iqn import HipIqnNet, TauSampler
+      B = self._batch_size
+      n_tgt = self.num_tau_prime_samples + (0 if self.double_dqn else self.num_quantile_samples)
+      self._iqn = dict(
+          online=HipIqnNet(self.online_convnet, B, self.num_tau_samples, keep=True),
+          target=[HipIqnNet(self.target_convnet, B, n_tgt, keep=False) for _ in range(2)])
+      if self.double_dqn:   # argmax from the ONLINE net on s' (iqn:205-214)
+        self._iqn['online_next'] = HipIqnNet(self.online_convnet, B, self.num_quantile_samples,
+                                             keep=False)
+      self._taus = TauSampler(0x5EED0000 + self._seed, self._device)
+
   def _build_train_op(self):
     B, A, dev = self._batch_size, self.num_actions, self._device
     self._loss_out = dict(grad=torch.empty((self.num_tau_samples * B, A), device=dev),
                           loss=torch.empty(B, device=dev), mean_loss=torch.empty(1, device=dev))
+
+  def mean_loss(self):
+    """mean over the batch of the quantile loss (the QuantileLoss summary, iqn:316-319)."""
+    return float(self._loss_out['mean_loss'].item())
+
+  def _needs_flat_grad(self):
+    return self._iqn is not None or super()._needs_flat_grad()
 
   def _post_loss(self, t):
     """No priority write-back: the reference IQN's train op never calls
@@ -60,7 +90,31 @@ class ImplicitQuantileAgent(rainbow_agent.RainbowAgent):
     qv, _ = self.online_convnet(x, self.num_quantile_samples)
     return qv.view(self.num_quantile_samples, x.shape[0], -1).mean(0)
 
+  def _q_values(self, state_np):
+    """Action selection (iqn:216-228 _q_values: the mean over K quantiles of the
+    online net), on the HIP executor at batch 1."""
+    if self._iqn is None:
+      return super()._q_values(state_np)
+    if 'act' not in self._iqn:
+      from dopamine_amd.iqn import HipIqnNet
+      self._iqn['act'] = HipIqnNet(self.online_convnet, 1, self.num_quantile_samples, keep=False)
+    ex = self._iqn['act']
+    scale = 1.0 / 255.0 if np.dtype(self.observation_dtype) == np.uint8 else 1.0
+    x = torch.as_tensor(np.asarray(state_np) * scale, dtype=torch.float32, device=self._device)
+    self._taus.draw(ex.taus)
+    q, _ = ex.forward(x.reshape(1, 84, 84, 4).contiguous())
+    return q.view(self.num_quantile_samples, 1, -1).mean(0)
+
   def _target_forward(self, t, slot):
+    if self._iqn is not None:
+      ex = self._iqn['target'][slot]
+      self._taus.draw(ex.taus)          # N' tau' (iqn:197-199) then K argmax samples (:200-204)
+      q, _ = ex.forward(t['next_state'])
+      npb = self.num_tau_prime_samples * self._batch_size
+      out = {'tq': q[:npb]}
+      if not self.double_dqn:
+        out['ta'] = q[npb:]
+      return out
     with torch.no_grad():
       tq, _ = self.target_convnet(t['next_state'], self.num_tau_prime_samples)
       out = {'tq': tq}
@@ -71,10 +125,36 @@ class ImplicitQuantileAgent(rainbow_agent.RainbowAgent):
   def _online_loss(self, t, tgt):
     """implicit_quantile_agent.py:190-321."""
     ta = tgt.get('ta')
-    if ta is None:
-      with torch.no_grad():
-        ta, _ = self.online_convnet(t['next_state'], self.num_quantile_samples)
-    qv, taus = self.online_convnet(t['state'], self.num_tau_samples)
+    if self._iqn is not None:
+      if ta is None:
+        ex = self._iqn['online_next']
+        self._taus.draw(ex.taus)
+        ta, _ = ex.forward(t['next_state'])
+      on = self._iqn['online']
+      self._taus.draw(on.taus)
+      qv, taus = on.forward(t['state'])
+    else:
+      if ta is None:
+        with torch.no_grad():
+          ta, _ = self.online_convnet(t['next_state'], self.num_quantile_samples)
+      qv, taus = self.online_convnet(t['state'], self.num_tau_samples)
     out = ops.iqn_loss(qv.detach(), tgt['tq'], ta, taus, t['action'], t['reward'], t['terminal'],
                        self.cumulative_gamma, self.kappa, out=self._loss_out)
+    self._last_ta = ta
     return qv, out['grad']
+
+  def _backward(self, y, g, k=0):
+    if self._iqn is not None:
+      self._iqn['online'].backward(g)
+      return
+    super()._backward(y, g, k)
+
+  def _trace_outputs(self, c):
+    d = rainbow_agent.dqn_agent.DQNAgent._trace_outputs(self, c)
+    if self._iqn is not None:
+      on, tg = self._iqn['online'], self._iqn['target'][c]
+      d['qv'] = on.acts['q']
+      d['taus'] = on.taus
+      d['target_q'] = tg.acts['q']
+      d['target_taus'] = tg.taus
+    return d

@@ -1,0 +1,204 @@
+// The implicit-quantile head of ImplicitQuantileNetwork (atari_lib.py:147-199) and its
+// backward, on the exact-fp32 matrix cores (v_mfma_f32_32x32x2_f32) through the tile
+// engine of cnn_tile.h.  The Nature-CNN torso runs on nature_cnn.hip
+// (dq_cnn_forward_torso / dq_cnn_backward_torso); this file owns everything after
+// the 7744-wide state vector.
+//
+// Rows: R = nq * B quantile rows, row r = q * B + b (tf.tile of the state, atari_lib.py:174),
+// so the state row of r is r % B.  E = quantile_embedding_dim, F = 7744, H = 512.
+//
+//   forward                                                   (FLOP at R = 4096, E = 64)
+//     cos[r][i] = cos((i+1) * pi * tau[r])                     atari_lib.py:176-178
+//     emb = relu(cos We^T + be); x = state[r % B] * emb         :179-185     4.1 G  (1 launch)
+//     h   = relu(x W1^T + b1)                                   :186-188    32.5 G  (split-K 4 + sum)
+//     q   = h W2^T + b2                                         :189-191    small
+//   backward (TF autodiff of the same graph)
+//     dh   = (dq W2) * (h > 0);   dW2 | db2 = dq^T [h | 1]
+//     dx   = dh W1  ->  d tiled = dx * emb,  d pre = (emb > 0) ? dx * state : 0     32.5 G
+//     dW1 | db1 = dh^T [x | 1]                                                     32.5 G
+//     dWe | dbe = dpre^T [cos | 1]                                                   4.1 G
+//     d state[b] = (state[b] > 0) * sum_q d tiled[q B + b]   (the torso's ReLU, then its backward)
+// The 7744-wide intermediates (emb, x, d tiled, d pre: 127 MB each at R = 4096) are
+// kept in HBM: each is written once and read by the next GEMM as a streamed operand.
+#include "cnn_tile.h"
+
+namespace dq {
+namespace iqn {
+
+using namespace dq::cnn;
+
+constexpr int F = 11 * 11 * 64;   // 7744, the torso's state vector
+constexpr int H = 512;
+constexpr int kSplitFc1 = 4;      // h = relu(x W1^T + b1): K = 7744, 4 slabs (R/128 x 4 tiles x 4)
+constexpr int kSplitW1 = 2;       // dW1: K = R
+constexpr int kSplitWe = 8;       // dWe: K = R, 61 row tiles
+constexpr int kSplitW2 = 32;      // dW2: M = A, K = R
+
+__global__ __launch_bounds__(256) void k_cos_embedding(const float* __restrict__ tau, int64_t n,
+                                                        int E, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t r = i / E;
+  const int k = (int)(i - r * E);
+  const float pi = 3.14159265358979323846f;           // tf.constant(math.pi), float32
+  // tf.cast(tf.range(1, E + 1), float32) * pi * quantile_net, left to right, then tf.cos
+  out[i] = cosf(__fmul_rn(__fmul_rn((float)(k + 1), pi), tau[r]));
+}
+
+// emb = relu(acc + be[n]) (kept for the backward if emb != null); x = state[r % B][n] * emb
+struct EpiEmb {
+  float* emb;
+  float* x;
+  const float* bias;
+  const float* state;
+  int B;
+  __device__ __forceinline__ void operator()(int m, int n, float v, int) const {
+    const float e = fmaxf(__fadd_rn(v, bias[n]), 0.0f);
+    const int64_t i = (int64_t)m * F + n;
+    if (emb) emb[i] = e;
+    x[i] = __fmul_rn(state[(int64_t)(m % B) * F + n], e);
+  }
+};
+
+// dx -> d tiled = dx * emb, d pre = (emb > 0) ? dx * state[r % B] : 0  (Mul + ReluGrad)
+struct EpiDx {
+  float* dtl;
+  float* dpre;
+  const float* emb;
+  const float* state;
+  int B;
+  __device__ __forceinline__ void operator()(int m, int n, float v, int) const {
+    const int64_t i = (int64_t)m * F + n;
+    const float e = emb[i];
+    dtl[i] = __fmul_rn(v, e);
+    dpre[i] = e > 0.0f ? __fmul_rn(v, state[(int64_t)(m % B) * F + n]) : 0.0f;
+  }
+};
+
+// tf.tile's gradient (the sum over the nq copies, q in order) and the torso's last ReLU
+__global__ __launch_bounds__(256) void k_tile_grad(const float* __restrict__ dtl,
+                                                    const float* __restrict__ state, int B, int nq,
+                                                    float* __restrict__ dstate) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)B * F) return;
+  float s = 0.0f;
+  for (int q = 0; q < nq; ++q) s = __fadd_rn(s, dtl[(int64_t)q * B * F + i]);
+  dstate[i] = state[i] > 0.0f ? s : 0.0f;
+}
+
+void forward(Ctx& c, const dq_iqn_head* hp, int B, int nq, const float* state, const float* tau,
+             const dq_iqn_acts* a) {
+  const int R = nq * B, E = hp->embed_dim, A = hp->num_actions;
+  if (!c.dry) {
+    const int64_t n = (int64_t)R * E;
+    hipLaunchKernelGGL(k_cos_embedding, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c.s, tau,
+                       n, E, a->cos);
+  }
+  gemm<4, 4, 1>(c, RowK{a->cos, E}, RowK{hp->emb_w, E}, EpiEmb{a->emb, a->x, hp->emb_b, state, B},
+                R, F, E);
+  gemm<4, 4, 1>(c, RowK{a->x, F}, RowK{hp->fc1_w, F}, EpiBiasAct{a->h, hp->fc1_b, H, true}, R, H,
+                F, kSplitFc1);
+  gemm<1, 1, 16>(c, RowK{a->h, H}, RowK{hp->fc2_w, H}, EpiBiasAct{a->q, hp->fc2_b, A, false}, R,
+                 A, H);
+}
+
+void backward(Ctx& c, const dq_iqn_head* hp, const dq_iqn_head* hg, int B, int nq,
+              const float* state, const dq_iqn_acts* a, const float* dq, dq_iqn_grads* d,
+              float* dstate) {
+  const int R = nq * B, E = hp->embed_dim, A = hp->num_actions;
+  gemm<1, 1, 16>(c, RowKScalar{dq, A}, ColK{hp->fc2_w, H}, EpiMask{d->dh, a->h, H}, R, H, A);
+  gemm<1, 4, 4>(c, ColKScalar{dq, A}, ColKOnes{a->h, H}, EpiGrad{hg->fc2_w, hg->fc2_b, H}, A,
+                H + 1, R, kSplitW2);
+  gemm<4, 4, 1>(c, RowK{d->dh, H}, ColK{hp->fc1_w, F}, EpiDx{d->dtl, d->dpre, a->emb, state, B},
+                R, F, H);
+  gemm<4, 4, 1>(c, ColK{d->dh, H}, ColKOnes{a->x, F}, EpiGrad{hg->fc1_w, hg->fc1_b, F}, H, F + 1,
+                R, kSplitW1);
+  gemm<4, 4, 1>(c, ColK{d->dpre, F}, ColKOnes{a->cos, E}, EpiGrad{hg->emb_w, hg->emb_b, E}, F,
+                E + 1, R, kSplitWe);
+  if (!c.dry) {
+    const int64_t n = (int64_t)B * F;
+    hipLaunchKernelGGL(k_tile_grad, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c.s, d->dtl,
+                       state, B, nq, dstate);
+  }
+}
+
+// U[0, 1) float32 draws of call `counter[0]` of a generator: a splitmix64 hash of (seed,
+// call, i), 24 random bits -> k * 2^-24.  The call counter lives on the device and is
+// bumped by a second one-thread launch, so replaying a captured graph draws new values
+// exactly as the same sequence of eager calls does.
+__global__ __launch_bounds__(256) void k_uniform_draw(const int64_t* __restrict__ counter,
+                                                       uint64_t seed, int64_t n,
+                                                       float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t z = seed + (uint64_t)counter[0] * 0x9E3779B97F4A7C15ull + (uint64_t)(i + 1) * 0xD1B54A32D192ED03ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  out[i] = (float)(z >> 40) * (1.0f / 16777216.0f);
+}
+
+__global__ void k_bump_counter(int64_t* counter) { counter[0] += 1; }
+
+}  // namespace iqn
+}  // namespace dq
+
+using namespace dq;
+
+static bool head_ok(const dq_iqn_head* h) {
+  return h && h->embed_dim >= 4 && h->embed_dim % 4 == 0 && h->num_actions >= 1 && h->emb_w &&
+         h->emb_b && h->fc1_w && h->fc1_b && h->fc2_w && h->fc2_b;
+}
+
+extern "C" {
+
+int dq_iqn_head_forward(const dq_iqn_head* hp, int32_t batch, int32_t nq, const float* state,
+                        const float* taus, dq_iqn_acts* a, float* ws, void* stream) {
+  DQ_CHECK_ARG(head_ok(hp) && state && taus && a && ws && batch >= 1 && nq >= 1, "bad arguments");
+  DQ_CHECK_ARG(a->cos && a->x && a->h && a->q, "null activation buffer");
+  DQ_CHECK_ARG((int64_t)batch * nq * iqn::F < ((int64_t)1 << 31), "R * 7744 must fit int32");
+  cnn::Ctx c{(hipStream_t)stream, ws, false, 0};
+  iqn::forward(c, hp, batch, nq, state, taus, a);
+  DQ_CHECK_LAUNCH("dq_iqn_head_forward");
+  return DQ_OK;
+}
+
+int dq_iqn_head_backward(const dq_iqn_head* hp, const dq_iqn_head* hg, int32_t batch, int32_t nq,
+                         const float* state, const dq_iqn_acts* a, const float* dq,
+                         dq_iqn_grads* d, float* dstate, float* ws, void* stream) {
+  DQ_CHECK_ARG(head_ok(hp) && head_ok(hg) && state && a && dq && d && dstate && ws && batch >= 1 &&
+               nq >= 1, "bad arguments");
+  DQ_CHECK_ARG(hg->embed_dim == hp->embed_dim && hg->num_actions == hp->num_actions,
+               "gradient head shape differs");
+  DQ_CHECK_ARG(a->cos && a->emb && a->x && a->h && d->dh && d->dtl && d->dpre,
+               "the backward needs the forward's emb (kept) and gradient buffers");
+  cnn::Ctx c{(hipStream_t)stream, ws, false, 0};
+  iqn::backward(c, hp, hg, batch, nq, state, a, dq, d, dstate);
+  DQ_CHECK_LAUNCH("dq_iqn_head_backward");
+  return DQ_OK;
+}
+
+int dq_uniform_draw(int64_t* counter, uint64_t seed, int64_t n, float* out, void* stream) {
+  DQ_CHECK_ARG(counter && out && n >= 0, "bad arguments");
+  if (n > 0)
+    hipLaunchKernelGGL(iqn::k_uniform_draw, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, counter, seed, n, out);
+  hipLaunchKernelGGL(iqn::k_bump_counter, dim3(1), dim3(1), 0, (hipStream_t)stream, counter);
+  DQ_CHECK_LAUNCH("dq_uniform_draw");
+  return DQ_OK;
+}
+
+size_t dq_iqn_workspace_floats(int32_t batch, int32_t nq, int32_t num_actions, int32_t embed_dim) {
+  dq_iqn_head h = {};
+  h.embed_dim = embed_dim;
+  h.num_actions = num_actions;
+  dq_iqn_acts a = {};
+  dq_iqn_grads d = {};
+  cnn::Ctx f{nullptr, nullptr, true, 0};
+  iqn::forward(f, &h, batch, nq, nullptr, nullptr, &a);
+  cnn::Ctx b{nullptr, nullptr, true, 0};
+  iqn::backward(b, &h, &h, batch, nq, nullptr, &a, nullptr, &d, nullptr);
+  return f.need > b.need ? f.need : b.need;
+}
+
+}  // extern "C"

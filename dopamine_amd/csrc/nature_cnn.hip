@@ -27,752 +27,12 @@
 #include <algorithm>
 
 
-#include "common.h"
-#include "replay_dev.h"
+#include "cnn_tile.h"
 
 #include <cstring>
 
 namespace dq {
 namespace cnn {
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-// ----------------------------------------------------------------- geometry
-template <int H_, int W_, int CI_, int KH_, int KW_, int S_, int PT_, int PL_, int OH_, int OW_, int CO_>
-struct Conv {
-  static constexpr int H = H_, W = W_, CI = CI_, KH = KH_, KW = KW_, S = S_, PT = PT_, PL = PL_;
-  static constexpr int OH = OH_, OW = OW_, CO = CO_;
-  static constexpr int K = KH * KW * CI;     // im2col depth
-  static_assert(CI % 4 == 0 && CO % 4 == 0, "16-byte operand groups need CI, CO % 4 == 0");
-};
-// TF SAME: conv1 84 -> 21 (pad 2/2), conv2 21 -> 11 (pad 1/2), conv3 11 -> 11 (pad 1/1)
-using Conv1 = Conv<84, 84, 4, 8, 8, 4, 2, 2, 21, 21, 32>;
-using Conv2 = Conv<21, 21, 32, 4, 4, 2, 1, 1, 11, 11, 64>;
-using Conv3 = Conv<11, 11, 64, 3, 3, 1, 1, 1, 11, 11, 64>;
-constexpr int kFlat = 11 * 11 * 64;   // 7744
-constexpr int kHidden = 512;
-
-__device__ __forceinline__ float4 zero4() { return make_float4(0.0f, 0.0f, 0.0f, 0.0f); }
-__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
-
-// ------------------------------------------------------------------ loaders
-// get(r, k, rlim, klim): the 16-byte group of 4 consecutive operand elements
-// along the contiguous dimension (k when kFast, else r) at (r, k), zero outside
-// [0, rlim) x [0, klim) and in conv padding.  Branch-free by construction: the
-// address is clamped to a valid one, the load always issues and a select zeroes
-// it, so the loads of a whole K slice stay in flight together (a divergent
-// fallback branch would make the compiler drain vmcnt at every join).
-// Vector loaders need the ragged dimension to be a multiple of 4 (a group is
-// wholly in or out); the scalar ones (ld = n_out) pay 4 loads per group.
-
-__device__ __forceinline__ float4 sel4(bool ok, float4 v) { return ok ? v : zero4(); }
-
-// Raw buffer loads: an offset at or past num_records reads as zero in hardware,
-// so an out-of-range group costs one offset select instead of a clamped 64-bit
-// address and four data selects.  Valid byte offsets are < 2 GB here.
-constexpr int kOOB = 0x7ffffff0;
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* base) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, kOOB, 0x00020000);
-}
-__device__ __forceinline__ float4 bload4(const float* base, int off, bool ok) {   // off in floats
-#ifdef DQ_ABLATE_LOADS   // timing experiments only: operands without memory traffic
-  const float f = ok ? (float)off * 1e-9f : 0.0f;
-  return make_float4(f, f, f, f);
-#endif
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc(base), ok ? off * 4 : kOOB, 0, 0);
-  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
-                     __uint_as_float(v.w));
-}
-__device__ __forceinline__ float bload1(const float* base, int off, bool ok) {
-  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc(base), ok ? off * 4 : kOOB, 0, 0));
-}
-
-// forward im2col of an NHWC input: rows = output pixels, k = (kh, kw, ci).
-// CI % 4 == 0, so a 16-byte group never straddles a (kh, kw) tap.
-template <class G>
-struct Im2col {
-  static constexpr bool kFast = true;
-  const float* x;
-  __device__ __forceinline__ int offset(int m, int k) const {   // -1 in the padding
-    const int b = m / (G::OH * G::OW), p = m - b * (G::OH * G::OW);
-    const int oh = p / G::OW, ow = p - oh * G::OW;
-    const int kk = k / G::CI, ci = k - kk * G::CI;
-    const int kh = kk / G::KW, kw = kk - kh * G::KW;
-    const int ih = oh * G::S - G::PT + kh, iw = ow * G::S - G::PL + kw;
-    if (ih < 0 || ih >= G::H || iw < 0 || iw >= G::W) return -1;
-    return ((b * G::H + ih) * G::W + iw) * G::CI + ci;
-  }
-  __device__ __forceinline__ float4 get(int m, int k, int mlim, int klim) const {
-    const int o = offset(m, k);
-    return bload4(x, o, m < mlim && k < klim && o >= 0);
-  }
-};
-
-// im2col as the B operand of a weight gradient: rows k = pixels, cols n = (kh,kw,ci);
-// column n == G::K is the bias "ones" column (K % 4 == 0: its group is (1, 0, 0, 0)).
-template <class G>
-struct Im2colT {
-  static constexpr bool kFast = false;
-  const float* x;
-  __device__ __forceinline__ float4 get(int n, int k, int, int klim) const {
-    const float4 v = Im2col<G>{x}.get(k, n, klim, G::K);
-    return (n == G::K && k < klim) ? make_float4(1.0f, 0.0f, 0.0f, 0.0f) : v;
-  }
-};
-
-// stride-1 conv input gradient (transposed conv): rows m = input pixels, k = (kh, kw, co)
-template <class G>
-struct Col2im {
-  static_assert(G::S == 1, "strided input gradients go through the sub-pixel classes (SubPix)");
-  static constexpr bool kFast = true;
-  const float* dy;
-  __device__ __forceinline__ float4 get(int m, int k, int mlim, int klim) const {
-    const int b = m / (G::H * G::W), p = m - b * (G::H * G::W);
-    const int ih = p / G::W, iw = p - ih * G::W;
-    const int kk = k / G::CO, co = k - kk * G::CO;
-    const int kh = kk / G::KW, kw = kk - kh * G::KW;
-    const int oh = ih + G::PT - kh, ow = iw + G::PL - kw;
-    const bool ok = m < mlim && k < klim && oh >= 0 && ow >= 0 && oh < G::OH && ow < G::OW;
-    return bload4(dy, ((b * G::OH + oh) * G::OW + ow) * G::CO + co, ok);
-  }
-};
-
-// conv weights as B of the transposed conv: B(n = ci, k = (kh, kw, co)) = W[co][kh][kw][ci]
-template <class G>
-struct WeightT {
-  static constexpr bool kFast = false;
-  const float* w;
-  __device__ __forceinline__ float4 get(int n, int k, int nlim, int klim) const {
-    const int kk = k / G::CO, co = k - kk * G::CO;
-    return bload4(w, (co * (G::KH * G::KW) + kk) * G::CI + n, n < nlim && k < klim);
-  }
-};
-
-// Stride-S conv input gradient by sub-pixel class: the input pixels with
-// (ih % S, iw % S) == (PY, PX) receive exactly the taps kh = (PY + PT) mod S + S*th,
-// kw = (PX + PL) mod S + S*tw, so the transposed conv is S*S dense GEMMs (rows = that
-// class's pixels, k = (th, tw, co)) with no stride holes and no dcol round trip.
-template <class G, int PY, int PX>
-struct SubPix {
-  static_assert(G::KH % G::S == 0 && G::KW % G::S == 0, "taps split evenly over the classes");
-  static constexpr int NY = (G::H - PY + G::S - 1) / G::S, NX = (G::W - PX + G::S - 1) / G::S;
-  static constexpr int TW = G::KW / G::S, K = (G::KH / G::S) * TW * G::CO;
-  static constexpr int KH0 = (PY + G::PT) % G::S, KW0 = (PX + G::PL) % G::S;
-  __device__ static __forceinline__ int pixel(int m) {      // NHWC pixel index of class row m
-    const int b = m / (NY * NX), q = m - b * (NY * NX);
-    const int i = q / NX, j = q - i * NX;
-    return (b * G::H + PY + G::S * i) * G::W + PX + G::S * j;
-  }
-  __device__ static __forceinline__ void tap(int k, int& kh, int& kw, int& co) {
-    const int t = k / G::CO;
-    co = k - t * G::CO;
-    const int th = t / TW;
-    kh = KH0 + G::S * th;
-    kw = KW0 + G::S * (t - th * TW);
-  }
-};
-// A: dy of the taps landing on class row m, k = (th, tw, co) with co contiguous
-template <class G, int PY, int PX>
-struct SubPixDy {
-  using SP = SubPix<G, PY, PX>;
-  static constexpr bool kFast = true;
-  const float* dy;
-  __device__ __forceinline__ float4 get(int m, int k, int mlim, int klim) const {
-    const int b = m / (SP::NY * SP::NX), q = m - b * (SP::NY * SP::NX);
-    const int i = q / SP::NX, j = q - i * SP::NX;
-    int kh, kw, co;
-    SP::tap(k, kh, kw, co);
-    const int th = PY + G::S * i + G::PT - kh, tw = PX + G::S * j + G::PL - kw;   // even
-    const int oh = th / G::S, ow = tw / G::S;
-    const bool ok = m < mlim && k < klim && th >= 0 && tw >= 0 && oh < G::OH && ow < G::OW;
-    return bload4(dy, ((b * G::OH + oh) * G::OW + ow) * G::CO + co, ok);
-  }
-};
-// B: W[co][kh][kw][ci] as B(n = ci, k = (th, tw, co)), ci contiguous
-template <class G, int PY, int PX>
-struct SubPixW {
-  using SP = SubPix<G, PY, PX>;
-  static constexpr bool kFast = false;
-  const float* w;
-  __device__ __forceinline__ float4 get(int n, int k, int nlim, int klim) const {
-    int kh, kw, co;
-    SP::tap(k, kh, kw, co);
-    return bload4(w, ((co * G::KH + kh) * G::KW + kw) * G::CI + n, n < nlim && k < klim);
-  }
-};
-
-// plain row-major [rows][ld], k contiguous (x of an FC layer, weights [N][K]); ld % 4 == 0
-struct RowK {
-  static constexpr bool kFast = true;
-  const float* p;
-  int ld;
-  __device__ __forceinline__ float4 get(int r, int k, int rlim, int klim) const {
-    return bload4(p, r * ld + k, r < rlim && k < klim);
-  }
-};
-// [k][rows] with rows contiguous: dy^T of FC dW (A), W of FC dX as B(n = in, k = out); ld % 4 == 0
-struct ColK {
-  static constexpr bool kFast = false;
-  const float* p;
-  int ld;
-  __device__ __forceinline__ float4 get(int r, int k, int rlim, int klim) const {
-    return bload4(p, k * ld + r, r < rlim && k < klim);
-  }
-};
-// FC dW's B operand: B(n, k = batch) = x[k][n], with the bias ones-column at n == ld
-struct ColKOnes {
-  static constexpr bool kFast = false;
-  const float* p;
-  int ld;
-  __device__ __forceinline__ float4 get(int n, int k, int, int klim) const {
-    const float4 v = bload4(p, k * ld + n, n < ld && k < klim);
-    return (n == ld && k < klim) ? make_float4(1.0f, 0.0f, 0.0f, 0.0f) : v;
-  }
-};
-// conv dW's A operand: A(m = co, k = pixel) = dy[pixel][co]
-template <int CO>
-struct DyT {
-  static constexpr bool kFast = false;
-  const float* dy;
-  __device__ __forceinline__ float4 get(int m, int k, int mlim, int klim) const {
-    return bload4(dy, k * CO + m, m < mlim && k < klim);
-  }
-};
-// scalar forms of RowK / ColK for a leading dimension that is not a multiple of 4
-// (the n_out-wide output gradient): 4 clamped loads + selects per group
-struct RowKScalar {
-  static constexpr bool kFast = true;
-  const float* p;
-  int ld;
-  __device__ __forceinline__ float4 get(int r, int k, int rlim, int klim) const {
-    float v[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      v[j] = bload1(p, r * ld + k + j, r < rlim && k + j < klim);
-    }
-    return make_float4(v[0], v[1], v[2], v[3]);
-  }
-};
-struct ColKScalar {
-  static constexpr bool kFast = false;
-  const float* p;
-  int ld;
-  __device__ __forceinline__ float4 get(int r, int k, int rlim, int klim) const {
-    float v[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      v[j] = bload1(p, k * ld + r + j, r + j < rlim && k < klim);
-    }
-    return make_float4(v[0], v[1], v[2], v[3]);
-  }
-};
-
-// ---------------------------------------------------------------- epilogues
-// Epilogues with kPrefetch read one input per output element (bias, ReLU mask)
-// that does not depend on the product: the tile kernel issues pf() before its K
-// loop and hands the value to apply(), so that load's latency hides under the
-// operand fetches instead of following the reduction (same arithmetic).
-struct EpiBiasAct {          // out[m][n] = act(acc + bias[n])
-  float* out;
-  const float* bias;
-  int ld;
-  bool relu;
-  static constexpr bool kPrefetch = true;
-  __device__ __forceinline__ float pf(int, int n) const { return bias[n]; }
-  __device__ __forceinline__ void apply(int m, int n, float v, float b) const {
-    v = __fadd_rn(v, b);
-    out[(int64_t)m * ld + n] = relu ? fmaxf(v, 0.0f) : v;
-  }
-  __device__ __forceinline__ void operator()(int m, int n, float v, int) const {
-    apply(m, n, v, pf(m, n));
-  }
-};
-struct EpiMask {             // out[m][n] = acc * (act[m][n] > 0)   (ReLU backward)
-  float* out;
-  const float* act;
-  int ld;
-  static constexpr bool kPrefetch = true;
-  __device__ __forceinline__ float pf(int m, int n) const { return act[(int64_t)m * ld + n]; }
-  __device__ __forceinline__ void apply(int m, int n, float v, float a) const {
-    out[(int64_t)m * ld + n] = a > 0.0f ? v : 0.0f;
-  }
-  __device__ __forceinline__ void operator()(int m, int n, float v, int) const {
-    apply(m, n, v, pf(m, n));
-  }
-};
-template <class SP, int C>
-struct EpiMaskPix {          // EpiMask on a sub-pixel class: row m -> its NHWC pixel
-  float* out;
-  const float* act;
-  static constexpr bool kPrefetch = true;
-  __device__ __forceinline__ float pf(int m, int n) const {
-    return act[(int64_t)SP::pixel(m) * C + n];
-  }
-  __device__ __forceinline__ void apply(int m, int n, float v, float a) const {
-    out[(int64_t)SP::pixel(m) * C + n] = a > 0.0f ? v : 0.0f;
-  }
-  __device__ __forceinline__ void operator()(int m, int n, float v, int) const {
-    apply(m, n, v, pf(m, n));
-  }
-};
-struct EpiStore {            // out[m][n] = acc
-  float* out;
-  int ld;
-  __device__ __forceinline__ void operator()(int m, int n, float v, int) const {
-    out[(int64_t)m * ld + n] = v;
-  }
-};
-struct EpiPartial {          // split-K slab z
-  float* ws;
-  int M, N;
-  __device__ __forceinline__ void operator()(int m, int n, float v, int z) const {
-    ws[((int64_t)z * M + m) * N + n] = v;
-  }
-};
-struct EpiGrad {             // n < nw: dW[m][n]; n == nw: db[m]
-  float* gw;
-  float* gb;
-  int nw;
-  __device__ __forceinline__ void operator()(int m, int n, float v, int) const {
-    if (n < nw) gw[(int64_t)m * nw + n] = v;
-    else gb[m] = v;
-  }
-};
-
-// gradient + TF1 Adam in one pass: the element's gradient is final here, so the
-// optimizer update (same arithmetic as dq_adam_tf1) is applied where it is made.
-struct AdamDev {
-  float* state;
-  int slot;
-  float lr, b1, b2, eps;
-};
-struct EpiGradAdam {
-  float* gw;
-  float* gb;
-  int nw;
-  float *w, *mw, *vw;      // parameter / moment slices at the same offsets as gw
-  float *b, *mb, *vb;      // ... and as gb
-  AdamDev o;
-  int bump;                // this epilogue advances the beta powers (one per step)
-  // two-phase form: pre() issues the element's loads, commit() updates and stores,
-  // so a thread's loads for ALL its elements are in flight before the first store
-  // (the stores may alias later loads as far as the compiler knows)
-  static constexpr bool kPre = true;
-  struct Pre {
-    float w, m, v;
-  };
-  __device__ __forceinline__ Pre pre(int m, int n) const {
-    if (n < nw) {
-      const int64_t i = (int64_t)m * nw + n;
-      return Pre{w[i], mw[i], vw[i]};
-    }
-    return Pre{b[m], mb[m], vb[m]};
-  }
-  __device__ __forceinline__ void commit(int m, int n, float g, Pre q) const {
-    const float alpha = adam_alpha_of(o.state, o.slot, o.lr);
-    const float omb1 = __fsub_rn(1.0f, o.b1), omb2 = __fsub_rn(1.0f, o.b2);
-    adam1(q.w, g, q.m, q.v, alpha, omb1, omb2, o.eps);
-    if (n < nw) {
-      const int64_t i = (int64_t)m * nw + n;
-      gw[i] = g;
-      w[i] = q.w;
-      mw[i] = q.m;
-      vw[i] = q.v;
-    } else {
-      gb[m] = g;
-      b[m] = q.w;
-      mb[m] = q.m;
-      vb[m] = q.v;
-    }
-    if (bump && m == 0 && n == 0) adam_bump(o.state, o.slot, o.b1, o.b2);
-  }
-  __device__ __forceinline__ void operator()(int m, int n, float g, int) const {
-    commit(m, n, g, pre(m, n));
-  }
-};
-
-template <class EP, class = void>
-struct HasPf {
-  static constexpr bool value = false;
-};
-template <class EP>
-struct HasPf<EP, decltype((void)EP::kPrefetch)> {
-  static constexpr bool value = EP::kPrefetch;
-};
-
-template <class EP, class = void>
-struct HasPre {
-  static constexpr bool value = false;
-};
-template <class EP>
-struct HasPre<EP, decltype((void)EP::kPre)> {
-  static constexpr bool value = EP::kPre;
-};
-
-// host-side: EpiGrad, or EpiGradAdam with the moment slices of the same parameter
-struct AdamHost {
-  const dq_adam_args* a;
-};
-template <bool kAdam>
-struct GradEpi;
-template <>
-struct GradEpi<false> {
-  static EpiGrad make(float* gw, float* gb, int nw, float*, float*, const AdamHost&, int) {
-    return EpiGrad{gw, gb, nw};
-  }
-};
-template <>
-struct GradEpi<true> {
-  static EpiGradAdam make(float* gw, float* gb, int nw, float* w, float* b, const AdamHost& h,
-                          int bump) {
-    const dq_adam_args* a = h.a;
-    const ptrdiff_t ow = w - a->var, ob = b - a->var;
-    return EpiGradAdam{gw, gb, nw, w, a->m + ow, a->v + ow, b, a->m + ob, a->v + ob,
-                       AdamDev{a->state, a->slot, a->lr, a->beta1, a->beta2, a->epsilon}, bump};
-  }
-};
-
-// ------------------------------------------------------------- tile kernel
-// 16-byte group g of an R x BKT operand slice -> (row rr, k offset kk).
-// kFast: 8 consecutive lanes cover 128 contiguous bytes of one row, then rows,
-// then the next 32-wide k band.  Otherwise lanes walk the rows 4 at a time.
-template <bool kFast, int R, int BKT>
-__device__ __forceinline__ void group_coord(int g, int& rr, int& kk) {
-  if (kFast) {
-    kk = 4 * ((g & 7) + 8 * (g / (8 * R)));
-    rr = (g >> 3) % R;
-  } else {
-    kk = g / (R / 4);
-    rr = 4 * (g % (R / 4));
-  }
-}
-
-// Block = WM x WN x WK waves.  The WM x WN output tiles are 32x32 (one MFMA
-// accumulator each); each K slice of BKT = 32*WK is split WK ways, one 32-wide
-// k band per wave, so a block with many waves covers a small GEMM's whole K in
-// one or two slices and keeps several waves per SIMD (address math of one wave
-// overlaps the MFMAs of another).  The next slice's operands are fetched into
-// registers while the MFMAs of the current one run.  The WK partial
-// accumulators are then summed through LDS by all threads, each output element
-// in wave order (deterministic), and handed to the epilogue with consecutive
-// threads on consecutive columns.
-// compile with -DDQ_SHARED_STAGING=1 for the block-shared operand staging (A/B builds)
-#ifndef DQ_SHARED_STAGING
-#define DQ_SHARED_STAGING 0
-#endif
-
-template <int WM, int WN, int WK>
-struct Tile {
-  static constexpr int T = 64 * WM * WN * WK;
-  static constexpr int BM = 32 * WM, BN = 32 * WN, BKT = 32 * WK;
-  // one wave per k band (WM = WN = 1): each wave stages only its own band, 16 k at a time
-  static constexpr bool kPrivate = WM == 1 && WN == 1 && WK > 1 && !DQ_SHARED_STAGING;
-  template <class AL, class BL>
-  static constexpr int lds() {      // operand slices, or the WK > 1 reduction scratch
-    const int sa = BM + (AL::kFast ? 1 : 4), sb = BN + (BL::kFast ? 1 : 4);
-    const int pa = AL::kFast ? 32 * 16 : 16 * 36, pb = BL::kFast ? 32 * 16 : 16 * 36;
-    const int tile = kPrivate ? WK * (pa + pb) : BKT * sa + BKT * sb;
-    const int red = WK > 1 ? WK * WM * WN * 1024 : 0;
-    return tile > red ? tile : red;
-  }
-};
-
-// kLate: issue each half-band fetch after the previous half's MFMAs (<= 64 VGPRs,
-// for launches with several rounds of blocks, two 16-wave blocks per CU); else
-// while they run (one more fetch in flight, for single-round launches).
-template <int WM, int WN, int WK, class AL, class BL, class EP, bool kLate = true>
-__device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& E, int M, int N,
-                                            int K, int kchunk, int bx, int by, int bz,
-                                            float* smem) {
-#ifdef DQ_ABLATE_ALL      // timing experiments only: the launch floor of these grids
-  if (M > 0) return;
-#endif
-  using TL = Tile<WM, WN, WK>;
-  constexpr int T = TL::T, BM = TL::BM, BN = TL::BN, BKT = TL::BKT;
-  constexpr int SA = BM + (AL::kFast ? 1 : 4), SB = BN + (BL::kFast ? 1 : 4);
-  constexpr int NA = BM * BKT / 4 / T, NB = BN * BKT / 4 / T;
-  static_assert(NA >= 1 && NB >= 1 && NA * 4 * T == BM * BKT && NB * 4 * T == BN * BKT, "tile/threads");
-  constexpr int OUT = WM * WN * 1024;     // output elements per block
-  float* As = smem;
-  float* Bs = smem + BKT * SA;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave % WM, wn = (wave / WM) % WN, wk = wave / (WM * WN);
-  const int m0 = bx * BM, n0 = by * BN;
-  const int kbeg = bz * kchunk;
-  const int kend = min(K, kbeg + kchunk);
-  float4 ra[NA], rb[NB];
-
-  auto load = [&](int k0) {
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      int rr, kk;
-      group_coord<AL::kFast, BM, BKT>(i * T + tid, rr, kk);
-      ra[i] = A.get(m0 + rr, k0 + kk, M, kend);
-    }
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      int rr, kk;
-      group_coord<BL::kFast, BN, BKT>(i * T + tid, rr, kk);
-      rb[i] = B.get(n0 + rr, k0 + kk, N, kend);
-    }
-  };
-  auto put = [](float* S, int stride, bool kfast, int rr, int kk, float4 v) {
-    if (kfast) {
-      S[(kk + 0) * stride + rr] = v.x;
-      S[(kk + 1) * stride + rr] = v.y;
-      S[(kk + 2) * stride + rr] = v.z;
-      S[(kk + 3) * stride + rr] = v.w;
-    } else {
-      *reinterpret_cast<float4*>(S + kk * stride + rr) = v;
-    }
-  };
-  auto stash = [&]() {
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      int rr, kk;
-      group_coord<AL::kFast, BM, BKT>(i * T + tid, rr, kk);
-      put(As, SA, AL::kFast, rr, kk, ra[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      int rr, kk;
-      group_coord<BL::kFast, BN, BKT>(i * T + tid, rr, kk);
-      put(Bs, SB, BL::kFast, rr, kk, rb[i]);
-    }
-  };
-
-  // the epilogue's product-independent input (bias / ReLU mask) of this thread's
-  // reduction elements, loaded now (clamped, never branching); see kPrefetch
-  constexpr int NE = (OUT + T - 1) / T;
-#ifdef DQ_NO_PF
-  constexpr bool kPf = false;
-#else
-  constexpr bool kPf = WK > 1 && HasPf<EP>::value && NE <= 2;
-#endif
-  float pfv[NE];
-  if constexpr (kPf) {
-#pragma unroll
-    for (int i = 0; i < NE; ++i) {
-      const int e = min(tid + i * T, OUT - 1);
-      const int tile = e >> 10, r = (e >> 6) & 15, l = e & 63;
-      const int m = m0 + (tile % WM) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
-      const int n = n0 + (tile / WM) * 32 + (l & 31);
-      pfv[i] = E.pf(min(m, M - 1), min(n, N - 1));
-    }
-  }
-  f32x16 acc;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-  if constexpr (TL::kPrivate) {
-    // Wave-private staging: wave wk fetches its own 32-wide k band (the same
-    // coalesced 128-byte row segments as the shared layout) and transposes it
-    // through its own LDS window, 16 k at a time -- no block barrier until the
-    // reduction, and about half the LDS of a block-shared slice.
-    // MFMA step s of a half takes k = s from lanes 0-31 and k = 8 + s from lanes
-    // 32-63, so a lane's 8 operands of the half are contiguous in k: a k-contiguous
-    // operand is kept [row][16 k] (float4 slots XOR-swizzled by row, conflict-free
-    // 128-bit writes and reads), a row-contiguous one [k][row] (stride 36: its
-    // 128-bit writes and the two half-waves' scalar reads hit disjoint banks).
-    constexpr int WA = AL::kFast ? 32 * 16 : 16 * 36, WB = BL::kFast ? 32 * 16 : 16 * 36;
-    float* Aw = smem + wave * (WA + WB);
-    float* Bw = Aw + WA;
-    auto st = [](float* W, bool kfast, int rr, int kl, float4 v) {   // kl in [0, 16)
-      float* q = kfast ? W + rr * 16 + 4 * ((kl >> 2) ^ ((rr >> 2) & 3)) : W + kl * 36 + rr;
-      *reinterpret_cast<float4*>(q) = v;
-    };
-    const int r = lane & 31, hh = lane >> 5;
-    auto operands = [&](const float* W, bool kfast, float* o) {   // o[s] = element (r, 8 hh + s)
-      if (kfast) {
-        const float4 x0 = *reinterpret_cast<const float4*>(W + r * 16 + 4 * ((2 * hh) ^ ((r >> 2) & 3)));
-        const float4 x1 =
-            *reinterpret_cast<const float4*>(W + r * 16 + 4 * ((2 * hh + 1) ^ ((r >> 2) & 3)));
-        o[0] = x0.x; o[1] = x0.y; o[2] = x0.z; o[3] = x0.w;
-        o[4] = x1.x; o[5] = x1.y; o[6] = x1.z; o[7] = x1.w;
-      } else {
-#pragma unroll
-        for (int s = 0; s < 8; ++s) o[s] = W[(8 * hh + s) * 36 + r];
-      }
-    };
-    // Half-band fetch: 16 k per fetch (2 float4 per operand per lane), the second
-    // half's loads issued behind the first half's MFMAs: 16 fewer live registers
-    // (66-69 VGPRs instead of 88-91) than fetching the whole band at once, which
-    // lets small blocks share the CU with a 16-wave one (+7% per step, measured).
-    float4 qa[2], qb[2];
-    auto hcoord = [&](bool kfast, int h, int j, int& rr, int& kk) {
-      if (kfast) {
-        rr = 16 * j + (lane >> 2);
-        kk = 32 * wk + 16 * h + 4 * (lane & 3);
-      } else {
-        rr = 4 * (lane & 7);
-        kk = 32 * wk + 16 * h + 8 * j + (lane >> 3);
-      }
-    };
-    auto fetch_h = [&](int k0, int h) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        int rr, kk;
-        hcoord(AL::kFast, h, j, rr, kk);
-        qa[j] = A.get(m0 + rr, k0 + kk, M, kend);
-        hcoord(BL::kFast, h, j, rr, kk);
-        qb[j] = B.get(n0 + rr, k0 + kk, N, kend);
-      }
-    };
-    auto stage_h = [&](int h) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        int rr, kk;
-        hcoord(AL::kFast, h, j, rr, kk);
-        st(Aw, AL::kFast, rr, kk - 32 * wk - 16 * h, qa[j]);
-        hcoord(BL::kFast, h, j, rr, kk);
-        st(Bw, BL::kFast, rr, kk - 32 * wk - 16 * h, qb[j]);
-      }
-    };
-    fetch_h(kbeg, 0);
-    for (int k0 = kbeg; k0 < kend; k0 += BKT) {
-      const bool live = k0 + wk * 32 < kend;   // wave-uniform: bands past the end are all zero
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        stage_h(h);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        if constexpr (!kLate) {
-          if (h == 0) fetch_h(k0, 1);
-          else if (k0 + BKT < kend) fetch_h(k0 + BKT, 0);
-        }
-        if (live) {
-          float av[8], bv[8];
-          operands(Aw, AL::kFast, av);
-          operands(Bw, BL::kFast, bv);
-#ifdef DQ_ABLATE_MFMA    // timing experiments only: no matrix-core chain
-          for (int s = 0; s < 8; ++s) acc[s] += av[s] * bv[s];
-#else
-#pragma unroll
-          for (int s = 0; s < 8; ++s)
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc, 0, 0, 0);
-#endif
-        }
-        if constexpr (kLate) {
-          if (h == 0) fetch_h(k0, 1);
-          else if (k0 + BKT < kend) fetch_h(k0 + BKT, 0);
-        }
-      }
-    }
-    __syncthreads();                 // staging windows are reused as reduction scratch
-  } else {
-  load(kbeg);
-  const float* pa = As + (wk * 32 + (lane >> 5)) * SA + wm * 32 + (lane & 31);
-  const float* pb = Bs + (wk * 32 + (lane >> 5)) * SB + wn * 32 + (lane & 31);
-  for (int k0 = kbeg; k0 < kend; k0 += BKT) {
-    stash();
-    __syncthreads();
-    if (k0 + BKT < kend) load(k0 + BKT);
-    if (k0 + wk * 32 < kend) {              // wave-uniform: bands past the end are all zero
-#pragma unroll
-      for (int s = 0; s < 32; s += 2)
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(pa[s * SA], pb[s * SB], acc, 0, 0, 0);
-    }
-    __syncthreads();
-  }
-  }
-  // C/D layout of the 32x32 f32 MFMA: col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5)
-  if (WK == 1) {
-    const int n = n0 + wn * 32 + (lane & 31);
-    if constexpr (HasPre<EP>::value) {      // all loads first, then updates + stores
-      typename EP::Pre q[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        q[r] = E.pre(min(m, M - 1), min(n, N - 1));     // clamped: loads never branch
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (m < M && n < N) E.commit(m, n, acc[r], q[r]);
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (m < M && n < N) E(m, n, acc[r], bz);
-      }
-    }
-    return;
-  }
-#ifdef DQ_ABLATE_REDUCE   // timing experiments only: wave 0's partial goes straight out
-  if (wk == 0) {
-    const int n = n0 + wn * 32 + (lane & 31);
-    for (int r = 0; r < 16; ++r) {
-      const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      if (m < M && n < N) E(m, n, acc[r], bz);
-    }
-  }
-  return;
-#endif
-  // partials -> LDS [wk][tile][r][lane]
-  {
-    float* red = smem + (wk * WM * WN + wm + WM * wn) * 1024 + lane;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) red[r * 64] = acc[r];
-  }
-  __syncthreads();
-  if constexpr (kPf) {
-#pragma unroll
-    for (int i = 0; i < NE; ++i) {
-      const int e = tid + i * T;
-      if (e >= OUT) break;
-      float v = smem[e];
-#pragma unroll
-      for (int j = 1; j < WK; ++j) v = __fadd_rn(v, smem[j * OUT + e]);
-      const int tile = e >> 10, r = (e >> 6) & 15, l = e & 63;
-      const int m = m0 + (tile % WM) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
-      const int n = n0 + (tile / WM) * 32 + (l & 31);
-      if (m < M && n < N) E.apply(m, n, v, pfv[i]);
-    }
-    return;
-  }
-  for (int e = tid; e < OUT; e += T) {
-    float v = smem[e];
-#pragma unroll
-    for (int j = 1; j < WK; ++j) v = __fadd_rn(v, smem[j * OUT + e]);
-    const int tile = e >> 10, r = (e >> 6) & 15, l = e & 63;
-    const int m = m0 + (tile % WM) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
-    const int n = n0 + (tile / WM) * 32 + (l & 31);
-    if (m < M && n < N) E(m, n, v, bz);
-  }
-}
-
-template <int WM, int WN, int WK, class AL, class BL, class EP>
-__global__ __launch_bounds__(64 * WM * WN * WK) void k_igemm(AL A, BL B, EP E, int M, int N, int K,
-                                                             int kchunk) {
-  __shared__ __attribute__((aligned(16))) float smem[Tile<WM, WN, WK>::template lds<AL, BL>()];
-  igemm_block<WM, WN, WK>(A, B, E, M, N, K, kchunk, blockIdx.x, blockIdx.y, blockIdx.z, smem);
-}
-
-// ordered split-K sum + epilogue: element i of the (M x N) result, slab loads in flight together
-template <class EP>
-__device__ __forceinline__ void splitk_sum(const float* ws, int splits, int M, int N, const EP& E,
-                                           int64_t i) {
-  if (i >= (int64_t)M * N) return;
-  const int64_t MN = (int64_t)M * N;
-  float s = ws[i];
-  for (int z0 = 1; z0 < splits; z0 += 8) {
-    float v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = ws[(int64_t)min(z0 + u, splits - 1) * MN + i];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) s = z0 + u < splits ? __fadd_rn(s, v[u]) : s;
-  }
-  E((int)(i / N), (int)(i % N), s, 0);
-}
-
-template <class EP>
-__global__ __launch_bounds__(256) void k_splitk_reduce(const float* ws, int splits, int M, int N, EP E) {
-  splitk_sum(ws, splits, M, N, E, (int64_t)blockIdx.x * blockDim.x + threadIdx.x);
-}
 
 // ------------------------------------------------------------ grouped launches
 // Independent operations of the backward (layer L's weight gradient beside layer
@@ -1033,46 +293,6 @@ void k_grouped(GroupArgs<Ops...> g, Ops... ops) {
 }
 
 // Launch context: a dry run only sizes the workspace, so the two can never disagree.
-struct Ctx {
-  hipStream_t s;
-  float* ws;       // split-K slabs
-  bool dry;
-  size_t need;
-  size_t take(size_t n) {        // carve a private workspace region (grouped ops run together)
-    const size_t o = need;
-    need += (n + 3) / 4 * 4;
-    return o;
-  }
-};
-
-// K slice per split (multiple of the block's K slice)
-inline int split_chunk(int K, int splits, int bkt) {
-  return ((K + splits - 1) / splits + bkt - 1) / bkt * bkt;
-}
-
-template <int WM, int WN, int WK, class AL, class BL, class EP>
-void gemm(Ctx& c, AL a, BL b, EP e, int M, int N, int K, int splits = 1) {
-  constexpr int BKT = 32 * WK, T = 64 * WM * WN * WK;
-  const unsigned gx = (M + 32 * WM - 1) / (32 * WM), gy = (N + 32 * WN - 1) / (32 * WN);
-  const int kchunk = splits > 1 ? split_chunk(K, splits, BKT) : K;
-  const int nz = splits > 1 ? (K + kchunk - 1) / kchunk : 1;
-  if (nz > 1) {
-    const size_t need = (size_t)nz * M * N;
-    c.need = need > c.need ? need : c.need;
-  }
-  if (c.dry) return;
-  if (nz == 1) {
-    hipLaunchKernelGGL((k_igemm<WM, WN, WK, AL, BL, EP>), dim3(gx, gy, 1), dim3(T), 0, c.s, a, b, e,
-                       M, N, K, K);
-    return;
-  }
-  hipLaunchKernelGGL((k_igemm<WM, WN, WK, AL, BL, EpiPartial>), dim3(gx, gy, nz), dim3(T), 0, c.s, a,
-                     b, EpiPartial{c.ws, M, N}, M, N, K, kchunk);
-  const int64_t total = (int64_t)M * N;
-  hipLaunchKernelGGL((k_splitk_reduce<EP>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                     c.s, c.ws, nz, M, N, e);
-}
-
 // a grouped GEMM op; split-K ops write slabs into ws + off (EpiPartial)
 template <int WM, int WN, int WK, bool kLate = true, class AL, class BL, class EP>
 GemmOp<WM, WN, WK, AL, BL, EP, kLate> gemm_op(AL a, BL b, EP e, int M, int N, int K, int kchunk) {
@@ -1724,6 +944,33 @@ int dq_cnn_backward_riders(const dq_cnn_params* p, const dq_cnn_params* g, int32
                               n_riders, hp);
   }
   DQ_CHECK_LAUNCH("dq_cnn_backward_riders");
+  return DQ_OK;
+}
+
+int dq_cnn_forward_torso(const dq_cnn_params* p, int32_t batch, const float* x, dq_cnn_acts* a,
+                         float* ws, void* stream) {
+  DQ_CHECK_ARG(p && a && x && ws && batch >= 1, "null argument");
+  DQ_CHECK_ARG(p->in_channels == 4, "the Nature CNN takes 84x84x4 NHWC input");
+  Ctx c{(hipStream_t)stream, ws, false, 0};
+  const FwdOps f{p, x, a, ws, batch};
+  group(c, f.conv1<false>());
+  group(c, f.conv2<false>());
+  group(c, f.conv3<false>());
+  DQ_CHECK_LAUNCH("dq_cnn_forward_torso");
+  return DQ_OK;
+}
+
+int dq_cnn_backward_torso(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch,
+                          const float* x, const dq_cnn_acts* a, dq_cnn_acts* d, float* ws,
+                          void* stream) {
+  DQ_CHECK_ARG(p && g && a && d && x && ws && batch >= 1, "null argument");
+  DQ_CHECK_ARG(p->in_channels == 4, "the Nature CNN takes 84x84x4 NHWC input");
+  Ctx c{(hipStream_t)stream, ws, false, 0};
+  for (int layer = 2; layer <= 4; ++layer) {        // conv3, conv2, conv1 (same tiles as
+    backward_layer(c, p, g, batch, x, a, nullptr, d, layer, 1);   // the full backward)
+    if (layer < 4) backward_layer(c, p, g, batch, x, a, nullptr, d, layer, 0);
+  }
+  DQ_CHECK_LAUNCH("dq_cnn_backward_torso");
   return DQ_OK;
 }
 

@@ -1,11 +1,22 @@
-"""Experiment runner (reference dopamine/discrete_domains/run_experiment.py:40-560)
-over the dopamine_amd agents, configured by the reference's .gin files through
-``dopamine_amd.gin_lite``.
+"""Experiment runner over the dopamine_amd agents, with the interface and behaviour of
+the reference's dopamine/discrete_domains/run_experiment.py:40-560, configured by the
+reference's .gin files through ``dopamine_amd.gin_lite``.
 
-Differences from the reference: no TF session or TensorBoard summary writer
-(``sess``/``summary_writer`` are accepted and ignored); Atari environments are
-out of scope (ALE/cv2 are not available), so ``create_environment_fn`` must be
-a gym domain (``gym_lib.create_gym_environment``: CartPole-v0).
+What a run does (the reference's semantics):
+  * iterations [start, num_iterations): each one a training phase of at least
+    ``training_steps`` environment steps and (Runner only) an evaluation phase of at
+    least ``evaluation_steps``, whole episodes, the agent's eval_mode set accordingly;
+  * an episode ends at game over or after ``max_steps_per_episode`` steps; a terminal
+    that is not game over (an Atari life loss) ends the agent's episode and begins a
+    new one inside the same game; the agent sees rewards clipped to [-1, 1], the
+    statistics the raw returns;
+  * after each iteration its statistics go to the Logger ('iteration_<k>'), written
+    every ``log_every_n`` iterations, and the agent + runner state is checkpointed;
+    a run finds the newest checkpoint in ``<base_dir>/checkpoints`` and resumes after it.
+
+Not here: the TF session / TensorBoard summary writer (``sess``/``summary_writer`` are
+accepted and ignored) and Atari environments (ALE/cv2 are not available), so
+``create_environment_fn`` must be a gym domain (``gym_lib.create_gym_environment``).
 """
 import logging
 import os
@@ -46,10 +57,11 @@ gin_lite.register('atari_lib.create_atari_environment', _no_atari)
 
 
 def load_gin_configs(gin_files, gin_bindings):
-  """run_experiment.py:40-51."""
+  """Parse the gin files, then the extra bindings (run_experiment.py:40-51)."""
   gin_lite.parse_config_files_and_bindings(gin_files, bindings=gin_bindings, skip_unknown=False)
 
 
+# agent_name -> (agent class, the replay wrapper class whose bindings it honours)
 _AGENTS = {'dqn': (dqn_agent.DQNAgent, 'WrappedReplayBuffer'),
            'rainbow': (rainbow_agent.RainbowAgent, 'WrappedPrioritizedReplayBuffer'),
            'implicit_quantile': (implicit_quantile_agent.ImplicitQuantileAgent,
@@ -57,96 +69,92 @@ _AGENTS = {'dqn': (dqn_agent.DQNAgent, 'WrappedReplayBuffer'),
 
 
 def _agent_kwargs(agent_name):
-  """Bindings of the agent's class and of the classes it derives from (gin
-  fills a base class's unset constructor arguments the same way), plus the
-  replay wrapper's replay_capacity / batch_size, which dopamine_amd's agents take
-  directly."""
+  """Bindings of the agent's class and of the classes it derives from (gin fills a
+  base class's unset constructor arguments the same way), plus the replay wrapper's
+  replay_capacity / batch_size, which dopamine_amd's agents take directly."""
   cls, wrapper = _AGENTS[agent_name]
   kwargs = {}
   for klass in reversed(cls.__mro__[:-1]):       # base classes first, the agent last
     kwargs.update(gin_lite.query(klass.__name__))
   for w in ('WrappedReplayBuffer', wrapper):
-    q = gin_lite.query(w)
-    for k in ('replay_capacity', 'batch_size'):
-      if k in q:
-        kwargs[k] = q[k]
+    bound = gin_lite.query(w)
+    kwargs.update({k: bound[k] for k in ('replay_capacity', 'batch_size') if k in bound})
   return cls, kwargs
 
 
 @gin_lite.configurable('create_agent')
 def create_agent(sess, environment, agent_name=None, summary_writer=None, debug_mode=False):
-  """run_experiment.py:54-95."""
+  """The agent named by ``agent_name`` for ``environment`` (run_experiment.py:54-95)."""
   assert agent_name is not None
-  if not debug_mode:
-    summary_writer = None
   if agent_name not in _AGENTS:
     raise ValueError('Unknown agent: {}'.format(agent_name))
   cls, kwargs = _agent_kwargs(agent_name)
-  return cls(sess, num_actions=environment.action_space.n, summary_writer=summary_writer,
-             **kwargs)
+  return cls(sess, num_actions=environment.action_space.n,
+             summary_writer=summary_writer if debug_mode else None, **kwargs)
 
 
 @gin_lite.configurable('create_runner')
 def create_runner(base_dir, schedule='continuous_train_and_eval'):
-  """run_experiment.py:99-121."""
+  """Runner for 'continuous_train_and_eval', TrainRunner for 'continuous_train'
+  (run_experiment.py:99-121)."""
   assert base_dir is not None
-  if schedule == 'continuous_train_and_eval':
-    return Runner(base_dir, create_agent)
-  elif schedule == 'continuous_train':
-    return TrainRunner(base_dir, create_agent)
-  raise ValueError('Unknown schedule: {}'.format(schedule))
+  runners = {'continuous_train_and_eval': Runner, 'continuous_train': TrainRunner}
+  if schedule not in runners:
+    raise ValueError('Unknown schedule: {}'.format(schedule))
+  return runners[schedule](base_dir, create_agent)
+
+
+# Runner settings and their defaults (run_experiment.py:143-153)
+_DEFAULTS = (('create_environment_fn', _no_atari), ('checkpoint_file_prefix', 'ckpt'),
+             ('logging_file_prefix', 'log'), ('log_every_n', 1), ('num_iterations', 200),
+             ('training_steps', 250000), ('evaluation_steps', 125000),
+             ('max_steps_per_episode', 27000))
 
 
 class Runner(object):
-  """run_experiment.py:124-491."""
+  """Runs an agent in an environment for num_iterations train (+ eval) iterations."""
 
   def __init__(self, base_dir, create_agent_fn, **kwargs):
-    # defaults of run_experiment.py:143-153 < Runner bindings < the subclass's own
-    # bindings (TrainRunner.*) < explicit arguments
-    opts = dict(create_environment_fn=_no_atari, checkpoint_file_prefix='ckpt',
-                logging_file_prefix='log', log_every_n=1, num_iterations=200,
-                training_steps=250000, evaluation_steps=125000, max_steps_per_episode=27000)
-    opts.update(gin_lite.query('Runner'))
-    if type(self) is not Runner:
-      opts.update(gin_lite.query(type(self).__name__))
-    opts.update(kwargs)
     assert base_dir is not None
-    self._logging_file_prefix = opts['logging_file_prefix']
-    self._log_every_n = opts['log_every_n']
-    self._num_iterations = opts['num_iterations']
-    self._training_steps = opts['training_steps']
-    self._evaluation_steps = opts['evaluation_steps']
-    self._max_steps_per_episode = opts['max_steps_per_episode']
+    # precedence: defaults < Runner bindings < the subclass's own (TrainRunner.*) < kwargs
+    settings = dict(_DEFAULTS)
+    for klass in dict.fromkeys((Runner, type(self))):
+      settings.update(gin_lite.query(klass.__name__))
+    settings.update(kwargs)
+    for name, _ in _DEFAULTS:
+      if name not in ('create_environment_fn', 'checkpoint_file_prefix'):
+        setattr(self, '_' + name, settings[name])
     self._base_dir = base_dir
     self._create_directories()
-    self._environment = opts['create_environment_fn']()
+    self._environment = settings['create_environment_fn']()
     self._sess = None
     self._agent = create_agent_fn(self._sess, self._environment, summary_writer=None)
-    self._initialize_checkpointer_and_maybe_resume(opts['checkpoint_file_prefix'])
+    self._initialize_checkpointer_and_maybe_resume(settings['checkpoint_file_prefix'])
 
+  # ------------------------------------------------------------------ setup
   def _create_directories(self):
     self._checkpoint_dir = os.path.join(self._base_dir, 'checkpoints')
     self._logger = logger.Logger(os.path.join(self._base_dir, 'logs'))
 
   def _initialize_checkpointer_and_maybe_resume(self, checkpoint_file_prefix):
-    """run_experiment.py:210-249."""
+    """Resume after the newest checkpoint that the agent accepts (run_experiment.py:210-249)."""
     self._checkpointer = checkpointer.Checkpointer(self._checkpoint_dir, checkpoint_file_prefix)
     self._start_iteration = 0
-    latest = checkpointer.get_latest_checkpoint_number(self._checkpoint_dir)
-    if latest >= 0:
-      experiment_data = self._checkpointer.load_checkpoint(latest)
-      if self._agent.unbundle(self._checkpoint_dir, latest, experiment_data):
-        if experiment_data is not None:
-          assert 'logs' in experiment_data
-          assert 'current_iteration' in experiment_data
-          self._logger.data = experiment_data['logs']
-          self._start_iteration = experiment_data['current_iteration'] + 1
-        logging.info('Reloaded checkpoint and will start from iteration %d',
-                     self._start_iteration)
+    newest = checkpointer.get_latest_checkpoint_number(self._checkpoint_dir)
+    if newest < 0:
+      return
+    runner_state = self._checkpointer.load_checkpoint(newest)
+    if not self._agent.unbundle(self._checkpoint_dir, newest, runner_state):
+      return
+    if runner_state is not None:
+      assert 'logs' in runner_state and 'current_iteration' in runner_state
+      self._logger.data = runner_state['logs']
+      self._start_iteration = runner_state['current_iteration'] + 1
+    logging.info('Reloaded checkpoint and will start from iteration %d', self._start_iteration)
 
+  # --------------------------------------------------------------- episodes
   def _initialize_episode(self):
-    initial_observation = self._environment.reset()
-    return self._agent.begin_episode(initial_observation)
+    return self._agent.begin_episode(self._environment.reset())
 
   def _run_one_step(self, action):
     observation, reward, is_terminal, _ = self._environment.step(action)
@@ -156,61 +164,60 @@ class Runner(object):
     self._agent.end_episode(reward)
 
   def _run_one_episode(self):
-    """run_experiment.py:281-317 (rewards clipped to [-1, 1] for the agent)."""
-    step_number = 0
-    total_reward = 0.
+    """(steps, undiscounted return) of one game."""
+    steps, episode_return = 0, 0.
     action = self._initialize_episode()
-    while True:
+    agent_reward = 0.
+    game_over = False
+    while not game_over:
       observation, reward, is_terminal = self._run_one_step(action)
-      total_reward += reward
-      step_number += 1
-      reward = np.clip(reward, -1, 1)
-      if self._environment.game_over or step_number == self._max_steps_per_episode:
-        break
-      elif is_terminal:
-        self._agent.end_episode(reward)
+      steps += 1
+      episode_return += reward
+      agent_reward = np.clip(reward, -1, 1)
+      game_over = self._environment.game_over or steps == self._max_steps_per_episode
+      if game_over:
+        continue
+      if is_terminal:                  # a life lost: new agent episode, same game
+        self._agent.end_episode(agent_reward)
         action = self._agent.begin_episode(observation)
       else:
-        action = self._agent.step(reward, observation)
-    self._end_episode(reward)
-    return step_number, total_reward
+        action = self._agent.step(agent_reward, observation)
+    self._end_episode(agent_reward)
+    return steps, episode_return
 
   def _run_one_phase(self, min_steps, statistics, run_mode_str):
-    step_count = 0
-    num_episodes = 0
-    sum_returns = 0.
-    while step_count < min_steps:
-      episode_length, episode_return = self._run_one_episode()
-      statistics.append({'{}_episode_lengths'.format(run_mode_str): episode_length,
-                         '{}_episode_returns'.format(run_mode_str): episode_return})
-      step_count += episode_length
-      sum_returns += episode_return
-      num_episodes += 1
+    """Whole episodes until at least min_steps steps: (steps, sum of returns, episodes)."""
+    lengths, returns = [], []
+    while sum(lengths) < min_steps:
+      length, ret = self._run_one_episode()
+      lengths.append(length)
+      returns.append(ret)
+      statistics.append({run_mode_str + '_episode_lengths': length,
+                         run_mode_str + '_episode_returns': ret})
       sys.stdout.write('Steps executed: {} Episode length: {} Return: {}\r'.format(
-          step_count, episode_length, episode_return))
+          sum(lengths), length, ret))
       sys.stdout.flush()
-    return step_count, sum_returns, num_episodes
+    return sum(lengths), float(sum(returns)), len(returns)
+
+  def _phase(self, statistics, run_mode_str, min_steps, eval_mode):
+    self._agent.eval_mode = eval_mode
+    t0 = time.time()
+    steps, total, episodes = self._run_one_phase(min_steps, statistics, run_mode_str)
+    average = total / episodes if episodes else 0.0
+    statistics.append({run_mode_str + '_average_return': average})
+    logging.info('Average undiscounted return per %s episode: %.2f',
+                 'training' if run_mode_str == 'train' else 'evaluation', average)
+    if not eval_mode:
+      logging.info('Average training steps per second: %.2f', steps / (time.time() - t0))
+    return episodes, average
 
   def _run_train_phase(self, statistics):
-    self._agent.eval_mode = False
-    start_time = time.time()
-    number_steps, sum_returns, num_episodes = self._run_one_phase(
-        self._training_steps, statistics, 'train')
-    average_return = sum_returns / num_episodes if num_episodes > 0 else 0.0
-    statistics.append({'train_average_return': average_return})
-    time_delta = time.time() - start_time
-    logging.info('Average undiscounted return per training episode: %.2f', average_return)
-    logging.info('Average training steps per second: %.2f', number_steps / time_delta)
-    return num_episodes, average_return
+    return self._phase(statistics, 'train', self._training_steps, eval_mode=False)
 
   def _run_eval_phase(self, statistics):
-    self._agent.eval_mode = True
-    _, sum_returns, num_episodes = self._run_one_phase(self._evaluation_steps, statistics, 'eval')
-    average_return = sum_returns / num_episodes if num_episodes > 0 else 0.0
-    logging.info('Average undiscounted return per evaluation episode: %.2f', average_return)
-    statistics.append({'eval_average_return': average_return})
-    return num_episodes, average_return
+    return self._phase(statistics, 'eval', self._evaluation_steps, eval_mode=True)
 
+  # ------------------------------------------------------------- iterations
   def _run_one_iteration(self, iteration):
     statistics = iteration_statistics.IterationStatistics()
     logging.info('Starting iteration %d', iteration)
@@ -224,15 +231,15 @@ class Runner(object):
       self._logger.log_to_file(self._logging_file_prefix, iteration)
 
   def _checkpoint_experiment(self, iteration):
-    experiment_data = self._agent.bundle_and_checkpoint(self._checkpoint_dir, iteration)
-    if experiment_data:
-      experiment_data['current_iteration'] = iteration
-      experiment_data['logs'] = self._logger.data
-      self._checkpointer.save_checkpoint(iteration, experiment_data)
+    state = self._agent.bundle_and_checkpoint(self._checkpoint_dir, iteration)
+    if not state:
+      return
+    state.update(current_iteration=iteration, logs=self._logger.data)
+    self._checkpointer.save_checkpoint(iteration, state)
 
   def run_experiment(self):
     logging.info('Beginning training...')
-    if self._num_iterations <= self._start_iteration:
+    if self._start_iteration >= self._num_iterations:
       logging.warning('num_iterations (%d) < start_iteration(%d)', self._num_iterations,
                       self._start_iteration)
       return
@@ -243,7 +250,7 @@ class Runner(object):
 
 
 class TrainRunner(Runner):
-  """run_experiment.py:493-560: training phases only."""
+  """Training phases only, no evaluation (run_experiment.py:493-560)."""
 
   def _run_one_iteration(self, iteration):
     statistics = iteration_statistics.IterationStatistics()

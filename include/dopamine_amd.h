@@ -374,6 +374,51 @@ int dq_cnn_backward_layer(const dq_cnn_params* p, const dq_cnn_params* g, int32_
                           const float* x, const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d,
                           float* ws, int32_t layer, int32_t part, void* stream);
 size_t dq_cnn_workspace_floats(int32_t batch, int32_t n_out);
+/* The Nature-CNN torso alone (conv1..conv3 + ReLU -> a->a3, the (B, 7744) state vector of
+   atari_lib.py:98-101), the trunk of ImplicitQuantileNetwork; and its backward from
+   d->a3 = d loss / d (conv3 pre-activation) (already masked by a3 > 0) into the conv
+   weight / bias gradients of g.  Same tiles as the full forward / backward. */
+int dq_cnn_forward_torso(const dq_cnn_params* p, int32_t batch, const float* x, dq_cnn_acts* a,
+                         float* ws, void* stream);
+int dq_cnn_backward_torso(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch,
+                          const float* x, const dq_cnn_acts* a, dq_cnn_acts* d, float* ws,
+                          void* stream);
+
+/* ImplicitQuantileNetwork's quantile head (atari_lib.py:147-199) on the fp32 matrix cores.
+   R = nq * batch rows ordered q * batch + b (tf.tile, atari_lib.py:174). */
+typedef struct dq_iqn_head {
+  int32_t embed_dim;              /* quantile_embedding_dim (multiple of 4; 64) */
+  int32_t num_actions;
+  float* emb_w; float* emb_b;     /* (7744, E), (7744) */
+  float* fc1_w; float* fc1_b;     /* (512, 7744), (512) */
+  float* fc2_w; float* fc2_b;     /* (A, 512), (A) */
+} dq_iqn_head;
+typedef struct dq_iqn_acts {
+  float* cos;                     /* (R, E)    cos(pi * i * tau), i = 1..E   (atari_lib.py:176-178) */
+  float* emb;                     /* (R, 7744) relu(cos We^T + be), kept for the backward; may be NULL */
+  float* x;                       /* (R, 7744) tiled state * emb             (atari_lib.py:185) */
+  float* h;                       /* (R, 512)  relu(x W1^T + b1) */
+  float* q;                       /* (R, A)    quantile values              (atari_lib.py:189-191) */
+} dq_iqn_acts;
+typedef struct dq_iqn_grads {
+  float* dh;                      /* (R, 512) */
+  float* dpre;                    /* (R, 7744) d loss / d (cos We^T + be) */
+  float* dtl;                     /* (R, 7744) d loss / d tiled state */
+} dq_iqn_grads;
+/* forward: state = the torso's (B, 7744) output, taus (R). ws: dq_iqn_workspace_floats. */
+int dq_iqn_head_forward(const dq_iqn_head* hp, int32_t batch, int32_t nq, const float* state,
+                        const float* taus, dq_iqn_acts* a, float* ws, void* stream);
+/* backward from dq = d loss / d q (R, A) (dq_iqn_loss): head weight / bias gradients into hg,
+   dstate (B, 7744) = the torso's d->a3 for dq_cnn_backward_torso (tile sum, ReLU mask). */
+int dq_iqn_head_backward(const dq_iqn_head* hp, const dq_iqn_head* hg, int32_t batch, int32_t nq,
+                         const float* state, const dq_iqn_acts* a, const float* dq,
+                         dq_iqn_grads* d, float* dstate, float* ws, void* stream);
+size_t dq_iqn_workspace_floats(int32_t batch, int32_t nq, int32_t num_actions, int32_t embed_dim);
+/* tf.random_uniform([n], 0, 1) for the quantile samples (atari_lib.py:171-172; TF's stream
+   itself is not reproducible without TF): n float32 draws of call counter[0] of the
+   generator `seed` (a splitmix64 hash of seed, call, index; 24 random bits), then
+   counter[0] += 1 on the device -- graph replays continue the eager sequence. */
+int dq_uniform_draw(int64_t* counter, uint64_t seed, int64_t n, float* out, void* stream);
 
 /* _build_sync_op (dqn_agent.py:324-339): online -> target copy of the flat buffer. */
 int dq_sync_copy(void* dst, const void* src, int64_t bytes, void* stream);

@@ -49,12 +49,29 @@ class Params64(object):
     return g.numpy()
 
 
-def torso(P, x_nhwc):
+def _relu(z, masks, name, nhwc=False):
+  """ReLU, or -- given the device's activations in ``masks`` -- z * (device output > 0):
+  the float64 arithmetic on the device's own ReLU decisions.  A pre-activation within
+  fp32 rounding of 0 can take the other branch in float64 and move a gradient that sums
+  thousands of terms with cancellation by a whole term (mask-pinned checks isolate the
+  arithmetic from those flips)."""
+  if masks is None or name not in masks:
+    return F.relu(z)
+  m = torch.as_tensor(np.asarray(masks[name]) > 0, dtype=torch.float64)
+  if nhwc:                                   # device NHWC -> torch NCHW
+    m = m.reshape(z.shape[0], z.shape[2], z.shape[3], z.shape[1]).permute(0, 3, 1, 2)
+  return z * m.reshape(z.shape)
+
+
+def torso(P, x_nhwc, masks=None):
   """x (B, 84, 84, stack) float64, already /255 -> (B, 7744) in TF's flatten order."""
   x = x_nhwc.permute(0, 3, 1, 2)
-  x = F.relu(F.conv2d(F.pad(x, (2, 2, 2, 2)), P['conv1_w'], P['conv1_b'], stride=4))   # SAME 84->21
-  x = F.relu(F.conv2d(F.pad(x, (1, 2, 1, 2)), P['conv2_w'], P['conv2_b'], stride=2))   # SAME 21->11
-  x = F.relu(F.conv2d(F.pad(x, (1, 1, 1, 1)), P['conv3_w'], P['conv3_b'], stride=1))   # SAME 11->11
+  x = _relu(F.conv2d(F.pad(x, (2, 2, 2, 2)), P['conv1_w'], P['conv1_b'], stride=4), masks, 'a1',
+            True)                                                                      # SAME 84->21
+  x = _relu(F.conv2d(F.pad(x, (1, 2, 1, 2)), P['conv2_w'], P['conv2_b'], stride=2), masks, 'a2',
+            True)                                                                      # SAME 21->11
+  x = _relu(F.conv2d(F.pad(x, (1, 1, 1, 1)), P['conv3_w'], P['conv3_b'], stride=1), masks, 'a3',
+            True)                                                                      # SAME 11->11
   return x.permute(0, 2, 3, 1).reshape(x.shape[0], -1)
 
 
@@ -64,19 +81,31 @@ def forward(P, x_nhwc):
   return F.linear(h, P['fc2_w'], P['fc2_b'])
 
 
-def iqn_forward(P, x_nhwc, taus):
+def iqn_forward(P, x_nhwc, taus, masks=None):
   """ImplicitQuantileNetwork (atari_lib.py:147-199): taus (N*B,) rows ordered
-  q*B + b; returns quantile values (N*B, A)."""
-  state = torso(P, x_nhwc)
+  q*B + b; returns quantile values (N*B, A).  masks: the device's activations
+  (a1, a2, a3, emb, h) to pin the ReLU decisions (see _relu)."""
+  state = torso(P, x_nhwc, masks)
   B = state.shape[0]
   nq = taus.shape[0] // B
   E = P['emb_w'].shape[1]
   tiled = state.repeat(nq, 1)
-  i_pi = torch.arange(1, E + 1, dtype=torch.float64) * math.pi
-  emb = torch.cos(taus.reshape(-1, 1) * i_pi)
-  emb = F.relu(F.linear(emb, P['emb_w'], P['emb_b']))
-  h = F.relu(F.linear(tiled * emb, P['fc1_w'], P['fc1_b']))
+  # the reference forms the cosine's argument in float32 -- (float(i) * float32(pi)) * tau,
+  # atari_lib.py:176-178 -- an argument up to 64 pi carries ~1e-5 of rounding that is part
+  # of the reference's result; the cosine itself is taken in float64
+  i_pi = (torch.arange(1, E + 1, dtype=torch.float32) * torch.tensor(math.pi, dtype=torch.float32))
+  arg = (taus.to(torch.float32).reshape(-1, 1) * i_pi).double()
+  emb = torch.cos(arg)
+  emb = _relu(F.linear(emb, P['emb_w'], P['emb_b']), masks, 'emb')
+  h = _relu(F.linear(tiled * emb, P['fc1_w'], P['fc1_b']), masks, 'h')
   return F.linear(h, P['fc2_w'], P['fc2_b'])
+
+
+def iqn_masks(ex):
+  """The ReLU outputs of a HipIqnNet's last forward (host copies) for iqn_forward."""
+  t = ex.torso.acts
+  return dict(a1=t['a1'].cpu().numpy(), a2=t['a2'].cpu().numpy(), a3=t['a3'].cpu().numpy(),
+              emb=ex.acts['emb'].cpu().numpy(), h=ex.acts['h'].cpu().numpy())
 
 
 def to_input(x_float32_nhwc):

@@ -1,0 +1,81 @@
+"""The IQN network on the HIP kernels (dopamine_amd/iqn.py: torso on nature_cnn.hip,
+quantile head on iqn.hip) against a float64 restatement of ImplicitQuantileNetwork
+(oracle/nature_cnn.py, atari_lib.py:147-199) on the same flat parameters and taus:
+quantile values within 1e-5 of their scale, and every parameter gradient of a given
+d loss / d q within 1e-5 of its tensor's scale."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import nature_cnn as ONC
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+
+
+def _rel(got, ref):
+  got, ref = np.asarray(got, np.float64), np.asarray(ref, np.float64)
+  return float(np.abs(got - ref).max() / max(np.abs(ref).max(), 1e-30))
+
+
+@pytest.mark.parametrize('B,nq,A', [(3, 5, 4), (64, 64, 4), (16, 8, 18)])
+def test_iqn_executor_matches_float64(B, nq, A):
+  from dopamine_amd.agents.networks import ImplicitQuantileNetwork
+  from dopamine_amd.iqn import HipIqnNet
+  torch.manual_seed(0)
+  net = ImplicitQuantileNetwork(A, device='cuda', seed=3)
+  with torch.no_grad():     # non-zero biases so every term is exercised
+    for n in ('conv1_b', 'conv2_b', 'conv3_b', 'emb_b', 'fc1_b', 'fc2_b'):
+      net.fp[n].uniform_(-0.05, 0.05)
+  rs = np.random.RandomState(B)
+  x = torch.from_numpy(rs.randint(0, 256, (B, 84, 84, 4)).astype(np.float32) / np.float32(255))
+  taus = torch.from_numpy(rs.rand(nq * B).astype(np.float32))
+  ex = HipIqnNet(net, B, nq, keep=True)
+  q, _ = ex.forward(x.cuda(), taus.cuda())
+  q = q.cpu().numpy().copy()
+  P = ONC.Params64(net.fp.flat.cpu().numpy(), net.fp.offsets)
+  ref = ONC.iqn_forward(P, x.double(), taus.double())
+  assert _rel(q, ref.detach().numpy()) <= TOL
+  # the no-backward form (target nets) gives the same values, bit for bit
+  ex2 = HipIqnNet(net, B, nq, keep=False)
+  q2, _ = ex2.forward(x.cuda(), taus.cuda())
+  np.testing.assert_array_equal(q2.cpu().numpy(), q)
+  # backward of a given d loss / d q
+  dq = torch.from_numpy(rs.randn(nq * B, A).astype(np.float32) / (nq * B))
+  net.fp.grad.fill_(np.nan)           # every gradient element must be written
+  ex.backward(dq.cuda())
+  g = net.fp.grad.cpu().numpy()
+  # gradients on the device's own ReLU decisions (see oracle/nature_cnn._relu): at R = 4096
+  # a few of the 2M + 32M pre-activations sit within fp32 rounding of 0 and take the other
+  # branch in float64, moving a cancelling 4096-term weight-gradient sum by a whole term
+  Pm = ONC.Params64(net.fp.flat.cpu().numpy(), net.fp.offsets)
+  ONC.iqn_forward(Pm, x.double(), taus.double(), masks=ONC.iqn_masks(ex)).backward(dq.double())
+  g64 = Pm.flat_grad()
+  errs = {}
+  for name, (o, shape) in net.fp.offsets.items():
+    n = int(np.prod(shape))
+    assert np.isfinite(g[o:o + n]).all(), name
+    errs[name] = _rel(g[o:o + n], g64[o:o + n])
+  print('iqn executor grad errors (mask-pinned)', B, nq, errs, flush=True)
+  assert max(errs.values()) <= TOL, errs
+
+
+def test_tau_sampler_is_uniform_and_replays_in_graphs():
+  from dopamine_amd.iqn import TauSampler
+  a = TauSampler(7, torch.device('cuda', 0))
+  out = torch.empty(4096, device='cuda')
+  eager = [a.draw(out).cpu().numpy().copy() for _ in range(3)]
+  assert all(((e >= 0) & (e < 1)).all() for e in eager)
+  assert abs(float(np.mean(np.concatenate(eager))) - 0.5) < 0.01
+  assert not np.array_equal(eager[0], eager[1])
+  b = TauSampler(7, torch.device('cuda', 0))
+  g = torch.cuda.CUDAGraph()
+  with torch.cuda.graph(g):
+    b.draw(out)
+  got = []
+  for _ in range(3):
+    g.replay()
+    got.append(out.cpu().numpy().copy())
+  for e, r in zip(eager, got):
+    np.testing.assert_array_equal(e, r)

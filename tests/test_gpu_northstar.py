@@ -258,3 +258,95 @@ def test_dqn_pong_bench_path_matches_float64_oracle():
   bench.fill_synthetic(agent._replay.memory, 6, seed=2)
   _prime(agent)
   _check(_run_lockstep(agent, 'dqn'), 'dqn')
+
+
+def _iqn_agent():
+  """Config 5 as implicit_quantile.gin binds it (N = N' = 64, K = 32, n = 3, Adam 5e-5 /
+  3.125e-4, 'uniform' replay scheme on the prioritized buffer) at batch 64, 1M buffer."""
+  from dopamine_amd.agents.implicit_quantile.implicit_quantile_agent import ImplicitQuantileAgent
+  from dopamine_amd.agents.optimizers import AdamOptimizer
+  return ImplicitQuantileAgent(num_actions=4, num_tau_samples=64, num_tau_prime_samples=64,
+                               num_quantile_samples=32, update_horizon=3, gamma=0.99,
+                               replay_scheme='uniform', min_replay_history=20000, update_period=4,
+                               target_update_period=8000,
+                               optimizer=AdamOptimizer(learning_rate=0.00005, epsilon=0.0003125),
+                               replay_capacity=1_000_000, batch_size=64,
+                               device=torch.device('cuda', 0))
+
+
+@pytest.mark.timeout(900)
+def test_iqn_breakout_step_matches_float64_oracle():
+  """Config 5: every step of the captured-graph learner loop (per-step graph replays;
+  IQN has no chunk graphs) against float64 at the device's parameters of that step
+  (each step is one call, so they are read between steps):
+    * indices bit-exact (the oracle sampler from the same tree and RNG state);
+    * online quantile values Z(s, tau) and target values on (tau', tau_K), the quantile
+      loss and d loss / d Z within 1e-5 of scale (float64 ImplicitQuantileNetwork and
+      quantile-Huber loss on the device's taus);
+    * every parameter gradient within 1e-5 per tensor of float64 on the device's ReLU
+      decisions (mask-pinned: see oracle/nature_cnn._relu; the unpinned error is printed);
+    * the Adam update: float64 Adam from the device's state and gradient reproduces the
+      device's new parameters within PARAM_ATOL."""
+  import bench
+  torch.cuda.set_device(0)
+  agent = _iqn_agent()
+  assert agent._iqn is not None
+  agent.enable_trace()
+  random.seed(0)
+  bench.fill_synthetic(agent._replay.memory, 4, seed=3)
+  _prime(agent)
+  B, U, Np = 64, agent._UNROLL, 64
+  offsets = agent.online_convnet.fp.offsets
+  k0 = agent._opt_steps % 2
+  T64 = ONC.Params64(agent.target_convnet.fp.flat.cpu().numpy(), offsets)
+  orc = _oracle_replay(agent, True)
+  cg = np.float64(np.float32(agent.cumulative_gamma))
+  errs = dict(q=0.0, target_q=0.0, loss=0.0, dq=0.0, grad={}, grad_unpinned={}, params=0.0)
+  eager0 = dict(agent._eager_steps)
+  for s in range(6):
+    w = agent.online_convnet.fp.flat.cpu().double().numpy().copy()
+    opt = _Adam64(agent._opt, (k0 + s) % 2)
+    agent.train_gradient_steps(1)
+    torch.cuda.synchronize()
+    tr = {k: v[U + (k0 + s) % 2].cpu().numpy() for k, v in agent._trace.items()}
+    masks = ONC.iqn_masks(agent._iqn['online'])
+    idx = orc.sample_index_batch(B)
+    np.testing.assert_array_equal(tr['indices'], idx)
+    b = orc.sample_transition_batch(B, indices=idx)
+    st, act, rew, nst, term = b[0], b[1], b[2], b[3], b[6]
+    x = np.moveaxis(st, -1, 1).astype(np.float32) / np.float32(255)
+    nx = np.moveaxis(nst, -1, 1).astype(np.float32) / np.float32(255)
+    np.testing.assert_array_equal(tr['state'], x)
+    np.testing.assert_array_equal(tr['next_state'], nx)
+    xin = ONC.to_input(np.moveaxis(x, 1, -1))
+    taus = torch.from_numpy(tr['taus']).double()
+    P = ONC.Params64(w, offsets)
+    q = ONC.iqn_forward(P, xin, taus)
+    with torch.no_grad():
+      tq_all = ONC.iqn_forward(T64, ONC.to_input(np.moveaxis(nx, 1, -1)),
+                               torch.from_numpy(tr['target_taus']).double()).numpy()
+    errs['q'] = max(errs['q'], _rel(tr['qv'], q.detach().numpy()))
+    errs['target_q'] = max(errs['target_q'], _rel(tr['target_q'], tq_all))
+    ref = OL.iqn_loss(q.detach().numpy(), tq_all[:Np * B], tq_all[Np * B:], tr['taus'], act, rew,
+                      term, cg, 1.0, dtype=np.float64)
+    errs['loss'] = max(errs['loss'], _rel(tr['loss'], ref['loss']))
+    errs['dq'] = max(errs['dq'], _rel(tr['grad_out'], ref['grad']))
+    q.backward(torch.from_numpy(ref['grad']))
+    g_free = P.flat_grad()
+    Pm = ONC.Params64(w, offsets)
+    ONC.iqn_forward(Pm, xin, taus, masks=masks).backward(torch.from_numpy(ref['grad']))
+    g = Pm.flat_grad()
+    for name, (o, shape) in offsets.items():
+      n = int(np.prod(shape))
+      errs['grad'][name] = max(errs['grad'].get(name, 0.0), _rel(tr['grad'][o:o + n], g[o:o + n]))
+      errs['grad_unpinned'][name] = max(errs['grad_unpinned'].get(name, 0.0),
+                                        _rel(tr['grad'][o:o + n], g_free[o:o + n]))
+    opt.step(w, tr['grad'].astype(np.float64))        # the device's gradient, float64 Adam
+    gw = agent.online_convnet.fp.flat.cpu().double().numpy()
+    errs['params'] = max(errs['params'], float(np.abs(gw - w).max()))
+  assert agent._eager_steps == eager0, 'a step ran eagerly: not the graph path'
+  print(json.dumps({'northstar_errors': 'iqn', **errs}), flush=True)
+  assert errs['q'] <= Q_TOL and errs['target_q'] <= Q_TOL and errs['loss'] <= Q_TOL, errs
+  assert errs['dq'] <= Q_TOL, errs
+  assert max(errs['grad'].values()) <= GRAD_TOL, errs
+  assert errs['params'] <= PARAM_ATOL, errs

@@ -35,7 +35,8 @@ def measure(make, actions, steps, warmup=20):
   dt = time.perf_counter() - t0
   agent._replay.memory.sync_rng()
   out = {'steps_per_s': round(steps / dt, 1), 'ms_per_step': round(1e3 * dt / steps, 4),
-         'batch': agent._batch_size, 'hip_cnn': agent._hip is not None}
+         'batch': agent._batch_size,
+         'hip_cnn': agent._hip is not None or getattr(agent, '_iqn', None) is not None}
   del agent
   gc.collect()
   torch.cuda.empty_cache()
@@ -52,11 +53,12 @@ def main():
                                              update_period=4, target_update_period=8000,
                                              replay_capacity=1_000_000, batch_size=32,
                                              device=dev), 6, steps)
-  res['iqn_breakout'] = measure(lambda: ImplicitQuantileAgent(
-      num_actions=4, update_horizon=3, replay_scheme='uniform',   # implicit_quantile.gin:24
-      min_replay_history=20000, update_period=4,
-      target_update_period=8000, replay_capacity=1_000_000, batch_size=64, device=dev), 4,
-      max(steps // 3, 50))
+  from dopamine_amd.agents.optimizers import AdamOptimizer
+  res['iqn_breakout'] = measure(lambda: ImplicitQuantileAgent(   # implicit_quantile.gin
+      num_actions=4, num_tau_samples=64, num_tau_prime_samples=64, num_quantile_samples=32,
+      update_horizon=3, replay_scheme='uniform', min_replay_history=20000, update_period=4,
+      target_update_period=8000, optimizer=AdamOptimizer(learning_rate=0.00005, epsilon=0.0003125),
+      replay_capacity=1_000_000, batch_size=64, device=dev), 4, max(steps // 3, 50))
   print(json.dumps(res))
 
 
