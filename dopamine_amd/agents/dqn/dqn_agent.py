@@ -198,7 +198,10 @@ class DQNAgent(object):
          if k in t}
     d['loss'] = self._loss_out['loss']
     d['grad_out'] = self._loss_out['grad']
-    d['grad'] = self.online_convnet.fp.grad
+    if self._needs_flat_grad():
+      d['grad'] = self.online_convnet.fp.grad
+    else:   # the optimizer reads autograd's per-parameter tensors: copy them into the flat one
+      d['grad'] = self.online_convnet.fp.gather_grads()
     if self._hip is not None:
       d['online_out'] = self._hip['online'].acts['out']
       d['target_out'] = self._hip['target'][c].acts['out']
@@ -214,7 +217,7 @@ class DQNAgent(object):
     for k, v in self._trace_outputs(c).items():
       if k not in self._trace:
         self._trace[k] = torch.zeros((n,) + tuple(v.shape), dtype=v.dtype, device=v.device)
-      self._trace[k][slot].copy_(v)
+      self._trace[k][slot].copy_(v.detach())
 
   # ------------------------------------------------------------ graph parts
   def _build_replay_buffer(self, use_staging):
@@ -279,7 +282,7 @@ class DQNAgent(object):
   def _online_loss(self, t, tgt):
     """dqn_agent.py:283-322."""
     q = self._online_forward(t['state'])
-    self._last_online_out = q
+    self._last_online_out = q.detach()
     out = ops.dqn_huber_loss(q.detach(), tgt['q'], t['action'], t['reward'], t['terminal'],
                              self.cumulative_gamma, out=self._loss_out)
     return q, out['grad']

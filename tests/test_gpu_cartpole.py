@@ -97,7 +97,7 @@ def test_cartpole_dqn_steps_match_float64_oracle():
     for _ in range(agent.update_period):   # one gradient step, the reference's cadence
       agent._train_step()
     torch.cuda.synchronize()
-    tr = {n: t[U + k].cpu().numpy() for n, t in agent._trace.items()}
+    tr = {n: t[U + k].detach().cpu().numpy() for n, t in agent._trace.items()}
     idx = orc.sample_index_batch(B)
     np.testing.assert_array_equal(tr['indices'], idx)
     s, act, rew, ns, _, _, term, _ = orc.sample_transition_batch(B, indices=idx)
