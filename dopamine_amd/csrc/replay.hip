@@ -143,9 +143,18 @@ __global__ __launch_bounds__(256) void k_gather_f32(ReplayView v, GatherOut g) {
   }
 }
 
+// Standalone NHWC gather: block columns 0 .. gx-1 copy the frames, the last column's
+// first wave writes the sample's scalars (state slots only), so no frame wave waits on
+// the scalar chain.
 template <int R>
 __global__ __launch_bounds__(256) void k_gather_nhwc4(ReplayView v, GatherOut g) {
-  gather_nhwc4_body<R, true>(v, g, blockIdx.x, blockIdx.y, threadIdx.x);
+  const int slot = blockIdx.y;
+  if (blockIdx.x == gridDim.x - 1) {
+    if ((slot & 1) == 0 && threadIdx.x < kWave)
+      write_scalars_wave(v, g, slot >> 1, pymod((int64_t)g.indices[slot >> 1], v.C));
+    return;
+  }
+  gather_nhwc4_body<R, kScalNone, true>(v, g, blockIdx.x, slot, threadIdx.x);
 }
 
 __device__ __forceinline__ int64_t frame_of(const ReplayView& v, const GatherOut& g, int slot,
@@ -369,7 +378,7 @@ int dq_replay_gather(dq_replay* h, const int32_t* indices, int32_t batch, int32_
     DQ_CHECK_ARG(h->cfg.stack_size == 4, "F32_NHWC layout needs stack_size == 4");
     DQ_CHECK_ARG((h->cfg.obs_bytes & 3) == 0, "F32_NHWC layout needs obs_bytes % 4 == 0");
     const int64_t nd = h->cfg.obs_bytes >> 2;
-    dim3 grid((unsigned)((nd + 256 * kNhwcR - 1) / (256 * kNhwcR)), (unsigned)(2 * batch));
+    dim3 grid((unsigned)((nd + 256 * kNhwcR - 1) / (256 * kNhwcR) + 1), (unsigned)(2 * batch));
     hipLaunchKernelGGL(k_gather_nhwc4<kNhwcR>, grid, dim3(256), 0, s, h->view(), g);
   } else if (layout == DQ_LAYOUT_RAW) {
     const int64_t units = (h->cfg.obs_bytes & 15) == 0 ? h->cfg.obs_bytes >> 4 : h->cfg.obs_bytes;

@@ -381,6 +381,8 @@ __device__ __forceinline__ float u8_unit(uint32_t x) {
   return __builtin_fmaf(__builtin_fmaf(-q, 255.0f, xf), kInv, q);
 }
 
+typedef uint32_t gather_u32x4 __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ float4 u8x4_to_f32_255(uint32_t w) {
   float4 o;
   o.x = u8_unit(w & 0xffu);
@@ -395,16 +397,23 @@ __device__ __forceinline__ float4 u8x4_to_f32_255(uint32_t w) {
 // pixels) of each of the 4 frames -- all 4R loads in flight together -- and
 // writes 4 pixels x 4 channels = 64 contiguous bytes per lane per store.
 // (bx, slot) = the block's coordinates in the (column blocks, 2B) grid; tid in [0, 256).
-// kLateScalars: the scalars wave issues its frame loads first (standalone kernel: 6.5 ->
-// 5.6 us at B = 32).  Riders keep the early form: the late one's live frame registers
-// raise the grouped launch's VGPR count (-1% per learner step, measured).
-template <int R, bool kLateScalars = false>
+// kScalars: where the per-sample scalars are written --
+//   kScalEarly: by the first wave of the sample's state column, before its frame loads
+//               (the riders: the late form's live frame registers raise the grouped
+//               launch's VGPR count, -1% per learner step, measured);
+//   kScalLate:  by that wave after issuing its frame loads;
+//   kScalNone:  not here (the standalone kernel gives them a block column of their own,
+//               so no frame wave waits on the scalar chain: 5.58 -> 5.20 us at B = 32
+//               with kNt, tools/micro/gather_nhwc.hip).
+// kNt: non-temporal float4 stores (the line stays in L2; 5.58 -> 5.42 us alone).
+enum { kScalEarly = 0, kScalLate = 1, kScalNone = 2 };
+
+template <int R, int kScalars = kScalEarly, bool kNt = false>
 __device__ __forceinline__ void gather_nhwc4_body(const ReplayView& v, const GatherOut& g, int bx,
                                                   int slot, int tid) {
+  constexpr bool kLateScalars = kScalars == kScalLate;
   const int b = slot >> 1, which = slot & 1;
-  // one wave per sample also writes the scalars: after issuing its frame loads, so its
-  // scalar loads share their memory round (the kernel waits for its slowest wave)
-  const bool scal = bx == 0 && which == 0 && tid < 64;
+  const bool scal = kScalars != kScalNone && bx == 0 && which == 0 && tid < 64;
   if (!kLateScalars && scal) write_scalars_wave(v, g, b, pymod((int64_t)g.indices[b], v.C));
   float* dst_base = (float*)(which ? g.next_state : g.state);
   const int64_t nd = v.obs_bytes >> 2;
@@ -459,7 +468,14 @@ __device__ __forceinline__ void gather_nhwc4_body(const ReplayView& v, const Gat
       o.y = u8_unit((__shfl(w[r][1], src) >> sh) & 0xffu);
       o.z = u8_unit((__shfl(w[r][2], src) >> sh) & 0xffu);
       o.w = u8_unit((__shfl(w[r][3], src) >> sh) & 0xffu);
-      if (4 * d0 + 64 * j + lane < 4 * nd) dst[64 * j + lane] = o;
+      if (4 * d0 + 64 * j + lane < 4 * nd) {
+        if constexpr (kNt)   // buffer store, cache policy nt (aux = 2); dst is wave-uniform
+          __builtin_amdgcn_raw_buffer_store_b128(
+              *(const gather_u32x4*)&o, __builtin_amdgcn_make_buffer_rsrc(dst, 0, 0x7fffffff, 0x00020000),
+              (64 * j + lane) * 16, 0, 2);
+        else
+          dst[64 * j + lane] = o;
+      }
     }
   }
 }
