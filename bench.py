@@ -49,6 +49,10 @@ def parse():
                   help='override the agent default fuse_optimizer (0/1)')
   ap.add_argument('--ride', type=int, default=None,
                   help='override the agent default ride_replay (0/1)')
+  ap.add_argument('--force-dist', action='store_true',
+                  help='one rank only: run the N > 1 learner schedule over a one-rank RCCL group '
+                       'with every collective executed (a hardware check of the data-parallel '
+                       'path on a one-GPU box; not the bench line)')
   return ap.parse_args()
 
 
@@ -224,6 +228,13 @@ def main():
     else:
       dist.init_process_group('nccl', device_id=dev)
     pg = dist.group.WORLD
+  elif args.force_dist:
+    from dopamine_amd import parallel
+    parallel.FORCE_COLLECTIVES = True
+    os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+    os.environ.setdefault('MASTER_PORT', '29533')
+    dist.init_process_group('nccl', rank=0, world_size=1, device_id=dev)
+    pg = dist.group.WORLD
   agent = build_agent(args.actions, args.capacity, args.batch, dev, pg=pg,
                       use_hip_graph=not args.no_graph,
                       **({} if args.fuse_opt is None else {'fuse_optimizer': bool(args.fuse_opt)}),
@@ -287,7 +298,9 @@ def main():
         'config': {'workload': 'Rainbow/C51 Asterix (9 actions), prioritized sum-tree replay, '
                                'n=3, 1M-transition 84x84x4 uint8 buffer per GPU',
                    'global_batch': args.batch * world, 'per_gpu_batch': args.batch,
-                   'replay_capacity': args.capacity, 'parallelism': 'dp%d' % world,
+                   'replay_capacity': args.capacity,
+                   'parallelism': 'dp%d' % world + (' (one-rank RCCL group, --force-dist)'
+                                                    if args.force_dist and world == 1 else ''),
                    'hip_graph': not args.no_graph},
         'roofline': {'kernel': gname + ' (frame-stack gather + /255, state+next_state)',
                      'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,

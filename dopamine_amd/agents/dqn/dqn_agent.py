@@ -641,6 +641,7 @@ class DQNAgent(object):
                          lambda: self._grad_step_head(c, k, pipe, 'b'),
                          lambda: self._grad_step_tail(c, k, pipe),
                          lambda: self._device_opt_step(k), k=k)
+        self._eager_steps[pipe] += 1
       else:
         self._split_step(None, lambda: self._grad_step_head(c, k, pipe),
                          lambda: self._grad_step_tail(c, k, pipe),
@@ -852,20 +853,33 @@ class DQNAgent(object):
 
   def graphs_primed(self):
     """True once every HIP graph the learner loop replays is captured: the per-step
-    graphs and, where chunking applies (single replica), the chunk graphs of both
-    starting parities."""
+    graphs and, where chunking applies, the chunk graphs of both starting parities."""
     if not self.use_hip_graph:
       return True
     if self._graph_sets.get(True) is None:
       return False
-    if self._pg is not None or self._hip is None or not self.pipeline:
+    if not self._chunks_apply():
       return True
     return all(('chunk', self._UNROLL, k) in self._graph_sets for k in (0, 1))
+
+  def _captures_collectives(self):
+    """N > 1 over RCCL with the split fused-head schedule: the gradient all-reduces
+    are captured inside the learner loop's chunk graphs (gloo's host-side
+    collectives cannot be)."""
+    if self._pg is None:
+      return False
+    import torch.distributed as dist
+    return (dist.get_backend(self._pg) == 'nccl' and self._split_allreduce() and
+            self._head_splits() and isinstance(self._opt, ops.TF1Adam))
+
+  def _chunks_apply(self):
+    return (self._hip is not None and self.pipeline and
+            (self._pg is None or self._captures_collectives()))
 
   def _chunk_ok(self):
     K, U = self._UNROLL, self.update_period
     t0 = self.training_steps
-    if not (self.pipeline and self.use_hip_graph and self._pg is None and self._hip is not None
+    if not (self.pipeline and self.use_hip_graph and self._chunks_apply()
             and self.summary_writer is None
             and self._has_prefetch and not self._interleaved()
             and self._graph_sets.get(True) is not None and t0 % U == 0
@@ -885,16 +899,34 @@ class DQNAgent(object):
     key = ('chunk', K, k0)
     g = self._graph_sets.get(key)
     if g is None:
+      self._join_fc()                 # nothing outside the capture may be pending
       torch.cuda.synchronize(self._device)
       g = torch.cuda.CUDAGraph()
-      with torch.cuda.graph(g, pool=self._graph_pool):
-        for j in range(K):
-          k = (k0 + j) % 2
-          self._grad_step(k, k, True)
-          self._device_opt_step(k)
-          self._trace_step(j, k)
+      if self._pg is None:
+        with torch.cuda.graph(g, pool=self._graph_pool):
+          for j in range(K):
+            k = (k0 + j) % 2
+            self._grad_step(k, k, True)
+            self._device_opt_step(k)
+            self._trace_step(j, k)
+      else:
+        # N > 1: each step's split schedule with its RCCL all-reduces captured (the comm
+        # stream and RCCL's own streams fork from and join back into the capture; each
+        # step's fc all-reduce + update is joined in the next step, the last one at the
+        # end of the chunk).  thread_local: the process group's watchdog thread keeps
+        # querying its events while this thread captures.
+        with torch.cuda.graph(g, pool=self._graph_pool, capture_error_mode='thread_local'):
+          for j in range(K):
+            k = (k0 + j) % 2
+            self._split_step(lambda k=k: self._grad_step_head(k, k, True, 'a'),
+                             lambda k=k: self._grad_step_head(k, k, True, 'b'),
+                             lambda k=k: self._grad_step_tail(k, k, True),
+                             lambda k=k: self._device_opt_step(k), k=k)
+          self._join_fc()
       self._graph_pool = g.pool()
       self._graph_sets[key] = g
+    else:
+      self._join_fc()
     for _ in range(K):
       mem.reserve_rng(self._batch_size)
     g.replay()

@@ -9,14 +9,21 @@ Adam update, so replicas stay bit-identical.  PER's `w /= max(w)` stays
 per-rank (rainbow_agent.py:280): the multi-GPU gradient is the mean of the
 ranks' single-GPU gradients, not a single B*N batch.
 """
+import os
+
 import torch
 import torch.distributed as dist
+
+# Run the collectives even in a one-rank group (DQ_FORCE_COLLECTIVES=1): a one-GPU box
+# can then drive the RCCL path itself (bench.py --force-dist, tests/test_gpu_rccl.py);
+# an average over one rank leaves the values unchanged.
+FORCE_COLLECTIVES = os.environ.get('DQ_FORCE_COLLECTIVES') == '1'
 
 
 def allreduce_mean_(flat_grad, group=None):
   """In-place mean of a flat gradient buffer across the ranks of ``group``."""
   world = dist.get_world_size(group)
-  if world == 1:
+  if world == 1 and not FORCE_COLLECTIVES:
     return flat_grad
   if dist.get_backend(group) == 'nccl':     # RCCL averages in the collective (no extra kernel)
     dist.all_reduce(flat_grad, op=dist.ReduceOp.AVG, group=group)

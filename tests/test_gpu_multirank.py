@@ -60,6 +60,7 @@ def _worker(rank, world, port, same_seed, q, loop=False, net_seed_per_rank=False
   agent = _agent(dist.group.WORLD, 0 if same_seed else rank,
                  net_seed=1000 * rank if net_seed_per_rank else 0)
   flat = _run(agent, loop)
+  assert agent.graphs_primed()      # the later steps replayed the captured split graphs
   ok = parallel.replicas_in_sync(agent.online_convnet.fp.flat)
   ok = ok and parallel.replicas_in_sync(agent.target_convnet.fp.flat)
   if rank == 0:

@@ -5,7 +5,7 @@ _train_step cadence), for DESIGN.md -- not the bench line:
   config 2: DQN / Pong   -- 6 actions, uniform replay, n = 1, TF1 centered RMSProp, B = 32
   config 5: IQN / Breakout -- 4 actions, n = 3, Adam, B = 64 (quantile-Huber kernel)
 
-    python tools/bench_configs.py [steps]
+    python tools/bench_configs.py [steps] [dqn_pong|iqn_breakout|all]
 """
 import gc
 import json
@@ -45,16 +45,19 @@ def measure(make, actions, steps, warmup=20):
 
 def main():
   steps = int(sys.argv[1]) if len(sys.argv) > 1 else 300
+  which = sys.argv[2] if len(sys.argv) > 2 else 'all'
   dev = torch.device('cuda', 0)
   from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
   from dopamine_amd.agents.implicit_quantile.implicit_quantile_agent import ImplicitQuantileAgent
   res = {}
-  res['dqn_pong'] = measure(lambda: DQNAgent(num_actions=6, min_replay_history=20000,
-                                             update_period=4, target_update_period=8000,
-                                             replay_capacity=1_000_000, batch_size=32,
-                                             device=dev), 6, steps)
+  if which in ('all', 'dqn_pong'):
+    res['dqn_pong'] = measure(lambda: DQNAgent(num_actions=6, min_replay_history=20000,
+                                               update_period=4, target_update_period=8000,
+                                               replay_capacity=1_000_000, batch_size=32,
+                                               device=dev), 6, steps)
   from dopamine_amd.agents.optimizers import AdamOptimizer
-  res['iqn_breakout'] = measure(lambda: ImplicitQuantileAgent(   # implicit_quantile.gin
+  if which in ('all', 'iqn_breakout'):
+    res['iqn_breakout'] = measure(lambda: ImplicitQuantileAgent(   # implicit_quantile.gin
       num_actions=4, num_tau_samples=64, num_tau_prime_samples=64, num_quantile_samples=32,
       update_horizon=3, replay_scheme='uniform', min_replay_history=20000, update_period=4,
       target_update_period=8000, optimizer=AdamOptimizer(learning_rate=0.00005, epsilon=0.0003125),
