@@ -155,7 +155,8 @@ class DQNAgent(object):
       self._opt = self.optimizer.build(self.online_convnet.fp.flat,
                                        segments=self.online_convnet.fp.segments())
       self._side = torch.cuda.Stream(self._device)
-      self._comm = torch.cuda.Stream(self._device)
+      self._comm = torch.cuda.Stream(self._device)        # N > 1: the fc bucket's all-reduces
+      self._comm_opt = torch.cuda.Stream(self._device)    # ... and the Adam parts behind them
       if self._pg is not None:
         self._broadcast_replica()
     self._observation = None
@@ -527,6 +528,17 @@ class DQNAgent(object):
     o = fp.offsets['fc1_w'][0]
     return fp.grad[o:], fp.grad[:o]           # fc1 + fc2 (final after the head), convs
 
+  # fc-bucket all-reduce pieces (N > 1).  4 pieces pipeline each piece's Adam part
+  # behind its all-reduce, but with a one-rank RCCL group (bench --force-dist) they
+  # cost 174 -> 212 us per step in launches; 1 until an 8-GPU measurement says otherwise.
+  _FC_PIECES = 1
+
+  def _fc_pieces(self, lo, hi):
+    """[lo, hi) in _FC_PIECES ranges, every boundary a multiple of 4 floats."""
+    n = self._FC_PIECES
+    step = -(-(hi - lo) // (4 * n)) * 4
+    return [(a, min(a + step, hi)) for a in range(lo, hi, step)]
+
   def _join_fc(self):
     """The main stream waits for a deferred fc all-reduce + update (_split_step)."""
     if self._fc_pending is not None:
@@ -569,18 +581,31 @@ class DQNAgent(object):
     ev = torch.cuda.Event()
     ev.record(main)
     self._comm.wait_event(ev)
-    with torch.cuda.stream(self._comm):
-      parallel.allreduce_mean_(fc, self._pg)
+    # The fc bucket as _FC_PIECES all-reduces back to back on the comm stream; each
+    # piece's Adam part runs on a second stream behind its own all-reduce, under the
+    # next piece's (an HBM-bound update beside a link-bound collective).  Elementwise
+    # ops: bitwise the one-bucket result.  (Blocking collectives + events rather than
+    # async work handles, which graph capture does not survive.)
+    pieces = self._fc_pieces(o, grad.numel()) if split_opt else [(o, grad.numel())]
+    last = self._comm
+    for lo, hi in pieces:
+      with torch.cuda.stream(self._comm):
+        parallel.allreduce_mean_(grad[lo:hi], self._pg)
       if split_opt:
-        self._opt.step_part(grad, o, grad.numel(), slot=k, bump=False)
+        e = torch.cuda.Event()
+        e.record(self._comm)
+        self._comm_opt.wait_event(e)
+        with torch.cuda.stream(self._comm_opt):
+          self._opt.step_part(grad, lo, hi, slot=k, bump=False)
+        last = self._comm_opt
     tail()
     if defer:
       parallel.allreduce_mean_(conv, self._conv_group())
       self._fc_pending = torch.cuda.Event()
-      self._fc_pending.record(self._comm)
+      self._fc_pending.record(last)
     else:
       parallel.allreduce_mean_(conv, self._pg)
-      main.wait_stream(self._comm)
+      main.wait_stream(last)
     if split_opt:
       self._opt.step_part(grad, 0, o, slot=k, bump=True)
     else:
