@@ -10,7 +10,11 @@ from dopamine_amd._build import HEADER, LIB_PATH  # noqa: F401
 
 ABI_VERSION = 1
 OK = 0
-ST_OK, ST_EMPTY_TREE, ST_MAX_ATTEMPTS, ST_TAPE_EXHAUSTED, ST_NEG_PRIORITY, ST_TOO_FEW, ST_BAD_INDEX = range(7)
+(ST_OK, ST_EMPTY_TREE, ST_MAX_ATTEMPTS, ST_TAPE_EXHAUSTED, ST_NEG_PRIORITY, ST_TOO_FEW, ST_BAD_INDEX,
+ ST_BROADCAST) = range(8)
+# DQ_DT_*: element types of dq_replay_gather_elems' reward store
+DT_CODES = {'float32': 0, 'float64': 1, 'float16': 2, 'int8': 3, 'uint8': 4, 'int16': 5,
+            'int32': 6, 'int64': 7}
 LAYOUT_RAW, LAYOUT_F32_NORM, LAYOUT_F32_NHWC = 0, 1, 2
 SUMTREE_QUERY, SUMTREE_RANDOM, SUMTREE_STRATIFIED = 0, 1, 2
 
@@ -102,6 +106,8 @@ SIGNATURES = {
     'dq_replay_add': [_P, _I64, _P, _P, _P, _P, _P, _P],
     'dq_replay_sample_indices': [_P, _I32, _P, _P],
     'dq_replay_gather': [_P, _P, _I32, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    'dq_replay_gather_elems': [_P, _P, _I32, _P, _I32, _P, _I32, _I32, _I32, _I32, _P, _P, _P, _P,
+                               _P],
     'dq_sumtree_set': [_P, _P, _P, _I64, _P],
     'dq_sumtree_set_f64': [_P, _P, _P, _I64, _P],
     'dq_sumtree_sample': [_P, _I32, _I32, _P, _P, _P],

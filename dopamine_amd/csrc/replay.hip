@@ -6,6 +6,8 @@
 // live in replay_dev.h (shared with the grouped launches of nature_cnn.hip).
 #include "replay_dev.h"
 
+#include <hip/hip_fp16.h>
+
 #include <algorithm>
 #include <cstring>
 #include <new>
@@ -168,6 +170,101 @@ __device__ __forceinline__ int64_t frame_of(const ReplayView& v, const GatherOut
   *which_out = which;
   *k_out = k;
   return pymod(stack_base(v, g, b, which) - S + 1 + k, v.C);
+}
+
+// ---------------------------------------------------------------------------
+// Action / reward elements of buffers whose action or reward is not a scalar int32 /
+// float32 (circular_replay_buffer.py:96-183, sampled at :530-548).  One block per
+// sample: L from the terminal store, the action rows copied as bytes, the n-step reward
+// as numpy's np.sum(discount[:L] * trajectory_rewards, axis=0) -- the (L,) float32
+// discount broadcast against the LAST axis of (L,) + reward_shape, products and the
+// left-to-right sum (numpy's axis-0 order) in the promoted type -- then cast to the
+// reward dtype as the assignment into the batch array does.
+// ---------------------------------------------------------------------------
+struct ElemArgs {
+  const int32_t* indices;
+  const uint8_t* act;        // (C, act_bytes)
+  int act_bytes;
+  const void* rew;           // (C, rew_elems) of dtype rew_dt
+  int rew_elems, rew_last, rew_dt, acc64;
+  uint8_t* act_out;
+  uint8_t* nact_out;
+  void* rew_out;
+  void* nrew_out;
+};
+
+__device__ __forceinline__ int dt_size(int dt) {
+  return dt == DQ_DT_F64 || dt == DQ_DT_I64 ? 8 : dt == DQ_DT_F32 || dt == DQ_DT_I32 ? 4
+         : dt == DQ_DT_F16 || dt == DQ_DT_I16 ? 2 : 1;
+}
+
+// the element as a double: exact for every type here (int64 beyond 2^53 rounds as
+// numpy's int64 -> float64 promotion does)
+__device__ __forceinline__ double dt_load(const void* p, int64_t i, int dt) {
+  switch (dt) {
+    case DQ_DT_F32: return (double)((const float*)p)[i];
+    case DQ_DT_F64: return ((const double*)p)[i];
+    case DQ_DT_F16: return (double)__half2float(((const __half*)p)[i]);
+    case DQ_DT_I8: return (double)((const int8_t*)p)[i];
+    case DQ_DT_U8: return (double)((const uint8_t*)p)[i];
+    case DQ_DT_I16: return (double)((const int16_t*)p)[i];
+    case DQ_DT_I32: return (double)((const int32_t*)p)[i];
+    default: return (double)((const int64_t*)p)[i];
+  }
+}
+
+// store a float32-mode (f) or float64-mode (d) result with numpy's cast to the dtype
+__device__ __forceinline__ void dt_store(void* p, int64_t i, int dt, bool acc64, float f, double d) {
+  switch (dt) {
+    case DQ_DT_F32: ((float*)p)[i] = acc64 ? __double2float_rn(d) : f; return;
+    case DQ_DT_F64: ((double*)p)[i] = acc64 ? d : (double)f; return;
+    case DQ_DT_F16: ((__half*)p)[i] = __float2half_rn(acc64 ? __double2float_rn(d) : f); return;
+    case DQ_DT_I8: ((int8_t*)p)[i] = (int8_t)(acc64 ? (int64_t)d : (int64_t)f); return;
+    case DQ_DT_U8: ((uint8_t*)p)[i] = (uint8_t)(acc64 ? (int64_t)d : (int64_t)f); return;
+    case DQ_DT_I16: ((int16_t*)p)[i] = (int16_t)(acc64 ? (int64_t)d : (int64_t)f); return;
+    case DQ_DT_I32: ((int32_t*)p)[i] = (int32_t)(acc64 ? (int64_t)d : (int64_t)f); return;
+    default: ((int64_t*)p)[i] = acc64 ? (int64_t)d : (int64_t)f; return;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_gather_elems(ReplayView v, ElemArgs e) {
+  const int b = blockIdx.x;
+  const int64_t idx = pymod((int64_t)e.indices[b], v.C);
+  bool term;
+  const int L = traj_len(v, idx, &term);
+  const int64_t nxt = pymod(idx + L, v.C);
+  for (int i = threadIdx.x; i < e.act_bytes; i += blockDim.x) {
+    if (e.act_out) e.act_out[(int64_t)b * e.act_bytes + i] = e.act[idx * e.act_bytes + i];
+    if (e.nact_out) e.nact_out[(int64_t)b * e.act_bytes + i] = e.act[nxt * e.act_bytes + i];
+  }
+  const int es = dt_size(e.rew_dt);
+  if (e.nrew_out)
+    for (int i = threadIdx.x; i < e.rew_elems * es; i += blockDim.x)
+      ((uint8_t*)e.nrew_out)[(int64_t)b * e.rew_elems * es + i] =
+          ((const uint8_t*)e.rew)[nxt * e.rew_elems * es + i];
+  if (!e.rew_out) return;
+  // (L,) against (L,) + reward_shape: scalar reward -> elementwise; else the last axis m
+  // must equal L (discount indexed by the element's last coordinate) or be broadcast
+  // from 1 on either side; m == 1 < L broadcasts but its (.., L) sum cannot be assigned
+  const int m = e.rew_last;
+  if (m > 0 && L != m && L != 1) {
+    if (threadIdx.x == 0) latch(v.meta, DQ_ST_BROADCAST, L, m == 1 ? 1.0 : 0.0);
+    return;
+  }
+  for (int j = threadIdx.x; j < e.rew_elems; j += blockDim.x) {
+    const int di = m > 0 && L == m ? j % m : -1;     // -1: discount index = trajectory step
+    float f = 0.0f;
+    double d = 0.0;
+    for (int k = 0; k < L; ++k) {
+      const float disc = v.discount[di < 0 ? k : di];
+      const double r = dt_load(e.rew, pymod(idx + k, v.C) * e.rew_elems + j, e.rew_dt);
+      if (e.acc64)
+        d = __dadd_rn(d, __dmul_rn((double)disc, r));
+      else
+        f = __fadd_rn(f, __fmul_rn(disc, (float)r));
+    }
+    dt_store(e.rew_out, (int64_t)b * e.rew_elems + j, e.rew_dt, e.acc64 != 0, f, d);
+  }
 }
 
 // raw byte copy of each stacked frame (reference dtype preserved).
@@ -389,6 +486,29 @@ int dq_replay_gather(dq_replay* h, const int32_t* indices, int32_t batch, int32_
     DQ_CHECK_ARG(false, "unknown layout");
   }
   DQ_CHECK_LAUNCH("gather");
+  return DQ_OK;
+}
+
+int dq_replay_gather_elems(dq_replay* h, const int32_t* indices, int32_t batch,
+                           const void* action_rows, int32_t action_bytes, const void* rewards,
+                           int32_t reward_elems, int32_t reward_last, int32_t reward_dtype,
+                           int32_t acc_f64, void* action_out, void* next_action_out,
+                           void* reward_out, void* next_reward_out, void* stream) {
+  DQ_CHECK_ARG(h && indices && batch >= 1, "bad arguments");
+  DQ_CHECK_ARG(!h->tree_only, "a standalone sum tree has no transition store");
+  DQ_CHECK_ARG(action_bytes >= 0 && (action_rows || action_bytes == 0 ||
+                                     (!action_out && !next_action_out)), "bad action rows");
+  DQ_CHECK_ARG(reward_elems >= 1 && reward_last >= 0 && reward_dtype >= DQ_DT_F32 &&
+               reward_dtype <= DQ_DT_I64 && (rewards || (!reward_out && !next_reward_out)),
+               "bad reward store");
+  DQ_CHECK_ARG(reward_last == 0 || reward_elems % reward_last == 0,
+               "reward_last must divide reward_elems");
+  ElemArgs e{indices, (const uint8_t*)action_rows, action_bytes, rewards, reward_elems,
+             reward_last, reward_dtype, acc_f64 ? 1 : 0, (uint8_t*)action_out,
+             (uint8_t*)next_action_out, reward_out, next_reward_out};
+  hipLaunchKernelGGL(k_gather_elems, dim3((unsigned)batch), dim3(256), 0, (hipStream_t)stream,
+                     h->view(), e);
+  DQ_CHECK_LAUNCH("k_gather_elems");
   return DQ_OK;
 }
 

@@ -114,13 +114,18 @@ class OutOfGraphReplayBuffer(object):
     if replay_capacity < update_horizon + stack_size:
       raise ValueError('There is not enough capacity to cover '
                        'update_horizon and stack_size.')
-    if tuple(action_shape) != () or tuple(reward_shape) != ():
-      raise NotImplementedError('dopamine_amd stores scalar actions and rewards only')
+    # a scalar int32 action / float32 reward lives in the device store the learner kernels
+    # read; any other shape or dtype is kept as its own element store
+    # (dq_replay_gather_elems, crb:96-183 / 530-548)
+    self._generic_action = tuple(action_shape) != () or np.dtype(action_dtype) != np.int32
+    self._generic_reward = tuple(reward_shape) != () or np.dtype(reward_dtype) != np.float32
+    if self._generic_reward and np.dtype(reward_dtype).name not in _lib.DT_CODES:
+      raise NotImplementedError('reward_dtype {} is not supported'.format(np.dtype(reward_dtype)))
     if np.dtype(terminal_dtype).itemsize != 1:
       raise NotImplementedError('terminal_dtype must be a 1-byte type')
-    self._action_shape = action_shape
+    self._action_shape = tuple(action_shape)
     self._action_dtype = action_dtype
-    self._reward_shape = reward_shape
+    self._reward_shape = tuple(reward_shape)
     self._reward_dtype = reward_dtype
     self._observation_shape = observation_shape
     self._stack_size = stack_size
@@ -157,6 +162,12 @@ class OutOfGraphReplayBuffer(object):
     self._meta = torch.zeros((16,), dtype=torch.int64, device=dev)
     self._tree = None
     self._extras = {}
+    if self._generic_action:      # (C, action bytes) rows, reinterpreted on the host
+      ab = int(np.prod(self._action_shape, dtype=np.int64)) * np.dtype(self._action_dtype).itemsize
+      self._act_rows = torch.zeros((C, max(ab, 1)), dtype=torch.uint8, device=dev)
+    if self._generic_reward:
+      self._rew_store = torch.zeros((C,) + self._reward_shape, dtype=_torch_dtype(self._reward_dtype),
+                                    device=dev)
     for e in self._extra_storage_types:
       shape = (C,) + tuple(e.shape)
       self._extras[e.name] = torch.zeros(shape, dtype=_torch_dtype(e.type), device=dev)
@@ -210,6 +221,9 @@ class OutOfGraphReplayBuffer(object):
     m = _lib.Meta()
     _lib.call('dq_replay_read_meta', self._h, ctypes.byref(m), self._stream)
     return m
+
+  def _act_bytes(self):
+    return int(np.prod(self._action_shape, dtype=np.int64)) * np.dtype(self._action_dtype).itemsize
 
   # ------------------------------------------------------------ signatures
   def get_add_args_signature(self):
@@ -282,8 +296,18 @@ class OutOfGraphReplayBuffer(object):
     obs = np.empty((n, self._obs_bytes), np.uint8)
     for i, r in enumerate(rows):
       obs[i] = np.ascontiguousarray(np.asarray(r[0], dtype=self._observation_dtype)).view(np.uint8).reshape(-1)
-    act = np.array([r[1] for r in rows]).astype(np.int32)
-    rew = np.array([r[2] for r in rows]).astype(np.float32)
+    if self._generic_action:
+      act = np.zeros(n, np.int32)
+      act_rows = np.stack([np.ascontiguousarray(np.asarray(r[1], dtype=self._action_dtype))
+                           .reshape(-1).view(np.uint8) for r in rows])
+    else:
+      act = np.array([r[1] for r in rows]).astype(np.int32)
+    if self._generic_reward:
+      rew = np.zeros(n, np.float32)
+      rew_rows = np.stack([np.asarray(r[2], dtype=self._reward_dtype).reshape(self._reward_shape)
+                           for r in rows])
+    else:
+      rew = np.array([r[2] for r in rows]).astype(np.float32)
     term = np.array([r[3] for r in rows]).astype(self._terminal_dtype).view(np.uint8)
     prio = self._priority_column(rows)
     dev = self._device
@@ -293,8 +317,12 @@ class OutOfGraphReplayBuffer(object):
     d_term = torch.from_numpy(np.ascontiguousarray(term)).to(dev)
     d_prio = torch.from_numpy(prio).to(dev) if prio is not None else None
     base = int(self.add_count)
-    if self._extra_storage_types:
+    if self._extra_storage_types or self._generic_action or self._generic_reward:
       slots = torch.tensor([(base + i) % self._replay_capacity for i in range(n)], device=dev)
+      if self._generic_action and act_rows.shape[1]:
+        self._act_rows[slots] = torch.from_numpy(act_rows).to(dev)
+      if self._generic_reward:
+        self._rew_store[slots] = torch.from_numpy(rew_rows).to(dev)
       for j, e in enumerate(self._extra_storage_types):
         vals = np.array([np.asarray(r[4 + j], dtype=e.type) for r in rows])
         self._extras[e.name][slots] = torch.from_numpy(vals).to(dev)
@@ -367,6 +395,13 @@ class OutOfGraphReplayBuffer(object):
       raise ValueError('Sum tree values should be nonnegative. Got {}'.format(meta.status_value))
     if st == _lib.ST_BAD_INDEX:
       raise IndexError('index {} is out of bounds for the sum tree'.format(int(meta.status_value)))
+    if st == _lib.ST_BROADCAST:
+      # crb:540-541 with a trajectory length L that numpy cannot broadcast: raise numpy's
+      # own error for those shapes (host shapes only, no data)
+      L = int(meta.status_arg)
+      prod = np.zeros(L, np.float32) * np.zeros((L,) + self._reward_shape, self._reward_dtype)
+      np.empty((1,) + self._reward_shape, self._reward_dtype)[0] = np.sum(prod, axis=0)
+      raise ValueError('reward of trajectory length {} does not broadcast'.format(L))
     raise RuntimeError('replay device status %d' % st)
 
   def _clear_status(self, meta):
@@ -422,10 +457,20 @@ class OutOfGraphReplayBuffer(object):
       a = t.cpu().numpy().view(self._observation_dtype).reshape((batch_size, S) + self._observation_shape)
       return np.moveaxis(a, 1, -1)
 
-    res = [stack(out['state']), out['action'].cpu().numpy().astype(self._action_dtype),
-           out['reward'].cpu().numpy().astype(self._reward_dtype), stack(out['next_state']),
-           out['next_action'].cpu().numpy().astype(self._action_dtype),
-           out['next_reward'].cpu().numpy().astype(self._reward_dtype),
+    if self._generic_reward:
+      self._check_status(self._read_meta(), batch_size)   # a reward that did not broadcast
+
+    def act(t):
+      if self._generic_action:
+        return t.cpu().numpy().reshape(batch_size, -1)[:, :self._act_bytes()].copy().view(
+            self._action_dtype).reshape((batch_size,) + self._action_shape)
+      return t.cpu().numpy().astype(self._action_dtype)
+
+    def rew(t):
+      return t.cpu().numpy().astype(self._reward_dtype)
+
+    res = [stack(out['state']), act(out['action']), rew(out['reward']), stack(out['next_state']),
+           act(out['next_action']), rew(out['next_reward']),
            out['terminal'].cpu().numpy().view(np.uint8).astype(self._terminal_dtype),
            out['indices'].cpu().numpy()]
     for e in self._extra_storage_types:
@@ -449,12 +494,20 @@ class OutOfGraphReplayBuffer(object):
             (B, S) + tuple(self._observation_shape))
       return raw
 
+    if self._generic_action:
+      acts = lambda: torch.empty((B, self._act_rows.shape[1]), dtype=torch.uint8, device=dev)
+    else:
+      acts = lambda: torch.empty((B,), dtype=torch.int32, device=dev)
+    if self._generic_reward:
+      rews = lambda: torch.empty((B,) + self._reward_shape, dtype=self._rew_store.dtype, device=dev)
+    else:
+      rews = lambda: torch.empty((B,), dtype=torch.float32, device=dev)
     out = {'state': states(),
            'next_state': states(),
-           'action': torch.empty((B,), dtype=torch.int32, device=dev),
-           'reward': torch.empty((B,), dtype=torch.float32, device=dev),
-           'next_action': torch.empty((B,), dtype=torch.int32, device=dev),
-           'next_reward': torch.empty((B,), dtype=torch.float32, device=dev),
+           'action': acts(),
+           'reward': rews(),
+           'next_action': acts(),
+           'next_reward': rews(),
            'terminal': torch.empty((B,), dtype=torch.uint8, device=dev),
            'indices': torch.empty((B,), dtype=torch.int32, device=dev)}
     if self._prioritized:
@@ -466,8 +519,10 @@ class OutOfGraphReplayBuffer(object):
       out = self._alloc_batch(batch_size, layout)
     p = _lib.ptr
     if self._riders is not None:
-      if layout != _lib.LAYOUT_F32_NHWC or self._extra_storage_types:
-        raise ValueError('only the NHWC gather (no extra storage) can be recorded as a rider')
+      if (layout != _lib.LAYOUT_F32_NHWC or self._extra_storage_types or self._generic_action or
+          self._generic_reward):
+        raise ValueError('only the NHWC gather (no extra storage, scalar int32 action and '
+                         'float32 reward) can be recorded as a rider')
       r = _lib.Rider()
       _lib.call('dq_replay_record_gather_nhwc', self._h, p(d_idx), batch_size, p(out['state']),
                 p(out['next_state']), p(out['action']), p(out['reward']), p(out['next_action']),
@@ -475,10 +530,23 @@ class OutOfGraphReplayBuffer(object):
                 p(out.get('sampling_probabilities')), ctypes.byref(r))
       self._riders.append(r)
       return out
+    ga, gr = self._generic_action, self._generic_reward
     _lib.call('dq_replay_gather', self._h, p(d_idx), batch_size, layout, p(out['state']),
-              p(out['next_state']), p(out['action']), p(out['reward']), p(out['next_action']),
-              p(out['next_reward']), p(out['terminal']), p(out['indices']),
+              p(out['next_state']), None if ga else p(out['action']),
+              None if gr else p(out['reward']), None if ga else p(out['next_action']),
+              None if gr else p(out['next_reward']), p(out['terminal']), p(out['indices']),
               p(out.get('sampling_probabilities')), self._stream)
+    if ga or gr:
+      rs = self._rew_store if gr else None
+      _lib.call('dq_replay_gather_elems', self._h, p(d_idx), batch_size,
+                p(self._act_rows) if ga else None, self._act_bytes() if ga else 0,
+                p(rs), int(np.prod(self._reward_shape, dtype=np.int64)) if gr else 1,
+                (self._reward_shape[-1] if self._reward_shape else 0) if gr else 0,
+                _lib.DT_CODES[np.dtype(self._reward_dtype).name] if gr else 0,
+                int(np.result_type(np.float32, self._reward_dtype) == np.float64) if gr else 0,
+                p(out['action']) if ga else None, p(out['next_action']) if ga else None,
+                p(out['reward']) if gr else None, p(out['next_reward']) if gr else None,
+                self._stream)
     if self._extra_storage_types:
       li = d_idx.long() % self._replay_capacity
       for e in self._extra_storage_types:
@@ -580,8 +648,15 @@ class OutOfGraphReplayBuffer(object):
     C = self._replay_capacity
     obs = self._frames.view(_torch_dtype(self._observation_dtype)).reshape(
         (C,) + tuple(self._observation_shape))
-    st = collections.OrderedDict([('observation', obs), ('action', self._actions),
-                                  ('reward', self._rewards), ('terminal', self._terminals)])
+    act, rew = self._actions, self._rewards
+    if self._generic_action:
+      ab = self._act_bytes()
+      act = self._act_rows[:, :ab].view(_torch_dtype(self._action_dtype)).reshape(
+          (C,) + self._action_shape) if ab else self._act_rows[:, :0].reshape((C,) + self._action_shape)
+    if self._generic_reward:
+      rew = self._rew_store
+    st = collections.OrderedDict([('observation', obs), ('action', act),
+                                  ('reward', rew), ('terminal', self._terminals)])
     for e in self._extra_storage_types:
       st[e.name] = self._extras[e.name]
     return st

@@ -150,7 +150,9 @@ class WrappedPrioritizedReplayBuffer(circular_replay_buffer.WrappedReplayBuffer)
     memory = OutOfGraphPrioritizedReplayBuffer(
         observation_shape, stack_size, replay_capacity, batch_size, update_horizon, gamma,
         max_sample_attempts, extra_storage_types=extra_storage_types,
-        observation_dtype=observation_dtype, device=device)
+        observation_dtype=observation_dtype, terminal_dtype=terminal_dtype,
+        action_shape=action_shape, action_dtype=action_dtype, reward_shape=reward_shape,
+        reward_dtype=reward_dtype, device=device)
     super().__init__(observation_shape, stack_size, use_staging, replay_capacity, batch_size,
                      update_horizon, gamma, wrapped_memory=memory,
                      extra_storage_types=extra_storage_types,

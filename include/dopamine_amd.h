@@ -40,6 +40,10 @@ extern "C" {
 #define DQ_ST_NEG_PRIORITY 4      /* sum_tree.py:191-193 */
 #define DQ_ST_TOO_FEW 5           /* circular_replay_buffer.py:457-460 */
 #define DQ_ST_BAD_INDEX 6         /* leaf index outside the tree (numpy IndexError in sum_tree.py:196) */
+#define DQ_ST_BROADCAST 7         /* n-step reward: the (L,) discount vector does not broadcast
+                                     against (L,) + reward_shape (numpy ValueError at
+                                     circular_replay_buffer.py:540-541); status_arg = L,
+                                     status_value = 1 if the sum's shape could not be assigned */
 
 /* dq_sumtree_sample modes */
 #define DQ_SUMTREE_QUERY 0        /* SumTree.sample(query_value) for given values (sum_tree.py:99-141) */
@@ -127,6 +131,34 @@ int dq_replay_gather(dq_replay* h, const int32_t* indices, int32_t batch, int32_
                      float* reward_out, int32_t* next_action_out, float* next_reward_out,
                      uint8_t* terminal_out, int32_t* indices_out, float* probs_out,
                      void* stream);
+
+/* The action / reward elements of a transition batch for buffers whose action or reward
+ * is not a scalar int32 / float32 (action_shape, action_dtype, reward_shape, reward_dtype of
+ * circular_replay_buffer.py:96-183; the sampling at :530-548).  Per sample b with
+ * idx = indices[b] and L its n-step length (the terminal store, crb:517-526):
+ *   action_out[b] = action_rows[idx], next_action_out[b] = action_rows[(idx + L) % C]
+ *     (action_bytes-byte rows, copied as they are);
+ *   reward_out[b] = sum over i < L of disc * rewards[(idx + i) % C], numpy's
+ *     np.sum(discount[:L] * trajectory_rewards, axis=0): the (L,) float32 discount vector
+ *     broadcasts against the LAST axis of (L,) + reward_shape (reward_last = its size, 0 for
+ *     a scalar reward), products and the left-to-right sum in float64 when acc_f64 (numpy's
+ *     float32 x reward_dtype promotion) else float32, then cast to reward_dtype;
+ *   next_reward_out[b] = rewards[(idx + L) % C].
+ * reward_dtype: DQ_DT_*; reward_elems = prod(reward_shape).  A sample whose L does not
+ * broadcast latches DQ_ST_BROADCAST.  Any output pointer may be NULL. */
+#define DQ_DT_F32 0
+#define DQ_DT_F64 1
+#define DQ_DT_F16 2
+#define DQ_DT_I8 3
+#define DQ_DT_U8 4
+#define DQ_DT_I16 5
+#define DQ_DT_I32 6
+#define DQ_DT_I64 7
+int dq_replay_gather_elems(dq_replay* h, const int32_t* indices, int32_t batch,
+                           const void* action_rows, int32_t action_bytes, const void* rewards,
+                           int32_t reward_elems, int32_t reward_last, int32_t reward_dtype,
+                           int32_t acc_f64, void* action_out, void* next_action_out,
+                           void* reward_out, void* next_reward_out, void* stream);
 
 /* set_priority (prioritized_replay_buffer.py:203-214 -> sum_tree.py:178-205):
  * ordered, delta-propagating float64 updates, duplicates honoured. */

@@ -120,7 +120,8 @@ class ReplayOracle:
   def __init__(self, observation_shape, stack_size, replay_capacity, batch_size,
                update_horizon=1, gamma=0.99, max_sample_attempts=1000,
                observation_dtype=np.uint8, terminal_dtype=np.uint8,
-               reward_dtype=np.float32, py_rng=None, np_rng=None):
+               reward_dtype=np.float32, py_rng=None, np_rng=None, action_shape=(),
+               action_dtype=np.int32, reward_shape=()):
     if replay_capacity < update_horizon + stack_size:
       raise ValueError('There is not enough capacity to cover '
                        'update_horizon and stack_size.')
@@ -135,8 +136,10 @@ class ReplayOracle:
     self.py_rng = py_rng or _random
     self.np_rng = np_rng or np.random
     self.observation = np.zeros((self.C,) + self.obs_shape, observation_dtype)
-    self.action = np.zeros((self.C,), np.int32)
-    self.reward = np.zeros((self.C,), reward_dtype)
+    self.action_shape, self.action_dtype = tuple(action_shape), action_dtype
+    self.reward_shape, self.reward_dtype = tuple(reward_shape), reward_dtype
+    self.action = np.zeros((self.C,) + self.action_shape, action_dtype)
+    self.reward = np.zeros((self.C,) + self.reward_shape, reward_dtype)
     self.terminal = np.zeros((self.C,), terminal_dtype)
     self.add_count = 0
     self.invalid_range = np.zeros((self.stack,))
@@ -229,6 +232,10 @@ class ReplayOracle:
     term = bool(traj.any())
     L = int(np.argmax(traj.astype(bool))) + 1 if term else self.n
     r = self.reward[self._ring(idx, L)]
+    if self.reward_shape or np.dtype(self.reward_dtype) != np.float32:
+      # crb:540-541 as written: the (L,) float32 discount broadcast against (L,) +
+      # reward_shape (numpy raises where it does not), summed over axis 0
+      return np.sum(self.discount[:L] * r, axis=0), term, L
     acc = np.float32(0.0)
     for k in range(L):  # float32 products summed left to right (numpy n<8 loop)
       acc = np.float32(acc + np.float32(self.discount[k] * r[k]))
@@ -241,10 +248,10 @@ class ReplayOracle:
     assert len(indices) == B
     st = np.empty((B,) + self.obs_shape + (self.stack,), self.obs_dtype)
     nst = np.empty_like(st)
-    act = np.empty((B,), np.int32)
-    rew = np.empty((B,), np.float32)
-    nact = np.empty((B,), np.int32)
-    nrew = np.empty((B,), np.float32)
+    act = np.empty((B,) + self.action_shape, self.action_dtype)
+    rew = np.empty((B,) + self.reward_shape, self.reward_dtype)
+    nact = np.empty_like(act)
+    nrew = np.empty_like(rew)
     term = np.empty((B,), np.uint8)
     ind = np.empty((B,), np.int32)
     for b, idx in enumerate(indices):

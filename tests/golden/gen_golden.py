@@ -233,16 +233,85 @@ def gen_checkpoint_per(m):
   np.savez_compressed(os.path.join(OUT, 'ckpt_per_expected.npz'), **out)
 
 
+# (name, capacity, n, stack, adds, gamma, B, rounds, action (shape, dtype), reward (shape, dtype))
+SHAPE_CASES = [
+    ('a', 40, 1, 2, 97, 0.9, 6, 5, ((2,), 'int8'), ((3,), 'float32')),
+    ('b', 40, 3, 2, 101, 0.9, 6, 0, ((), 'int64'), ((3,), 'float64')),
+    ('c', 40, 3, 1, 89, 0.95, 5, 4, ((2, 2), 'float32'), ((), 'float64')),
+    ('d', 40, 3, 2, 77, 0.9, 5, 4, ((), 'int32'), ((), 'int32')),
+    ('e', 40, 1, 2, 66, 0.8, 4, 4, ((), 'uint8'), ((2, 3), 'float16')),
+]
+
+
+def gen_shapes(m):
+    """Non-scalar / non-default action and reward elements (crb:96-183, 530-548): sampled
+    batches (np.random, rounds > 0), an explicit-index batch over indices whose n-step
+    length broadcasts, and for case b one index whose length does not (numpy's error)."""
+    crb = m['circular_replay_buffer']
+    out = {'cases': np.array([c[0] for c in SHAPE_CASES])}
+    rs = np.random.RandomState(21)
+    for name, C, n, stack, adds, gamma, B, rounds, (ash, adt), (rsh, rdt) in SHAPE_CASES:
+        mem = crb.OutOfGraphReplayBuffer(observation_shape=(4, 4), stack_size=stack,
+                                         replay_capacity=C, batch_size=B, update_horizon=n,
+                                         gamma=gamma, action_shape=ash, action_dtype=np.dtype(adt),
+                                         reward_shape=rsh, reward_dtype=np.dtype(rdt))
+        obs = rs.randint(0, 256, (adds, 4, 4)).astype(np.uint8)
+        act = rs.randint(-3, 100, (adds,) + ash).astype(adt)
+        rew = (rs.randint(-4, 5, (adds,) + rsh) * 0.37).astype(rdt)
+        term = (rs.rand(adds) < 0.12).astype(np.uint8)
+        for i in range(adds):
+            mem.add(obs[i], act[i], rew[i], term[i])
+        pre = name + '_'
+        out[pre + 'meta'] = np.array([C, n, stack, adds, B, rounds], np.int64)
+        out[pre + 'gamma'] = np.float64(gamma)
+        out[pre + 'obs'], out[pre + 'act'], out[pre + 'rew'], out[pre + 'term'] = obs, act, rew, term
+        keys = ['state', 'action', 'reward', 'next_state', 'next_action', 'next_reward',
+                'terminal', 'indices']
+        np.random.seed(500 + C + n)
+        out[pre + 'seed'] = np.int64(500 + C + n)
+        rows = {k: [] for k in keys}
+        for _ in range(rounds):
+            for k, v in zip(keys, mem.sample_transition_batch()):
+                rows[k].append(np.array(v))
+        for k in keys:
+            if rounds:
+                out[pre + k] = np.stack(rows[k])
+        traj_len = {}
+        for i in range(C):
+            if mem.is_valid_transition(i):
+                t = mem._store['terminal'][[(i + j) % C for j in range(n)]]
+                traj_len[i] = int(np.argmax(t.astype(bool))) + 1 if t.any() else n
+        m_last = rsh[-1] if rsh else 0
+        ok = [i for i, L in sorted(traj_len.items()) if not m_last or L in (m_last, 1)]
+        fixed = ok[:B]
+        out[pre + 'fixed_indices'] = np.array(fixed, np.int64)
+        for k, v in zip(keys, mem.sample_transition_batch(batch_size=len(fixed), indices=fixed)):
+            out[pre + 'fixed_' + k] = np.array(v)
+        bad = [i for i, L in sorted(traj_len.items()) if m_last and L not in (m_last, 1)]
+        if bad:
+            try:
+                mem.sample_transition_batch(batch_size=1, indices=[bad[0]])
+                out[pre + 'bad_error'] = np.array('')
+            except ValueError as e:
+                out[pre + 'bad_error'] = np.array(str(e))
+            out[pre + 'bad_index'] = np.int64(bad[0])
+    np.savez_compressed(os.path.join(OUT, 'replay_shapes.npz'), **out)
+
+
 if __name__ == '__main__':
   mods = _load_reference()
   if sys.argv[1:] == ['ckpt_per']:
     gen_checkpoint_per(mods)
+    sys.exit(0)
+  if sys.argv[1:] == ['shapes']:
+    gen_shapes(mods)
     sys.exit(0)
   gen_sumtree(mods)
   gen_replay(mods, prioritized=False)
   gen_replay(mods, prioritized=True)
   gen_checkpoint(mods)
   gen_checkpoint_per(mods)
+  gen_shapes(mods)
   for f in sorted(os.listdir(OUT)):
     if f.endswith('.npz'):
       print(f, os.path.getsize(os.path.join(OUT, f)))

@@ -97,3 +97,43 @@ def test_reference_checkpoint_fixture_is_plain_npy():
   for f in names:
     with gzip.open(os.path.join(d, f), 'rb') as fh:
       np.load(fh, allow_pickle=False)
+
+
+SHAPE_KEYS = ['state', 'action', 'reward', 'next_state', 'next_action', 'next_reward',
+              'terminal', 'indices']
+
+
+def shape_case(z, name):
+  """(kwargs, adds) of a tests/golden/replay_shapes.npz case (gen_golden.SHAPE_CASES)."""
+  C, n, stack, adds, B, rounds = [int(x) for x in z[name + '_meta']]
+  act, rew = z[name + '_act'], z[name + '_rew']
+  kw = dict(observation_shape=(4, 4), stack_size=stack, replay_capacity=C, batch_size=B,
+            update_horizon=n, gamma=float(z[name + '_gamma']), action_shape=act.shape[1:],
+            action_dtype=act.dtype, reward_shape=rew.shape[1:], reward_dtype=rew.dtype)
+  return kw, adds, rounds
+
+
+def test_shapes_golden(golden):
+  """Non-scalar / non-default action and reward elements (crb:96-183, 530-548)."""
+  z = golden('replay_shapes.npz')
+  for name in _case_names(z):
+    kw, adds, rounds = shape_case(z, name)
+    np_rng = np.random.RandomState(int(z[name + '_seed']))
+    mem = orc.ReplayOracle(kw['observation_shape'], kw['stack_size'], kw['replay_capacity'],
+                           kw['batch_size'], update_horizon=kw['update_horizon'],
+                           gamma=kw['gamma'], np_rng=np_rng, action_shape=kw['action_shape'],
+                           action_dtype=kw['action_dtype'], reward_shape=kw['reward_shape'],
+                           reward_dtype=kw['reward_dtype'])
+    for i in range(adds):
+      mem.add(z[name + '_obs'][i], z[name + '_act'][i], z[name + '_rew'][i], z[name + '_term'][i])
+    for r in range(rounds):
+      for k, v in zip(SHAPE_KEYS, mem.sample_transition_batch()):
+        np.testing.assert_array_equal(v, z[name + '_' + k][r], err_msg='%s %s %d' % (name, k, r))
+        assert v.dtype == z[name + '_' + k].dtype, (name, k)
+    fixed = [int(i) for i in z[name + '_fixed_indices']]
+    for k, v in zip(SHAPE_KEYS, mem.sample_transition_batch(len(fixed), indices=fixed)):
+      np.testing.assert_array_equal(v, z[name + '_fixed_' + k], err_msg='%s fixed %s' % (name, k))
+    if name + '_bad_index' in z:
+      with pytest.raises(ValueError) as e:
+        mem.sample_transition_batch(1, indices=[int(z[name + '_bad_index'])])
+      assert str(e.value) == str(z[name + '_bad_error'])
