@@ -49,6 +49,9 @@ def parse():
                   help='override the agent default fuse_optimizer (0/1)')
   ap.add_argument('--ride', type=int, default=None,
                   help='override the agent default ride_replay (0/1)')
+  ap.add_argument('--split-c51', type=int, default=None,
+                  help='override RainbowAgent.split_c51 (0/1): the C51 target half riding in '
+                       'the forward (head_from 8) or inside the loss kernel')
   ap.add_argument('--force-dist', action='store_true',
                   help='one rank only: run the N > 1 learner schedule over a one-rank RCCL group '
                        'with every collective executed (a hardware check of the data-parallel '
@@ -235,6 +238,9 @@ def main():
     os.environ.setdefault('MASTER_PORT', '29533')
     dist.init_process_group('nccl', rank=0, world_size=1, device_id=dev)
     pg = dist.group.WORLD
+  if args.split_c51 is not None:
+    from dopamine_amd.agents.rainbow.rainbow_agent import RainbowAgent
+    RainbowAgent.split_c51 = bool(args.split_c51)
   agent = build_agent(args.actions, args.capacity, args.batch, dev, pg=pg,
                       use_hip_graph=not args.no_graph,
                       **({} if args.fuse_opt is None else {'fuse_optimizer': bool(args.fuse_opt)}),

@@ -66,6 +66,13 @@ class CnnActs(ctypes.Structure):
   _fields_ = [(n, ctypes.c_void_p) for n in ('a1', 'a2', 'a3', 'h', 'out')]
 
 
+class C51Target(ctypes.Structure):
+  _fields_ = [('rewards', ctypes.c_void_p), ('terminals', ctypes.c_void_p),
+              ('support', ctypes.c_void_p), ('num_atoms', ctypes.c_int32),
+              ('cumulative_gamma', ctypes.c_float), ('m_out', ctypes.c_void_p),
+              ('target_logits_out', ctypes.c_void_p)]
+
+
 class CnnNet(ctypes.Structure):
   _fields_ = [('p', ctypes.c_void_p), ('x', ctypes.c_void_p), ('a', ctypes.c_void_p),
               ('ws', ctypes.c_void_p)]
@@ -149,6 +156,11 @@ SIGNATURES = {
                              ctypes.POINTER(CnnParams), _P, ctypes.POINTER(CnnActs), _P, _I32,
                              _I32, _P],
     'dq_cnn_fc2_parts_offset': [_I32],
+    'dq_cnn_forward_fused_c51': [ctypes.POINTER(CnnParams), _P, ctypes.POINTER(CnnActs), _P,
+                                 ctypes.POINTER(CnnParams), ctypes.POINTER(CnnActs), _P, _I32,
+                                 ctypes.POINTER(C51Target), _I32, _P],
+    'dq_c51_loss_online': [_P, _P, _I32, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _I32,
+                           _P, _P],
     'dq_c51_loss_fused': [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _I32, _I32, _I32, _F, _P, _P,
                           _P, _P, _P, _P, _I32, _P, _P, _P],
     'dq_cnn_forward_head': [ctypes.POINTER(CnnParams), _I32, _P, ctypes.POINTER(CnnActs), _P, _P],

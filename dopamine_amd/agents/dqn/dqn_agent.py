@@ -363,6 +363,9 @@ class DQNAgent(object):
     from dopamine_amd import cnn
     if self._fused():
       hf = self._head_from()
+      if hf == 8:                   # the target net one launch ahead, its C51 half riding
+        self._forward_fused_c51(c, part)
+        return
       cnn.forward_fused(self._hip['online'], self._pbuf[c]['state'], self._hip['target'][c],
                         conv3_b=hf >= 5, conv2_b=hf >= 6, part=part,
                         xb=self._pbuf[c]['next_state'] if hf == 7 else None)
@@ -371,6 +374,14 @@ class DQNAgent(object):
     on, tg = cnn.forward_with_tail(self._hip['online'], self._pbuf[c]['state'], self._hip['target'][c])
     self._online_ready = on
     self._ptgt[c] = self._target_dict(tg)
+
+  def _forward_fused_c51(self, c, part=None):
+    raise NotImplementedError
+
+  def _bwd_head_from(self):
+    """head_from for the backward: 8 places the target's conv1 as 6 does."""
+    hf = self._head_from()
+    return 6 if hf == 8 else hf
 
   def _bwd_first(self):
     return 1 if self._fused() else 0
@@ -437,7 +448,7 @@ class DQNAgent(object):
       adam = self._opt if self._fused_opt() else None
       f = self._bwd_first()
       self._hip['online'].backward(g, riders=riders, adam=adam, slot=k, head=self._head,
-                                   groups=(f, 7), head_from=self._head_from())
+                                   groups=(f, 7), head_from=self._bwd_head_from())
       self._head = None
     elif pipe:
       main = torch.cuda.current_stream(self._device)
@@ -507,7 +518,7 @@ class DQNAgent(object):
       f = self._bwd_first()
       self._hip['online'].backward(g, groups=(self._SPLIT, 7),
                                    head=self._tail_head if pipe else None,
-                                   riders=self._tail_riders if pipe else None, head_from=self._head_from())
+                                   riders=self._tail_riders if pipe else None, head_from=self._bwd_head_from())
       self._tail_head = self._tail_riders = None
     elif pipe:
       main = torch.cuda.current_stream(self._device)

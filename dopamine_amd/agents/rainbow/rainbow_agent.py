@@ -100,6 +100,7 @@ class RainbowAgent(dqn_agent.DQNAgent):
     # mean_loss=None: the summary mean is not on the gradient path (computed on demand)
     self._loss_out = dict(grad=torch.empty((B, A, N), device=dev), loss=torch.empty(B, device=dev),
                           priorities=torch.empty(B, device=dev), mean_loss=None)
+    self._c51_m = torch.empty((B, N), device=dev)   # head_from 8: the projected target distribution
 
   def mean_loss(self):
     """mean(w * CE) of the last step (the CrossEntropyLoss summary, rb:298-301)."""
@@ -132,10 +133,37 @@ class RainbowAgent(dqn_agent.DQNAgent):
   def _fused(self):
     return self.fused_head and self._rides()
 
+  # The C51 loss split in two (head_from 8): the target half (softmax, Q, greedy action,
+  # projection: rb:200-251, 340-494) rides in the online forward's last launch, the target
+  # network running one launch ahead of the online one; the loss launch keeps the online
+  # half.  Bitwise the single-kernel loss (tests/test_gpu_cnn.py).  Measured (rocprof,
+  # profiles/r2_c51_split_ab.txt): the loss launch 9.6 -> 6.6 us, but the target's conv2
+  # beside the online conv1 takes that launch 6.4 -> 10.6 us: 7,290 vs 7,220 steps/s for
+  # the one-kernel loss, so off by default.
+  split_c51 = False
+
+  def _head_from(self):
+    if self._fused() and self.split_c51 and self.num_actions <= 16 and self._num_atoms <= 64:
+      return 8
+    return super()._head_from()
+
+  def _forward_fused_c51(self, c, part=None):
+    from dopamine_amd import cnn
+    t, tg = self._pbuf[c], self._hip['target'][c]
+    cnn.forward_fused_c51(self._hip['online'], t['state'], tg, t['reward'], t['terminal'],
+                          self._support, self.cumulative_gamma, self._c51_m,
+                          target_logits_out=tg.acts['out'] if self._trace is not None else None,
+                          part=part)
+
   def _fused_loss(self, t, c):
     """_online_loss on the CNN's fc2 partials (cnn.forward_fused): the logits are
     summed inside the loss kernel, which also writes fc2's input gradient."""
     prioritized = self._replay_scheme == 'prioritized'
+    if self._head_from() == 8:
+      out = ops.c51_loss_online(self._hip['online'], self._c51_m, t['action'],
+                                probs=t['sampling_probabilities'] if prioritized else None,
+                                out=self._loss_out, logits_out=self._trace is not None)
+      return None, out['grad']
     out = ops.c51_loss_fused(self._hip['online'], self._hip['target'][c], t['action'], t['reward'],
                              t['terminal'], self._support, self.cumulative_gamma,
                              probs=t['sampling_probabilities'] if prioritized else None,

@@ -252,3 +252,25 @@ def forward_fused(a, xa, b, fc1_b=True, conv3_b=False, part=None, conv2_b=False,
       16 * int(bool(conv2_b)) | 32 * int(xb is not None),
       a._stream(xa)), 'dq_cnn_forward_fused')
   return fc2_parts(a), fc2_parts(b)
+
+
+def forward_fused_c51(a, xa, b, rewards, terminals, support, cumulative_gamma, m_out,
+                      target_logits_out=None, part=None):
+  """dq_cnn_forward_fused_c51 (head_from = 8): ``a`` (online) on ``xa`` as
+  ``forward_fused``, ``b`` (target; its conv1 already run, by the previous backward) one
+  launch ahead -- its conv2 / conv3 / fc1 slabs / fused head beside ``a``'s conv1 / conv2
+  / conv3 / fc1 -- and the target half of the C51 loss beside ``a``'s fused head, writing
+  the projected target distribution into ``m_out`` (B, N).  part: as forward_fused."""
+  assert a.B == b.B and a is not b
+  xa = a._nhwc(xa)
+  a._x = xa
+  t = _lib.C51Target(rewards=rewards.data_ptr(), terminals=terminals.data_ptr(),
+                     support=support.data_ptr(), num_atoms=int(support.numel()),
+                     cumulative_gamma=float(cumulative_gamma), m_out=m_out.data_ptr(),
+                     target_logits_out=None if target_logits_out is None
+                     else target_logits_out.data_ptr())
+  _lib.check(_lib.lib.dq_cnn_forward_fused_c51(
+      ctypes.byref(a._p), xa.data_ptr(), ctypes.byref(a._a), a.ws.data_ptr(),
+      ctypes.byref(b._p), ctypes.byref(b._a), b.ws.data_ptr(), a.B, ctypes.byref(t),
+      {None: 0, 'convs': 4, 'fcs': 8}[part], a._stream(xa)), 'dq_cnn_forward_fused_c51')
+  return fc2_parts(a), m_out

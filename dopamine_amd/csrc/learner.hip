@@ -4,7 +4,7 @@
 // Restates the TF1 graph code of rainbow_agent.py:200-305 + 340-494,
 // dqn_agent.py:283-322, implicit_quantile_agent.py:190-321 and the TF1
 // ApplyAdam / ApplyCenteredRMSProp op semantics.
-#include "common.h"
+#include "c51_dev.h"
 
 namespace dq {
 
@@ -27,30 +27,6 @@ struct C51Args {
   float* mean_out;
 };
 
-// Logit sources: stored logits, or (the fused Rainbow path) fc2's 16 k-band
-// partial products summed in band order plus the bias -- exactly the reduction
-// order of the CNN's fc2 tile, so the logits are bitwise dq_cnn_forward's.
-struct LogitsDirect {
-  const float* p;
-  __device__ __forceinline__ float get(int64_t i) const { return p[i]; }
-};
-struct LogitsParts {
-  const float* part;   // [np][B * NO]
-  const float* bias;   // [NO]
-  int64_t stride;      // B * NO
-  int np, NO;          // np <= 16: straight-line loads, all in flight before the first add
-  __device__ __forceinline__ float get(int64_t i) const {
-    float v[16];
-#pragma unroll
-    for (int z = 0; z < 16; ++z) v[z] = part[(int64_t)min(z, np - 1) * stride + i];
-    float x = v[0];
-#pragma unroll
-    for (int z = 1; z < 16; ++z)
-      if (z < np) x = __fadd_rn(x, v[z]);
-    return __fadd_rn(x, bias[i % NO]);
-  }
-};
-
 // The fused path's extras: logits written out (the CNN never stores them), and the
 // fc2 input gradient d h = (dlogits . W2) * (h > 0) -- only the chosen action's
 // N logits of a sample have a nonzero gradient, so row b of d h is an N-term sum.
@@ -71,38 +47,6 @@ struct C51Extra {
 // instead of N -- before the softmax cross-entropy of the chosen online logits.
 // The fused path (x.w2) also forms d h from the chosen action's N logit
 // gradients; its W2 rows are fetched into LDS at the start, under the chain.
-
-// Wave-wide reductions on DPP row rotations (no LDS round trips, unlike __shfl_xor's
-// ds_bpermute chain): each 16-lane row reduces by row_ror 8, 4, 2, 1, then lanes 0, 16,
-// 32, 48 combine as (r0 op r1) op (r2 op r3) -- one value, the same in every lane.
-template <int kCtrl>
-__device__ __forceinline__ float dpp_ror(float v) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), kCtrl, 0xf, 0xf, false));
-}
-__device__ __forceinline__ float rl(float v, int l) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-}
-__device__ __forceinline__ float fast_sum(float v) {
-  v = __fadd_rn(v, dpp_ror<0x128>(v));
-  v = __fadd_rn(v, dpp_ror<0x124>(v));
-  v = __fadd_rn(v, dpp_ror<0x122>(v));
-  v = __fadd_rn(v, dpp_ror<0x121>(v));
-  return __fadd_rn(__fadd_rn(rl(v, 0), rl(v, 16)), __fadd_rn(rl(v, 32), rl(v, 48)));
-}
-__device__ __forceinline__ float fast_max(float v) {
-  v = fmaxf(v, dpp_ror<0x128>(v));
-  v = fmaxf(v, dpp_ror<0x124>(v));
-  v = fmaxf(v, dpp_ror<0x122>(v));
-  v = fmaxf(v, dpp_ror<0x121>(v));
-  return fmaxf(fmaxf(rl(v, 0), rl(v, 16)), fmaxf(rl(v, 32), rl(v, 48)));
-}
-__device__ __forceinline__ float fast_min(float v) {
-  v = fminf(v, dpp_ror<0x128>(v));
-  v = fminf(v, dpp_ror<0x124>(v));
-  v = fminf(v, dpp_ror<0x122>(v));
-  v = fminf(v, dpp_ror<0x121>(v));
-  return fminf(fminf(rl(v, 0), rl(v, 16)), fminf(rl(v, 32), rl(v, 48)));
-}
 
 #ifdef DQ_C51_PROF
 __device__ long long g_c51_t[256][8];
@@ -314,6 +258,111 @@ extern "C" int dq_debug_c51_wave_times(long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_c51_w), sizeof(g_c51_w)) == hipSuccess ? 0 : -1;
 }
 #endif
+
+// The online half of k_c51 (the fused Rainbow path with the target half riding in the
+// forward, TgtC51Op): m = the projected target distribution (B, N) is read instead of
+// formed.  Everything else is k_c51's online arithmetic in k_c51's order -- the chosen
+// online row's log-softmax, the cross-entropy, PER weights, priorities, dlogits and
+// d h = (dlogits . W2) * (h > 0) -- so loss, gradient and priorities are bitwise k_c51's.
+// One block per sample, T = 64 * waves threads.
+template <class LS>
+__global__ __launch_bounds__(1024) void k_c51_online(C51Args a, LS ol, const float* __restrict__ m,
+                                                     C51Extra x) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int N = a.N, A = a.A, b = blockIdx.x, T = blockDim.x;
+  float* s_g = smem;                                   // [N] the chosen row's logit gradient
+  float* s_w = smem + (N + 3) / 4 * 4;                 // [N][H] fc2 rows, 16-B aligned
+  __shared__ float s_red[16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = T >> 6;
+  const bool on = lane < N;
+  const float ninf = -__builtin_inff();
+  const int ab = a.act[b];
+  const float pr_t = a.probs ? a.probs[min((int)threadIdx.x, a.B - 1)] : 0.0f;
+  const float pr_b = a.probs ? a.probs[b] : 0.0f;
+  const float hv = x.w2 ? x.h[(int64_t)b * x.H + min((int)threadIdx.x, x.H - 1)] : 0.0f;
+  const int lc = min(lane, N - 1);
+  float y = ninf, proj = 0.0f;
+  if (wave == 0) {
+    const float y0 = ol.get(((int64_t)b * A + ab) * N + lc);
+    const float m0 = m[(int64_t)b * N + lc];
+    y = on ? y0 : ninf;
+    proj = on ? m0 : 0.0f;
+  }
+  if (a.probs) {
+    float pm = pr_t;
+    for (int i = threadIdx.x + T; i < a.B; i += T) pm = fminf(pm, a.probs[i]);
+    pm = fast_min(pm);
+    if (lane == 0) s_red[wave] = pm;
+  }
+  float sh = 0.0f, ey = 0.0f, lse = 0.0f, py = 0.0f;
+  if (wave == 0) {
+    const float my = fast_max(y);
+    sh = on ? __fsub_rn(y, my) : 0.0f;
+    ey = on ? expf(sh) : 0.0f;
+    const float sy = fast_sum(ey);
+    lse = logf(sy);
+    py = __fdiv_rn(ey, sy);
+  }
+  if (x.ol_out)
+    for (int act = wave; act < A; act += nw) {
+      const int64_t i = ((int64_t)b * A + act) * N + lane;
+      if (on) x.ol_out[i] = act == ab && wave == 0 ? y : ol.get(i);
+    }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // s_red complete (bare: see k_c51)
+  if (x.w2 && (wave > 0 || nw == 1)) {
+    const int bytes = N * x.H * 4, nq = (bytes + 1023) >> 10;
+    const int w0 = nw > 1 ? wave - 1 : 0, nwd = nw > 1 ? nw - 1 : 1;
+    const char* src = reinterpret_cast<const char*>(x.w2 + (int64_t)ab * N * x.H);
+    for (int q = w0; q < nq; q += nwd) {
+      const int off = min(q * 1024 + lane * 16, bytes - 16);
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + off),
+                                       (__attribute__((address_space(3))) void*)(
+                                           reinterpret_cast<char*>(s_w) + q * 1024),
+                                       16, 0, 0);
+    }
+  }
+  float w = 1.0f;
+  if (a.probs) {
+    float pm = s_red[0];
+    for (int i = 1; i < nw; ++i) pm = fminf(pm, s_red[i]);
+    const float mm = __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(pm, 1e-10f)));
+    w = __fdiv_rn(__fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(pr_b, 1e-10f))), mm);
+  }
+  const float gscale = __fmul_rn(w, __fdiv_rn(1.0f, (float)a.B));
+  for (int act = wave; act < A; act += nw) {
+    if (act == ab) continue;
+    if (on) a.grad[((int64_t)b * A + act) * N + lane] = 0.0f;
+  }
+  if (wave == 0) {
+    const float loss = fast_sum(on ? __fmul_rn(proj, __fsub_rn(lse, sh)) : 0.0f);
+    const float gr = on ? __fmul_rn(gscale, __fsub_rn(py, proj)) : 0.0f;
+    if (on) {
+      a.grad[((int64_t)b * A + ab) * N + lane] = gr;
+      s_g[lane] = gr;
+    }
+    if (lane == 0) {
+      if (a.loss_out) a.loss_out[b] = loss;
+      if (a.prio_out) a.prio_out[b] = __fsqrt_rn(__fadd_rn(loss, 1e-10f));
+    }
+  }
+  if (!x.w2) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int j = threadIdx.x; j < x.H; j += T) {
+    const float mk = j == (int)threadIdx.x ? hv : x.h[(int64_t)b * x.H + j];
+    float acc = 0.0f;
+    int i = 0;
+    for (; i + 8 <= N; i += 8) {
+      float tt[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) tt[u] = __fmul_rn(s_g[i + u], s_w[(i + u) * x.H + j]);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc = __fadd_rn(acc, tt[u]);
+    }
+    for (; i < N; ++i) acc = __fadd_rn(acc, __fmul_rn(s_g[i], s_w[i * x.H + j]));
+    x.dh[(int64_t)b * x.H + j] = mk > 0.0f ? acc : 0.0f;
+  }
+}
 
 // dynamic LDS of k_c51 (bytes), with the fused path's W2 rows when they fit the prefetch
 static size_t c51_lds(int A, int N, int H) {
@@ -622,6 +671,28 @@ int dq_c51_loss_fused(const float* online_parts, const float* online_bias,
                      LogitsParts{target_parts, target_bias, stride, n_parts, NO},
                      C51Extra{online_logits_out, target_logits_out, fc2_w, h, dh, hidden});
   DQ_CHECK_LAUNCH("k_c51 fused");
+  return DQ_OK;
+}
+
+int dq_c51_loss_online(const float* online_parts, const float* online_bias, int32_t n_parts,
+                       const float* target_m, const int32_t* actions, const float* probs,
+                       int32_t batch, int32_t num_actions, int32_t num_atoms, float* grad_logits,
+                       float* loss_out, float* priorities_out, const float* fc2_w, const float* h,
+                       float* dh, int32_t hidden, float* online_logits_out, void* stream) {
+  DQ_CHECK_ARG(online_parts && online_bias && target_m && actions && grad_logits, "null argument");
+  DQ_CHECK_ARG(n_parts >= 1 && n_parts <= 16, "n_parts must be in [1, 16]");
+  DQ_CHECK_ARG(num_atoms >= 2 && num_atoms <= 64, "num_atoms must be in [2, 64]");
+  DQ_CHECK_ARG(batch >= 1 && num_actions >= 1 && num_actions <= 64, "bad batch / num_actions");
+  DQ_CHECK_ARG(!fc2_w || (h && dh && hidden >= 1), "d h needs h, dh and hidden");
+  C51Args a{nullptr, nullptr, actions, nullptr, nullptr, probs, nullptr, batch, num_actions,
+            num_atoms, 0.0f, grad_logits, loss_out, priorities_out, nullptr};
+  const int NO = num_actions * num_atoms;
+  const size_t shm = ((size_t)(num_atoms + 3) / 4 * 4 + (fc2_w ? (size_t)num_atoms * hidden : 0)) *
+                     sizeof(float);
+  hipLaunchKernelGGL(k_c51_online<LogitsParts>, dim3(batch), dim3(512), shm, (hipStream_t)stream, a,
+                     LogitsParts{online_parts, online_bias, (int64_t)batch * NO, n_parts, NO},
+                     target_m, C51Extra{online_logits_out, nullptr, fc2_w, h, dh, hidden});
+  DQ_CHECK_LAUNCH("k_c51_online");
   return DQ_OK;
 }
 

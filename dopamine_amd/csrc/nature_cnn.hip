@@ -28,6 +28,7 @@
 
 
 #include "cnn_tile.h"
+#include "c51_dev.h"
 
 #include <cstring>
 
@@ -446,6 +447,38 @@ void forward_fused(Ctx& c0, Ctx& c1, const FwdOps& f0, const FwdOps& f1, bool fc
   group(c0, f0.fchead(), f1.fchead());
 }
 
+// The target half of the C51 loss (c51_dev.h) as a grouped-launch op: one 256-thread
+// block per sample, riding in the online fused-head launch (head_from = 8).
+struct TgtC51Op {
+  static constexpr int kT = 256;
+  static constexpr int kLds = c51_target_lds(4 * kC51TgtMaxWaveRows, 64);
+  C51Target t;
+  int blocks() const { return t.B; }
+  __device__ __forceinline__ void run(int blk, float* smem) const {
+    c51_target_block<kT>(t, blk, smem);
+  }
+};
+
+// head_from = 8: the target network one launch earlier than head_from = 6 (its conv1 rode
+// in the previous backward's last launch), so its fused head is final one launch before
+// the online one's and the C51 target half rides beside the online head.
+void forward_fused_c51(Ctx& c0, Ctx& c1, const FwdOps& f0, const FwdOps& f1, const C51Target& t,
+                       bool convs, bool fcs) {
+  const size_t n0 = FwdOps::fused_ws_floats(f0.B, f0.p->n_out);
+  const size_t n1 = FwdOps::fused_ws_floats(f1.B, f1.p->n_out);
+  c0.need = n0 > c0.need ? n0 : c0.need;
+  c1.need = n1 > c1.need ? n1 : c1.need;
+  if (c0.dry) return;
+  if (convs) {
+    group(c0, f0.conv1<DQ_F1_LATE>(), f1.conv2());
+    group(c0, f0.conv2<DQ_F2_LATE>(), f1.conv3());
+    group(c0, f0.conv3<DQ_F1_LATE>(), f1.fc1());
+  }
+  if (!fcs) return;
+  group(c0, f0.fc1<DQ_F4_LATE>(), f1.fchead());
+  group(c0, f0.fchead(), TgtC51Op{t});
+}
+
 // The online and target networks' forwards together: one grouped launch per layer
 // holding both nets' ops -- 6 launches instead of 12.
 void forward_pair(Ctx& c0, Ctx& c1, const dq_cnn_params* p0, const float* x0, dq_cnn_acts* a0,
@@ -845,6 +878,32 @@ int dq_cnn_forward_fused(const dq_cnn_params* p0, const float* x0, dq_cnn_acts* 
 }
 
 size_t dq_cnn_fc2_parts_offset(int32_t batch) { return FwdOps::part_offset(batch); }
+
+int dq_cnn_forward_fused_c51(const dq_cnn_params* p0, const float* x0, dq_cnn_acts* a0, float* ws0,
+                             const dq_cnn_params* p1, dq_cnn_acts* a1, float* ws1, int32_t batch,
+                             const dq_c51_target* c51, int32_t flags, void* stream) {
+  DQ_CHECK_ARG(p0 && a0 && x0 && ws0 && p1 && a1 && ws1 && c51 && batch >= 1, "null argument");
+  DQ_CHECK_ARG(p0->in_channels == 4 && p1->in_channels == 4 && p0->n_out >= 1 && p1->n_out >= 1,
+               "the Nature CNN takes 84x84x4 NHWC input");
+  DQ_CHECK_ARG(ws0 != ws1, "the two networks need separate workspaces");
+  DQ_CHECK_ARG((flags & 12) != 12, "flags 4 (convs only) and 8 (fc layers only) exclude each other");
+  DQ_CHECK_ARG(c51->rewards && c51->terminals && c51->support && c51->m_out, "null C51 argument");
+  DQ_CHECK_ARG(c51->num_atoms >= 2 && c51->num_atoms <= 64 && p1->n_out % c51->num_atoms == 0,
+               "n_out must be num_actions * num_atoms, 2 <= num_atoms <= 64");
+  const int A = p1->n_out / c51->num_atoms;
+  DQ_CHECK_ARG(A <= 4 * kC51TgtMaxWaveRows, "the riding C51 target half takes at most 16 actions");
+  Ctx c0{(hipStream_t)stream, ws0, false, 0}, c1{(hipStream_t)stream, ws1, false, 0};
+  const FwdOps f0{p0, x0, a0, ws0, batch}, f1{p1, nullptr, a1, ws1, batch};
+  const int NO = p1->n_out;
+  C51Target t{LogitsParts{ws1 + FwdOps::part_offset(batch), p1->fc2_b, (int64_t)batch * NO,
+                          FcHeadOp::kBands, NO},
+              c51->rewards, c51->terminals, c51->support, batch, A, c51->num_atoms,
+              c51->cumulative_gamma, c51->m_out, c51->target_logits_out};
+  forward_fused_c51(c0, c1, f0, f1, t, (flags & 8) == 0, (flags & 4) == 0);
+  DQ_CHECK_LAUNCH("dq_cnn_forward_fused_c51");
+  return DQ_OK;
+}
+
 
 int dq_cnn_backward(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch, const float* x,
                     const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d, float* ws,

@@ -67,6 +67,29 @@ def c51_loss_fused(online, target, actions, rewards, terminals, support, cumulat
   return out
 
 
+def c51_loss_online(online, target_m, actions, probs=None, out=None, logits_out=False):
+  """The online half of c51_loss_fused (dq_c51_loss_online): the target distribution
+  ``target_m`` (B, N) comes from cnn.forward_fused_c51.  Bitwise c51_loss_fused's loss,
+  gradient, priorities and d h.  Returns dict(grad, loss, priorities)."""
+  from dopamine_amd import cnn
+  B, NO = online.B, online.n_out
+  N = int(target_m.shape[-1])
+  A = NO // N
+  f32 = torch.float32
+  dev = target_m.device
+  if out is None:
+    out = dict(grad=torch.empty((B, A, N), dtype=f32, device=dev),
+               loss=torch.empty(B, dtype=f32, device=dev),
+               priorities=torch.empty(B, dtype=f32, device=dev))
+  po = cnn.fc2_parts(online)
+  _lib.call('dq_c51_loss_online', p(po), online._p.fc2_b, po.shape[0], p(target_m),
+            p(_c(actions, torch.int32)), p(probs if probs is None else _c(probs, f32)), B, A, N,
+            p(out['grad']), p(out['loss']), p(out['priorities']), online._p.fc2_w,
+            p(online.acts['h']), p(online.dacts['h']), 512,
+            p(online.acts['out']) if logits_out else None, _stream(target_m))
+  return out
+
+
 def dqn_huber_loss(online_q, target_q, actions, rewards, terminals, cumulative_gamma, out=None):
   """dqn_agent.py:283-322."""
   B, A = online_q.shape

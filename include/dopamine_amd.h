@@ -229,6 +229,16 @@ int dq_c51_loss(const float* online_logits, const float* target_logits, const in
                 float cumulative_gamma, float* grad_logits, float* loss_out,
                 float* priorities_out, float* mean_loss_out, void* stream);
 
+/* The online half of dq_c51_loss_fused (rainbow_agent.py:253-305: softmax cross-entropy of
+   the chosen online logits against the projected target distribution, PER weights, new
+   priorities, dlogits and d h) given target_m (B, num_atoms) from dq_cnn_forward_fused_c51;
+   loss, gradient, priorities and d h are bitwise dq_c51_loss_fused's. */
+int dq_c51_loss_online(const float* online_parts, const float* online_bias, int32_t n_parts,
+                       const float* target_m, const int32_t* actions, const float* probs,
+                       int32_t batch, int32_t num_actions, int32_t num_atoms, float* grad_logits,
+                       float* loss_out, float* priorities_out, const float* fc2_w, const float* h,
+                       float* dh, int32_t hidden, float* online_logits_out, void* stream);
+
 /* dq_c51_loss on the CNN's fc2 k-band partials (dq_cnn_forward_fused): logits = the n_parts
    partial slabs [n_parts][B][A*N] summed in order + bias (bitwise dq_cnn_forward's logits,
    written to *_logits_out when non-NULL); with fc2_w set it also writes the fc2 input
@@ -399,6 +409,29 @@ int dq_cnn_forward_fused(const dq_cnn_params* p0, const float* x0, dq_cnn_acts* 
                          const dq_cnn_params* p1, const float* x1, dq_cnn_acts* a1, float* ws1,
                          int32_t batch, int32_t fc1_1, void* stream);
 size_t dq_cnn_fc2_parts_offset(int32_t batch);
+/* The target network's half of the C51 loss (rainbow_agent.py:200-251 target softmax, Q,
+   greedy action, and project_distribution rainbow_agent.py:340-494) for the fused path. */
+typedef struct dq_c51_target {
+  const float* rewards;            /* (B,) n-step rewards of the batch */
+  const uint8_t* terminals;        /* (B,) */
+  const float* support;            /* (num_atoms,) linspace(-vmax, vmax) */
+  int32_t num_atoms;
+  float cumulative_gamma;          /* gamma^n as float32 (dqn_agent.py:175) */
+  float* m_out;                    /* (B, num_atoms) projected target distribution */
+  float* target_logits_out;        /* (B, n_out) or NULL */
+} dq_c51_target;
+/* dq_cnn_forward_fused with the target network one launch earlier (head_from = 8: its
+   conv1 rode in launch 5 of the previous backward, as for head_from = 6): net 1's conv2 in
+   net 0's conv1 launch, its conv3 in net 0's conv2 launch, its fc1 slabs in net 0's conv3
+   launch, its fused head in net 0's fc1 launch, and the target half of the C51 loss (one
+   block per sample) in net 0's fused-head launch -- the loss launch then runs only the
+   online half (dq_c51_loss_online), off the critical path's target chain.  flags: bit 2
+   only the conv launches, bit 3 only the fc launches (as dq_cnn_forward_fused).
+   num_actions = p1->n_out / num_atoms <= 16.  m_out is bitwise what dq_c51_loss_fused
+   forms internally. */
+int dq_cnn_forward_fused_c51(const dq_cnn_params* p0, const float* x0, dq_cnn_acts* a0, float* ws0,
+                             const dq_cnn_params* p1, dq_cnn_acts* a1, float* ws1, int32_t batch,
+                             const dq_c51_target* c51, int32_t flags, void* stream);
 /* one layer of the backward: layer 0..4 = fc2, fc1, conv3, conv2, conv1; part 1 = weight and
    bias gradient, part 0 = input gradient (not for conv1).  dW(L) depends only on dX(L-1),
    so the weight gradients may run on a second stream, each with its own ws. */

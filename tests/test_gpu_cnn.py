@@ -212,3 +212,30 @@ def test_fused_forward_and_c51_equal_separate_path(B, A):
     torch.cuda.synchronize()
     assert torch.equal(torch.cat([v.reshape(-1) for v in on.fp.grad_views]), g7), hf
     assert torch.equal(ht.acts['out'], ref_t2) and torch.equal(ho.acts['out'], ref_o), hf
+  # head_from = 8: the target net one launch ahead (conv1 in the backward as for 6) and
+  # the C51 loss split -- its target half riding beside the online fused head, the loss
+  # launch the online half: loss, gradient, priorities and d h bitwise the one kernel's
+  from dopamine_amd.cnn import forward_fused_c51
+  ho.dacts['h'].copy_(dh0)
+  ho.backward(got['grad'].view(B, -1), groups=(1, 7), head=(ht, nx2), head_from=6)
+  forward_fused(ho, x, ht, conv3_b=True, conv2_b=True)
+  ref6 = {k: v.clone() for k, v in ops.c51_loss_fused(ho, ht, act, rew, term, sup, 0.970299,
+                                                       probs=probs).items()}
+  dh6 = ho.dacts['h'].clone()
+  ho.dacts['h'].copy_(dh0)
+  on.fp.grad.fill_(float('nan'))
+  for t in (ht.acts['a1'], ht.acts['a2'], ht.acts['a3'], ht.acts['out']):
+    t.fill_(float('nan'))
+  ho.backward(got['grad'].view(B, -1), groups=(1, 7), head=(ht, nx2), head_from=6)
+  for t in (ht.acts['a2'], ht.acts['a3'], ho.acts['out'], ho.acts['h']):   # the forward's outputs
+    t.fill_(float('nan'))
+  m = torch.full((B, N), float('nan'), device='cuda')
+  forward_fused_c51(ho, x, ht, rew, term, sup, 0.970299, m, target_logits_out=ht.acts['out'])
+  got8 = ops.c51_loss_online(ho, m, act, probs=probs, logits_out=True)
+  torch.cuda.synchronize()
+  assert torch.equal(torch.cat([v.reshape(-1) for v in on.fp.grad_views]), g7)
+  assert torch.equal(ht.acts['out'], ref_t2) and torch.equal(ho.acts['out'], ref_o)
+  assert torch.equal(ho.acts['h'], ref_h)
+  for k in ('grad', 'loss', 'priorities'):
+    assert torch.equal(got8[k], ref6[k]), k
+  assert torch.equal(ho.dacts['h'], dh6)
