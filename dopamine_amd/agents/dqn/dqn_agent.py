@@ -591,6 +591,11 @@ class DQNAgent(object):
     head_b()
     ev = torch.cuda.Event()
     ev.record(main)
+    # the tail is issued (captured) before the comm branch, so in a captured graph it is the
+    # first child of the head's last launch and stays on that launch's hardware queue -- the
+    # all-reduce branch takes the other one (a fork to another queue costs ~10 us on the
+    # critical path, measured with the branch captured first)
+    tail()
     self._comm.wait_event(ev)
     # The fc bucket as _FC_PIECES all-reduces back to back on the comm stream; each
     # piece's Adam part runs on a second stream behind its own all-reduce, under the
@@ -609,7 +614,6 @@ class DQNAgent(object):
         with torch.cuda.stream(self._comm_opt):
           self._opt.step_part(grad, lo, hi, slot=k, bump=False)
         last = self._comm_opt
-    tail()
     if defer:
       parallel.allreduce_mean_(conv, self._conv_group())
       self._fc_pending = torch.cuda.Event()
