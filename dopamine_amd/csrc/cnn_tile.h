@@ -385,6 +385,18 @@ struct HasPre<EP, decltype((void)EP::kPre)> {
   static constexpr bool value = EP::kPre;
 };
 
+// EP::kVec: the epilogue takes 4 consecutive columns at a time (E.vec4(m, n, float4)),
+// so its loads and stores are 16 B per lane: igemm_block passes each wave's 32 x 32
+// accumulator tile through LDS (WK == 1 only; N % 4 == 0).
+template <class EP, class = void>
+struct HasVec {
+  static constexpr bool value = false;
+};
+template <class EP>
+struct HasVec<EP, decltype((void)EP::kVec)> {
+  static constexpr bool value = EP::kVec;
+};
+
 // host-side: EpiGrad, or EpiGradAdam with the moment slices of the same parameter
 struct AdamHost {
   const dq_adam_args* a;
@@ -654,6 +666,26 @@ __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& 
   }
   }
   // C/D layout of the 32x32 f32 MFMA: col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5)
+  if constexpr (HasVec<EP>::value) {
+    static_assert(WK == 1, "vector epilogues take whole tiles (WK == 1)");
+    // the wave's tile -> its own LDS window (rows padded to 33), then 8 lanes per row
+    // read 4 consecutive columns each: 16-B epilogue loads and stores, 8 rows per
+    // instruction.  The K loop's last barrier has freed the staging slices.
+    float* W = smem + wave * (32 * 33);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) W[((r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * 33 + (lane & 31)] = acc[r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int row = 8 * it + (lane >> 3), c = 4 * (lane & 7);
+      const float* q = W + row * 33 + c;
+      const int m = m0 + wm * 32 + row, n = n0 + wn * 32 + c;
+      if (m < M && n < N) E.vec4(m, n, make_float4(q[0], q[1], q[2], q[3]));
+    }
+    return;
+  }
   if (WK == 1) {
     const int n = n0 + wn * 32 + (lane & 31);
     if constexpr (HasPre<EP>::value) {      // all loads first, then updates + stores
@@ -723,7 +755,9 @@ __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& 
 template <int WM, int WN, int WK, class AL, class BL, class EP>
 __global__ __launch_bounds__(64 * WM * WN * WK) void k_igemm(AL A, BL B, EP E, int M, int N, int K,
                                                              int kchunk) {
-  __shared__ __attribute__((aligned(16))) float smem[Tile<WM, WN, WK>::template lds<AL, BL>()];
+  constexpr int kTile = Tile<WM, WN, WK>::template lds<AL, BL>();
+  constexpr int kVecW = HasVec<EP>::value ? WM * WN * WK * 32 * 33 : 0;   // vector epilogue windows
+  __shared__ __attribute__((aligned(16))) float smem[kTile > kVecW ? kTile : kVecW];
   igemm_block<WM, WN, WK>(A, B, E, M, N, K, kchunk, blockIdx.x, blockIdx.y, blockIdx.z, smem);
 }
 

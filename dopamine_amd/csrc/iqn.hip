@@ -52,11 +52,24 @@ struct EpiEmb {
   const float* bias;
   const float* state;
   int B;
+  static constexpr bool kVec = true;      // 4 columns per call: 16-B loads and stores
   __device__ __forceinline__ void operator()(int m, int n, float v, int) const {
     const float e = fmaxf(__fadd_rn(v, bias[n]), 0.0f);
     const int64_t i = (int64_t)m * F + n;
     if (emb) emb[i] = e;
     x[i] = __fmul_rn(state[(int64_t)(m % B) * F + n], e);
+  }
+  __device__ __forceinline__ void vec4(int m, int n, float4 v) const {
+    const float4 b = ld4(bias + n), s = ld4(state + (int64_t)(m % B) * F + n);
+    float4 e;
+    e.x = fmaxf(__fadd_rn(v.x, b.x), 0.0f);
+    e.y = fmaxf(__fadd_rn(v.y, b.y), 0.0f);
+    e.z = fmaxf(__fadd_rn(v.z, b.z), 0.0f);
+    e.w = fmaxf(__fadd_rn(v.w, b.w), 0.0f);
+    const int64_t i = (int64_t)m * F + n;
+    if (emb) *reinterpret_cast<float4*>(emb + i) = e;
+    *reinterpret_cast<float4*>(x + i) = make_float4(__fmul_rn(s.x, e.x), __fmul_rn(s.y, e.y),
+                                                    __fmul_rn(s.z, e.z), __fmul_rn(s.w, e.w));
   }
 };
 
@@ -67,11 +80,21 @@ struct EpiDx {
   const float* emb;
   const float* state;
   int B;
+  static constexpr bool kVec = true;
   __device__ __forceinline__ void operator()(int m, int n, float v, int) const {
     const int64_t i = (int64_t)m * F + n;
     const float e = emb[i];
     dtl[i] = __fmul_rn(v, e);
     dpre[i] = e > 0.0f ? __fmul_rn(v, state[(int64_t)(m % B) * F + n]) : 0.0f;
+  }
+  __device__ __forceinline__ void vec4(int m, int n, float4 v) const {
+    const int64_t i = (int64_t)m * F + n;
+    const float4 e = ld4(emb + i), s = ld4(state + (int64_t)(m % B) * F + n);
+    *reinterpret_cast<float4*>(dtl + i) =
+        make_float4(__fmul_rn(v.x, e.x), __fmul_rn(v.y, e.y), __fmul_rn(v.z, e.z), __fmul_rn(v.w, e.w));
+    *reinterpret_cast<float4*>(dpre + i) =
+        make_float4(e.x > 0.0f ? __fmul_rn(v.x, s.x) : 0.0f, e.y > 0.0f ? __fmul_rn(v.y, s.y) : 0.0f,
+                    e.z > 0.0f ? __fmul_rn(v.z, s.z) : 0.0f, e.w > 0.0f ? __fmul_rn(v.w, s.w) : 0.0f);
   }
 };
 

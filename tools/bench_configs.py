@@ -46,6 +46,10 @@ def measure(make, actions, steps, warmup=20):
 def main():
   steps = int(sys.argv[1]) if len(sys.argv) > 1 else 300
   which = sys.argv[2] if len(sys.argv) > 2 else 'all'
+  extra = {}
+  for a in sys.argv[3:]:            # agent keyword overrides, e.g. pipeline=0
+    k, v = a.split('=')
+    extra[k] = bool(int(v))
   dev = torch.device('cuda', 0)
   from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
   from dopamine_amd.agents.implicit_quantile.implicit_quantile_agent import ImplicitQuantileAgent
@@ -54,14 +58,14 @@ def main():
     res['dqn_pong'] = measure(lambda: DQNAgent(num_actions=6, min_replay_history=20000,
                                                update_period=4, target_update_period=8000,
                                                replay_capacity=1_000_000, batch_size=32,
-                                               device=dev), 6, steps)
+                                               device=dev, **extra), 6, steps)
   from dopamine_amd.agents.optimizers import AdamOptimizer
   if which in ('all', 'iqn_breakout'):
     res['iqn_breakout'] = measure(lambda: ImplicitQuantileAgent(   # implicit_quantile.gin
       num_actions=4, num_tau_samples=64, num_tau_prime_samples=64, num_quantile_samples=32,
       update_horizon=3, replay_scheme='uniform', min_replay_history=20000, update_period=4,
       target_update_period=8000, optimizer=AdamOptimizer(learning_rate=0.00005, epsilon=0.0003125),
-      replay_capacity=1_000_000, batch_size=64, device=dev), 4, max(steps // 3, 50))
+      replay_capacity=1_000_000, batch_size=64, device=dev, **extra), 4, max(steps // 3, 50))
   print(json.dumps(res))
 
 
