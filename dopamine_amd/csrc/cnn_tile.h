@@ -783,6 +783,32 @@ __global__ __launch_bounds__(256) void k_splitk_reduce(const float* ws, int spli
   splitk_sum(ws, splits, M, N, E, (int64_t)blockIdx.x * blockDim.x + threadIdx.x);
 }
 
+// the same sums 4 elements per thread with 16-B slab loads (M * N % 4 == 0); each element
+// still goes through the epilogue on its own, in the same slab order
+template <class EP>
+__global__ __launch_bounds__(256) void k_splitk_reduce4(const float* ws, int splits, int M, int N, EP E) {
+  const int64_t i = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+  const int64_t MN = (int64_t)M * N;
+  if (i >= MN) return;
+  float4 s = ld4(ws + i);
+  for (int z0 = 1; z0 < splits; z0 += 8) {
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = ld4(ws + (int64_t)min(z0 + u, splits - 1) * MN + i);
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (z0 + u < splits) {
+        s.x = __fadd_rn(s.x, v[u].x);
+        s.y = __fadd_rn(s.y, v[u].y);
+        s.z = __fadd_rn(s.z, v[u].z);
+        s.w = __fadd_rn(s.w, v[u].w);
+      }
+  }
+  const float r[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+  for (int u = 0; u < 4; ++u) E((int)((i + u) / N), (int)((i + u) % N), r[u], 0);
+}
+
 
 struct Ctx {
   hipStream_t s;
@@ -820,8 +846,12 @@ void gemm(Ctx& c, AL a, BL b, EP e, int M, int N, int K, int splits = 1) {
   hipLaunchKernelGGL((k_igemm<WM, WN, WK, AL, BL, EpiPartial>), dim3(gx, gy, nz), dim3(T), 0, c.s, a,
                      b, EpiPartial{c.ws, M, N}, M, N, K, kchunk);
   const int64_t total = (int64_t)M * N;
-  hipLaunchKernelGGL((k_splitk_reduce<EP>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                     c.s, c.ws, nz, M, N, e);
+  if (total % 4 == 0)
+    hipLaunchKernelGGL((k_splitk_reduce4<EP>), dim3((unsigned)((total / 4 + 255) / 256)), dim3(256),
+                       0, c.s, c.ws, nz, M, N, e);
+  else
+    hipLaunchKernelGGL((k_splitk_reduce<EP>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                       c.s, c.ws, nz, M, N, e);
 }
 
 
