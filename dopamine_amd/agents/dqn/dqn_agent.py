@@ -910,7 +910,8 @@ class DQNAgent(object):
       return False
     import torch.distributed as dist
     return (dist.get_backend(self._pg) == 'nccl' and self._split_allreduce() and
-            self._head_splits() and isinstance(self._opt, ops.TF1Adam))
+            self._head_splits() and isinstance(self._opt, ops.TF1Adam) and
+            parallel.collectives_capturable(self._pg, self._device, self._comm))
 
   def _chunks_apply(self):
     return (self._hip is not None and self.pipeline and

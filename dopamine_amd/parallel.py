@@ -41,3 +41,55 @@ def replicas_in_sync(flat_params, group=None):
   ok = torch.tensor([1.0 if torch.equal(s, ref) else 0.0], dtype=torch.float64, device=s.device)
   dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
   return bool(ok.item() == 1.0)
+
+
+_CAPTURABLE = {}
+
+
+def collectives_capturable(group, device, stream=None):
+  """Whether every rank of ``group`` can capture this backend's all-reduce into a HIP
+  graph and replay it correctly -- probed once per group on a small tensor, the ranks
+  agreeing (eager MIN all-reduces) after each phase so no rank replays a collective the
+  others did not capture.  False for gloo (host-side collectives).  The learner loop
+  captures its all-reduces only where this holds, else it replays per-step graphs with
+  the collectives issued between them."""
+  key = id(group)
+  if key in _CAPTURABLE:
+    return _CAPTURABLE[key]
+  if dist.get_backend(group) != 'nccl':
+    _CAPTURABLE[key] = False
+    return False
+
+  def agree(ok):
+    t = torch.tensor([1.0 if ok else 0.0], device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(t.item() == 1.0)
+
+  rank = dist.get_rank(group)
+  x = torch.full((1024,), float(rank + 1), device=device)
+  s = stream or torch.cuda.Stream(device)
+  g = torch.cuda.CUDAGraph()
+  ok = True
+  try:
+    allreduce_mean_(x, group)                     # the communicator is warm before capture
+    torch.cuda.synchronize(device)
+    s.wait_stream(torch.cuda.current_stream(device))
+    with torch.cuda.stream(s):
+      with torch.cuda.graph(g, stream=s, capture_error_mode='thread_local'):
+        allreduce_mean_(x, group)
+  except Exception:                               # noqa: BLE001 -- any failure means "no"
+    ok = False
+  ok = agree(ok)
+  if ok:
+    try:
+      x.fill_(float(rank + 1))
+      g.replay()
+      torch.cuda.synchronize(device)
+      world = dist.get_world_size(group)
+      want = sum(range(1, world + 1)) / world if (world > 1 or FORCE_COLLECTIVES) else 1.0
+      ok = bool(torch.allclose(x, torch.full_like(x, want)))
+    except Exception:                             # noqa: BLE001
+      ok = False
+    ok = agree(ok)
+  _CAPTURABLE[key] = ok
+  return ok

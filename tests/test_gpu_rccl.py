@@ -61,6 +61,13 @@ def test_rccl_one_rank_schedule_equals_single_learner_bitwise(rccl_group, loop):
   assert np.array_equal(flat, single)
 
 
+def test_collective_capture_probe(rccl_group):
+  """The probe that gates captured all-reduces in the learner loop says yes on RCCL."""
+  from dopamine_amd import parallel
+  parallel._CAPTURABLE.clear()
+  assert parallel.collectives_capturable(rccl_group, torch.device('cuda', 0))
+
+
 def test_allreduce_mean_over_rccl_is_identity_for_one_rank(rccl_group):
   from dopamine_amd import parallel
   x = torch.randn(4_278_891, device='cuda')
