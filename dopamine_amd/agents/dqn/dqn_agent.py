@@ -375,6 +375,17 @@ class DQNAgent(object):
     self._online_ready = on
     self._ptgt[c] = self._target_dict(tg)
 
+  # Empty launches inserted before the gather rider (the last recorded): 0 keeps the chain
+  # write-back -> sample -> gather in consecutive backward launches; k > 0 moves the gather
+  # k launches later (it must still precede the target head's first launch).
+  _GATHER_SHIFT = int(os.environ.get('DQ_GATHER_SHIFT', '0'))
+
+  def _place_riders(self, riders):
+    if not self._GATHER_SHIFT or not riders:
+      return riders
+    from dopamine_amd import _lib
+    return riders[:-1] + [_lib.Rider() for _ in range(self._GATHER_SHIFT)] + riders[-1:]
+
   def _forward_fused_c51(self, c, part=None):
     raise NotImplementedError
 
@@ -445,6 +456,7 @@ class DQNAgent(object):
       with self._replay.memory.recording() as riders:
         self._post_loss(self._pbuf[c])
         self._prefetch(1 - c)
+      riders = self._place_riders(riders)
       adam = self._opt if self._fused_opt() else None
       f = self._bwd_first()
       self._hip['online'].backward(g, riders=riders, adam=adam, slot=k, head=self._head,
@@ -501,6 +513,7 @@ class DQNAgent(object):
       with self._replay.memory.recording() as riders:
         self._post_loss(self._pbuf[c])
         self._prefetch(1 - c)
+      riders = self._place_riders(riders)
       n = self._SPLIT - f
       self._hip['online'].backward(g, groups=(f, self._SPLIT), riders=riders[:n])
       self._tail_riders = riders[n:] or None     # the fused path's gather rides in launch 3

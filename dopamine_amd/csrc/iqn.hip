@@ -30,7 +30,10 @@ using namespace dq::cnn;
 constexpr int F = 11 * 11 * 64;   // 7744, the torso's state vector
 constexpr int H = 512;
 constexpr int kSplitFc1 = 4;      // h = relu(x W1^T + b1): K = 7744, 4 slabs (R/128 x 4 tiles x 4)
-constexpr int kSplitW1 = 2;       // dW1: K = R
+#ifndef DQ_IQN_SPLIT_W1
+#define DQ_IQN_SPLIT_W1 2
+#endif
+constexpr int kSplitW1 = DQ_IQN_SPLIT_W1;   // dW1: K = R
 constexpr int kSplitWe = 8;       // dWe: K = R, 61 row tiles
 constexpr int kSplitW2 = 32;      // dW2: M = A, K = R
 
