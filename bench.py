@@ -167,8 +167,8 @@ def time_gather_large(agent, batch=1024, iters=50):
 def gather_traffic(batch):
   """HBM bytes per gather launch from the committed PMC passes (rocprofv3 --pmc
   FETCH_SIZE / WRITE_SIZE, calibrated as MI355X_MICROARCH.md prescribes;
-  tools/gather_traffic.py, profiles/r1_gather_traffic.json), or None."""
-  path = os.path.join(ROOT, 'profiles', 'r1_gather_traffic.json')
+  tools/gather_traffic.py, profiles/r2_gather_traffic.json), or None."""
+  path = os.path.join(ROOT, 'profiles', 'r2_gather_traffic.json')
   try:
     d = json.load(open(path))
     return round(float(d['traffic_bytes_per_launch'][str(batch)])), os.path.relpath(path, ROOT)
