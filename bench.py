@@ -13,6 +13,7 @@ gradient all-reduced over RCCL each step (weak scaling).
 """
 import argparse
 import ctypes
+import gc
 import json
 import os
 import platform
@@ -258,11 +259,17 @@ def main():
     else:   # the same calls, consecutive steps replayed K per HIP graph (learner-only loop)
       agent.train_gradient_steps(n)
 
-  # untimed: run until every graph the timed loop replays is captured (both step
-  # parities, the 4-step chunk graphs of both starting parities), whatever --warmup
-  # is, so a short timed window holds only steady-state steps; then the warmup
+  # No cyclic-garbage collection pass inside the timed window (a full pass over a torch
+  # process's objects takes milliseconds: one would dominate a short window).
+  gc.collect()
+  gc.disable()
+  # Untimed, whatever --warmup is: run until every graph the timed loop replays is captured
+  # (both step parities, the 4-step chunk graphs of both starting parities) and the device
+  # has been busy for at least MIN_PRE_STEPS steps before the window (its clocks ramp under
+  # load: a 20-step window after 5 warmup steps read 7% low); then the warmup.
+  MIN_PRE_STEPS = 100
   prime = 0
-  while not agent.graphs_primed() and prime < 200:
+  while ((not agent.graphs_primed() or prime + args.warmup < MIN_PRE_STEPS) and prime < 400):
     grad_steps(5)
     prime += 5
   grad_steps(args.warmup)
@@ -276,6 +283,7 @@ def main():
   if pg is not None:
     dist.barrier()
   elapsed = time.perf_counter() - t0
+  gc.enable()
   if pg is not None:
     t = torch.tensor([elapsed], dtype=torch.float64, device='cpu' if rehearse else dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
