@@ -805,8 +805,15 @@ __global__ __launch_bounds__(256) void k_splitk_reduce4(const float* ws, int spl
       }
   }
   const float r[4] = {s.x, s.y, s.z, s.w};
+  int m = (int)(i / N), n = (int)(i - (int64_t)m * N);   // one division, then step along the row
 #pragma unroll
-  for (int u = 0; u < 4; ++u) E((int)((i + u) / N), (int)((i + u) % N), r[u], 0);
+  for (int u = 0; u < 4; ++u) {
+    E(m, n, r[u], 0);
+    if (++n == N) {
+      n = 0;
+      ++m;
+    }
+  }
 }
 
 

@@ -139,8 +139,15 @@ void backward(Ctx& c, const dq_iqn_head* hp, const dq_iqn_head* hg, int B, int n
                 R, F, H);
   gemm<4, 4, 1>(c, ColK{d->dh, H}, ColKOnes{a->x, F}, EpiGrad{hg->fc1_w, hg->fc1_b, F}, H, F + 1,
                 R, kSplitW1);
-  gemm<4, 4, 1>(c, ColK{d->dpre, F}, ColKOnes{a->cos, E}, EpiGrad{hg->emb_w, hg->emb_b, E}, F,
-                E + 1, R, kSplitWe);
+#ifndef DQ_IQN_WE_NARROW
+#define DQ_IQN_WE_NARROW 0
+#endif
+  if (DQ_IQN_WE_NARROW)      // 128 x 32 tiles, K over 4 waves: 96 of 128 columns wasted -> 31
+    gemm<4, 1, 4>(c, ColK{d->dpre, F}, ColKOnes{a->cos, E}, EpiGrad{hg->emb_w, hg->emb_b, E}, F,
+                  E + 1, R, kSplitWe);
+  else
+    gemm<4, 4, 1>(c, ColK{d->dpre, F}, ColKOnes{a->cos, E}, EpiGrad{hg->emb_w, hg->emb_b, E}, F,
+                  E + 1, R, kSplitWe);
   if (!c.dry) {
     const int64_t n = (int64_t)B * F;
     hipLaunchKernelGGL(k_tile_grad, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c.s, d->dtl,
