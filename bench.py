@@ -177,6 +177,23 @@ def gather_traffic(batch):
     return None, None
 
 
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
+
+
+def step_mfma(actions, batch, sec_per_step):
+  """Algorithmic FLOPs of one Rainbow step's Nature-CNN work -- online forward + backward
+  (conv1's input gradient is never formed) + the target forward -- per second, against
+  the fp32 matrix peak."""
+  macs = [21 * 21 * 32 * 8 * 8 * 4, 11 * 11 * 64 * 4 * 4 * 32, 11 * 11 * 64 * 3 * 3 * 64,
+          7744 * 512, 512 * actions * 51]
+  fwd = 2 * sum(macs) * batch
+  bwd = 2 * (2 * sum(macs) - macs[0]) * batch
+  flops = 2 * fwd + bwd
+  achieved = flops / sec_per_step / 1e12
+  return {'flops_per_step': flops, 'achieved': round(achieved, 2), 'peak': FP32_MFMA_PEAK_TFLOPS,
+          'unit': 'TFLOP/s', 'frac': round(achieved / FP32_MFMA_PEAK_TFLOPS, 4)}
+
+
 def host_cores():
   """CPUs this process may run on: the affinity mask, capped by a cgroup CPU quota."""
   n = len(os.sched_getaffinity(0))
@@ -323,6 +340,9 @@ def main():
                      'algo_bytes_per_launch': algo_bytes,
                      'avg_launch_us': round(graph_us, 3), 'avg_launch_us_eager': round(eager_us, 3),
                      'same_kernel_batch_1024': large},
+        # supplementary: the whole step against the fp32 matrix peak (the CNN's fp32 MFMA
+        # work; the step is launch- and latency-bound at B = 32, not MFMA-bound)
+        'step_mfma': step_mfma(args.actions, args.batch, elapsed / args.steps),
         'cpu_baseline': cpu,
         'final_mean_loss': round(loss, 5),
     }
