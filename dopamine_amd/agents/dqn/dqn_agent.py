@@ -91,6 +91,7 @@ class DQNAgent(object):
                seed=0,
                process_group=None):
     assert num_actions is not None
+    assert isinstance(observation_shape, tuple)      # abstract_agent.py:34
     self.num_actions = num_actions
     self.observation_shape = tuple(observation_shape)
     self.observation_dtype = observation_dtype
@@ -811,10 +812,14 @@ class DQNAgent(object):
   def _q_values(self, state_np):
     if self._hip is not None and self.use_hip_graph:
       return self._act_q(state_np)
-    x = torch.as_tensor(state_np, dtype=torch.float32, device=self._device)
-    x = x.permute(0, 3, 1, 2) if x.dim() == 4 else x          # NHWC -> NCHW
+    # (1, *observation_shape, stack) -> (1, stack, *observation_shape): the layout the
+    # replay's gather hands the network in training (float32 / 255 for uint8 frames,
+    # the observation dtype otherwise; the network casts, as the reference's do)
+    s = np.moveaxis(np.asarray(state_np), -1, 1)
     if np.dtype(self.observation_dtype) == np.uint8:
-      x = x / 255.0
+      x = torch.as_tensor(s, dtype=torch.float32, device=self._device) / 255.0
+    else:
+      x = torch.as_tensor(s.astype(self.observation_dtype), device=self._device)
     with torch.no_grad():
       return self._online_q(self._state_input(x.contiguous()))
 

@@ -16,19 +16,45 @@ from dopamine_amd.agents.optimizers import AdamOptimizer
 from dopamine_amd.replay_memory import prioritized_replay_buffer
 
 
+class InvalidArgumentError(ValueError):
+  """Stands in for ``tf.errors.InvalidArgumentError``: a failed ``validate_args``
+  assertion (rainbow_agent.py:388-410).  Everything here is eager, so the
+  assertions fire at call time."""
+
+
 def project_distribution(supports, weights, target_support, validate_args=False):
   """rainbow_agent.py:340-494 as a torch expression (used for inspection and
-  by tests; the training path uses the fused HIP kernel)."""
+  by tests; the training path uses the fused HIP kernel).
+
+  Errors follow the reference: a 0-d target support fails its ``[1:]`` slice
+  ('Index out of range', rb:381), one with fewer than two rows fails ``deltas[0]``
+  ('out of bounds', rb:383), inconsistent supports / weights / target shapes fail
+  the static checks ('are incompatible', rb:385-387), and with ``validate_args`` a
+  non-increasing or unequally spaced target support raises InvalidArgumentError
+  ('assertion failed', rb:402-410)."""
   supports = torch.as_tensor(supports, dtype=torch.float32)
-  weights = torch.as_tensor(weights, dtype=torch.float32)
+  weights = torch.as_tensor(weights, dtype=torch.float32, device=supports.device)
   target_support = torch.as_tensor(target_support, dtype=torch.float32, device=supports.device)
+  if target_support.dim() == 0:
+    raise ValueError('Index out of range using input dim 0 of the target support')
   deltas = target_support[1:] - target_support[:-1]
+  if deltas.shape[0] == 0:
+    raise ValueError('slice index 0 of dimension 0 out of bounds (target support of shape %s)'
+                     % (tuple(target_support.shape),))
   delta_z = deltas[0]
+  if tuple(supports.shape) != tuple(weights.shape):
+    raise ValueError('Shapes %s and %s are incompatible' % (tuple(supports.shape),
+                                                            tuple(weights.shape)))
+  if tuple(supports.shape[1:]) != tuple(target_support.shape):
+    raise ValueError('Shapes %s and %s are incompatible' % (tuple(supports.shape[1:]),
+                                                            tuple(target_support.shape)))
+  if target_support.dim() != 1:
+    raise ValueError('Shape %s must have rank 1' % (tuple(target_support.shape),))
   if validate_args:
-    if supports.shape != weights.shape or supports.shape[1] != target_support.shape[0]:
-      raise ValueError('incompatible shapes')
-    if not bool((deltas > 0).all()) or not bool((deltas == delta_z).all()):
-      raise ValueError('target_support must be increasing and equally spaced')
+    if not bool((deltas > 0).all()):
+      raise InvalidArgumentError('assertion failed: target_support is not monotonically increasing')
+    if not bool((deltas == delta_z).all()):
+      raise InvalidArgumentError('assertion failed: target_support is not equally spaced')
   clipped = supports.clamp(target_support[0], target_support[-1])[:, None, :]
   quot = 1 - (clipped - target_support[None, :, None]).abs() / delta_z
   return (quot.clamp(0, 1) * weights[:, None, :]).sum(-1)
