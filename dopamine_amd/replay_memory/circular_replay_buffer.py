@@ -121,8 +121,9 @@ class OutOfGraphReplayBuffer(object):
     self._generic_reward = tuple(reward_shape) != () or np.dtype(reward_dtype) != np.float32
     if self._generic_reward and np.dtype(reward_dtype).name not in _lib.DT_CODES:
       raise NotImplementedError('reward_dtype {} is not supported'.format(np.dtype(reward_dtype)))
-    if np.dtype(terminal_dtype).itemsize != 1:
-      raise NotImplementedError('terminal_dtype must be a 1-byte type')
+    # the samplers test one byte per terminal flag; a wider terminal_dtype (e.g. np.int32,
+    # crb-test 83-90) keeps its stored values in a host mirror beside the device flags
+    self._wide_terminal = np.dtype(terminal_dtype).itemsize != 1
     self._action_shape = tuple(action_shape)
     self._action_dtype = action_dtype
     self._reward_shape = tuple(reward_shape)
@@ -159,6 +160,7 @@ class OutOfGraphReplayBuffer(object):
     self._actions = torch.zeros((C,), dtype=torch.int32, device=dev)
     self._rewards = torch.zeros((C,), dtype=torch.float32, device=dev)
     self._terminals = torch.zeros((C,), dtype=torch.uint8, device=dev)
+    self._term_host = np.zeros((C,), self._terminal_dtype) if self._wide_terminal else None
     self._meta = torch.zeros((16,), dtype=torch.int64, device=dev)
     self._tree = None
     self._extras = {}
@@ -308,7 +310,13 @@ class OutOfGraphReplayBuffer(object):
                            for r in rows])
     else:
       rew = np.array([r[2] for r in rows]).astype(np.float32)
-    term = np.array([r[3] for r in rows]).astype(self._terminal_dtype).view(np.uint8)
+    raw = np.array([r[3] for r in rows]).astype(self._terminal_dtype)
+    base = int(self.add_count)
+    if self._wide_terminal:
+      self._term_host[[(base + i) % self._replay_capacity for i in range(n)]] = raw
+      term = (raw != 0).astype(np.uint8)
+    else:
+      term = raw.view(np.uint8)
     prio = self._priority_column(rows)
     dev = self._device
     d_obs = torch.from_numpy(obs).to(dev, non_blocking=False)
@@ -316,7 +324,6 @@ class OutOfGraphReplayBuffer(object):
     d_rew = torch.from_numpy(rew).to(dev)
     d_term = torch.from_numpy(np.ascontiguousarray(term)).to(dev)
     d_prio = torch.from_numpy(prio).to(dev) if prio is not None else None
-    base = int(self.add_count)
     if self._extra_storage_types or self._generic_action or self._generic_reward:
       slots = torch.tensor([(base + i) % self._replay_capacity for i in range(n)], device=dev)
       if self._generic_action and act_rows.shape[1]:
@@ -329,7 +336,7 @@ class OutOfGraphReplayBuffer(object):
     _lib.call('dq_replay_add', self._h, n, _lib.ptr(d_obs), _lib.ptr(d_act), _lib.ptr(d_rew),
               _lib.ptr(d_term), _lib.ptr(d_prio), self._stream)
     self.add_count = np.array(base + n)
-    self._last_terminal = int(term[-1])
+    self._last_terminal = int(bool(raw[-1] == 1))    # crb:251 store['terminal'][cursor-1] == 1
     self.invalid_range = invalid_range(self.cursor(), self._replay_capacity,
                                        self._stack_size, self._update_horizon)
 
@@ -353,6 +360,8 @@ class OutOfGraphReplayBuffer(object):
     return np.moveaxis(frames, 0, -1)
 
   def get_terminal_stack(self, index):
+    if self._wide_terminal:
+      return self._term_host[self._stack_ids(index)]
     return self._terminals[self._stack_ids(index)].cpu().numpy().view(self._terminal_dtype)
 
   def is_valid_transition(self, index):
@@ -625,10 +634,14 @@ class OutOfGraphReplayBuffer(object):
     self._frames.copy_(torch.as_tensor(observations).reshape(C, self._obs_bytes))
     self._actions.copy_(torch.as_tensor(actions))
     self._rewards.copy_(torch.as_tensor(rewards))
-    self._terminals.copy_(torch.as_tensor(terminals))
+    terminals = torch.as_tensor(terminals)
+    if self._wide_terminal:
+      self._term_host[:] = terminals.cpu().numpy()
+      terminals = terminals != 0
+    self._terminals.copy_(terminals)
     self.add_count = np.array(int(add_count))
     self.invalid_range = invalid_range(self.cursor(), C, self._stack_size, self._update_horizon)
-    self._last_terminal = int(self._terminals[(self.cursor() - 1) % C].item())
+    self._last_terminal = self._terminal_is_one((self.cursor() - 1) % C)
     maxrec = 1.0
     if priorities is not None and self._prioritized:
       self._set_tree_leaves(priorities)
@@ -656,10 +669,22 @@ class OutOfGraphReplayBuffer(object):
     if self._generic_reward:
       rew = self._rew_store
     st = collections.OrderedDict([('observation', obs), ('action', act),
-                                  ('reward', rew), ('terminal', self._terminals)])
+                                  ('reward', rew), ('terminal', self._terminal_store())])
     for e in self._extra_storage_types:
       st[e.name] = self._extras[e.name]
     return st
+
+  def _terminal_store(self):
+    """The terminal store in terminal_dtype: a view of the device flags, or (wide types)
+    a CPU tensor sharing the host mirror, which _after_load pushes to the device."""
+    if self._wide_terminal:
+      return torch.from_numpy(self._term_host)
+    return self._terminals.view(_torch_dtype(self._terminal_dtype))
+
+  def _terminal_is_one(self, i):
+    if self._wide_terminal:
+      return int(bool(self._term_host[i] == 1))
+    return int(bool(self._terminal_store()[i].item() == 1))
 
   @property
   def _store(self):
@@ -740,7 +765,9 @@ class OutOfGraphReplayBuffer(object):
   def _after_load(self):
     """Re-derive the device control block from the loaded host state."""
     C = self._replay_capacity
-    self._last_terminal = int(self._terminals[(self.cursor() - 1) % C].item())
+    if self._wide_terminal:
+      self._terminals.copy_(torch.from_numpy(self._term_host != 0))
+    self._last_terminal = self._terminal_is_one((self.cursor() - 1) % C)
     _lib.call('dq_replay_set_meta', self._h, int(self.add_count), self._max_recorded_after_load(),
               self._stream)
 
