@@ -61,10 +61,11 @@ def load_gin_configs(gin_files, gin_bindings):
   gin_lite.parse_config_files_and_bindings(gin_files, bindings=gin_bindings, skip_unknown=False)
 
 
-# agent_name -> (agent class, the replay wrapper class whose bindings it honours)
-_AGENTS = {'dqn': (dqn_agent.DQNAgent, 'WrappedReplayBuffer'),
-           'rainbow': (rainbow_agent.RainbowAgent, 'WrappedPrioritizedReplayBuffer'),
-           'implicit_quantile': (implicit_quantile_agent.ImplicitQuantileAgent,
+# agent_name -> (module, class name, the replay wrapper class whose bindings it honours);
+# the class is looked up when the agent is created, as the reference's create_agent does
+_AGENTS = {'dqn': (dqn_agent, 'DQNAgent', 'WrappedReplayBuffer'),
+           'rainbow': (rainbow_agent, 'RainbowAgent', 'WrappedPrioritizedReplayBuffer'),
+           'implicit_quantile': (implicit_quantile_agent, 'ImplicitQuantileAgent',
                                  'WrappedPrioritizedReplayBuffer')}
 
 
@@ -72,10 +73,12 @@ def _agent_kwargs(agent_name):
   """Bindings of the agent's class and of the classes it derives from (gin fills a
   base class's unset constructor arguments the same way), plus the replay wrapper's
   replay_capacity / batch_size, which dopamine_amd's agents take directly."""
-  cls, wrapper = _AGENTS[agent_name]
+  module, name, wrapper = _AGENTS[agent_name]
+  cls = getattr(module, name)
   kwargs = {}
-  for klass in reversed(cls.__mro__[:-1]):       # base classes first, the agent last
-    kwargs.update(gin_lite.query(klass.__name__))
+  if isinstance(cls, type):                      # (not a stand-in callable)
+    for klass in reversed(cls.__mro__[:-1]):     # base classes first, the agent last
+      kwargs.update(gin_lite.query(klass.__name__))
   for w in ('WrappedReplayBuffer', wrapper):
     bound = gin_lite.query(w)
     kwargs.update({k: bound[k] for k in ('replay_capacity', 'batch_size') if k in bound})
@@ -114,9 +117,22 @@ _DEFAULTS = (('create_environment_fn', _no_atari), ('checkpoint_file_prefix', 'c
 class Runner(object):
   """Runs an agent in an environment for num_iterations train (+ eval) iterations."""
 
-  def __init__(self, base_dir, create_agent_fn, **kwargs):
+  def __init__(self, base_dir, create_agent_fn, *args, **kwargs):
+    """Runner(base_dir, create_agent_fn, create_environment_fn, checkpoint_file_prefix,
+    logging_file_prefix, log_every_n, num_iterations, training_steps, evaluation_steps,
+    max_steps_per_episode) -- the reference's parameters, positional or by name."""
     assert base_dir is not None
-    # precedence: defaults < Runner bindings < the subclass's own (TrainRunner.*) < kwargs
+    names = [n for n, _ in _DEFAULTS]
+    if len(args) > len(names):
+      raise TypeError('Runner takes at most {} positional arguments'.format(2 + len(names)))
+    for name, value in zip(names, args):
+      if name in kwargs:
+        raise TypeError("Runner got multiple values for argument '{}'".format(name))
+      kwargs[name] = value
+    unknown = sorted(set(kwargs) - set(names))
+    if unknown:
+      raise TypeError("Runner got an unexpected keyword argument '{}'".format(unknown[0]))
+    # precedence: defaults < Runner bindings < the subclass's own (TrainRunner.*) < arguments
     settings = dict(_DEFAULTS)
     for klass in dict.fromkeys((Runner, type(self))):
       settings.update(gin_lite.query(klass.__name__))

@@ -13,8 +13,12 @@ import pickle
 CHECKPOINT_DURATION = 4
 
 
-def get_latest_checkpoint_number(base_directory, sentinel_file_identifier='checkpoint'):
-  """Largest iteration with a completed checkpoint, or -1."""
+def get_latest_checkpoint_number(base_directory, override_number=None,
+                                 sentinel_file_identifier='checkpoint'):
+  """Largest iteration with a completed checkpoint, or -1 (none, or no such directory);
+  ``override_number`` (a gin-bindable override) is returned as is."""
+  if override_number is not None:
+    return override_number
   pattern = os.path.join(base_directory, 'sentinel_{}_complete.*'.format(sentinel_file_identifier))
   nums = []
   for f in glob.glob(pattern):
