@@ -46,7 +46,12 @@ MAX_TENSORS = 16
 class AdamArgs(ctypes.Structure):
   _fields_ = [('var', ctypes.c_void_p), ('m', ctypes.c_void_p), ('v', ctypes.c_void_p),
               ('state', ctypes.c_void_p), ('slot', ctypes.c_int32), ('lr', ctypes.c_float),
-              ('beta1', ctypes.c_float), ('beta2', ctypes.c_float), ('epsilon', ctypes.c_float)]
+              ('beta1', ctypes.c_float), ('beta2', ctypes.c_float), ('epsilon', ctypes.c_float),
+              ('kind', ctypes.c_int32), ('centered', ctypes.c_int32), ('mg', ctypes.c_void_p),
+              ('decay', ctypes.c_float), ('momentum', ctypes.c_float)]
+
+
+OPT_ADAM, OPT_RMSPROP = 0, 1
 
 
 class TensorList(ctypes.Structure):
@@ -131,6 +136,8 @@ SIGNATURES = {
                                      ctypes.POINTER(Rider)],
     'dq_c51_loss': [_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _F, _P, _P, _P, _P, _P],
     'dq_dqn_huber_loss': [_P, _P, _P, _P, _P, _I32, _I32, _F, _P, _P, _P, _P],
+    'dq_dqn_huber_loss_fused': [_P, _P, _P, _P, _I32, _P, _P, _P, _I32, _I32, _F, _P, _P, _P, _P,
+                                _P, _I32, _P, _P, _P],
     'dq_iqn_loss': [_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _F, _F, _P, _P, _P, _P],
     'dq_adam_tf1': [_P, _P, _P, _P, _P, _I32, _I64, _F, _F, _F, _F, _P],
     'dq_adam_tf1_part': [_P, _P, _P, _P, _P, _I32, _I64, _F, _F, _F, _F, _I32, _P],

@@ -290,15 +290,15 @@ class DQNAgent(object):
     return q, out['grad']
 
   def _fused_opt(self):
-    """fuse_optimizer + single replica + HIP CNN + TF1 Adam: the optimizer step
-    is spread over the backward's grouped launches (dq_cnn_backward_adam / _riders:
-    float4 Adam ops on each parameter range once its gradient is final, conv1's
+    """fuse_optimizer + single replica + HIP CNN + TF1 Adam or RMSProp: the optimizer
+    step is spread over the backward's grouped launches (dq_cnn_backward_adam / _riders:
+    float4 optimizer ops on each parameter range once its gradient is final, conv1's
     split-K sum applying it in its epilogue).  Bitwise identical to the separate
-    k_adam step and 3.5% faster on MI355X (5,500 vs 5,315 steps/s).  (Earlier
-    forms were slower: the whole update in the last launch -1.5%; Adam in every
-    gradient epilogue -12%, scalar RMW of 4M fc1 parameters.)"""
+    k_adam / k_rmsprop step and 3.5% faster on MI355X for Adam (5,500 vs 5,315
+    steps/s).  (Earlier forms were slower: the whole update in the last launch -1.5%;
+    Adam in every gradient epilogue -12%, scalar RMW of 4M fc1 parameters.)"""
     return (self.fuse_optimizer and self._hip is not None and self._pg is None and
-            isinstance(self._opt, ops.TF1Adam))
+            isinstance(self._opt, (ops.TF1Adam, ops.TF1RMSProp)))
 
   def _backward(self, y, g, k=0):
     if self._hip is not None:       # all gradients stored into the flat buffer
@@ -345,12 +345,18 @@ class DQNAgent(object):
 
   def _fused(self):
     """fused_head: the loss kernel consumes the CNN's fc2 k-band partials and writes
-    fc2's input gradient (cnn.forward_fused + a loss override of _fused_loss), so
-    the forward and the backward each lose a launch.  Rainbow/C51 only."""
-    return False
+    fc2's input gradient (cnn.forward_fused + _fused_loss), so the forward and the
+    backward each lose a launch (the Nature-CNN agents: DQN's Huber here, Rainbow's C51
+    in its subclass)."""
+    return self.fused_head and self._rides()
 
   def _fused_loss(self, t, c):
-    raise NotImplementedError
+    """_online_loss on the CNN's fc2 partials: Q / Q' summed in the loss kernel
+    (dq_dqn_huber_loss_fused), which also writes fc2's input gradient."""
+    out = ops.dqn_huber_loss_fused(self._hip['online'], self._hip['target'][c], t['action'],
+                                   t['reward'], t['terminal'], self.cumulative_gamma,
+                                   out=self._loss_out, q_out=self._trace is not None)
+    return None, out['grad']
 
   def _loss(self, t, c):
     """(output, d loss / d output) of step slot c, by the fused or the plain path."""
@@ -1014,7 +1020,10 @@ class DQNAgent(object):
   _loss_name = 'HuberLoss'
 
   def mean_loss(self):
-    """Mean loss of the last gradient step (the summary scalar, dqn:318-321)."""
+    """Mean loss of the last gradient step (the summary scalar, dqn:318-321); the fused
+    head's loss kernel leaves the mean to this call (it is not on the gradient path)."""
+    if self._fused():
+      return float(self._loss_out['loss'].double().mean().item())
     return float(self._loss_out['mean_loss'].item())
 
   def _record_observation(self, observation):

@@ -156,9 +156,6 @@ class RainbowAgent(dqn_agent.DQNAgent):
                        out=self._loss_out)
     return logits, out['grad']
 
-  def _fused(self):
-    return self.fused_head and self._rides()
-
   # The C51 loss split in two (head_from 8): the target half (softmax, Q, greedy action,
   # projection: rb:200-251, 340-494) rides in the online forward's last launch, the target
   # network running one launch ahead of the online one; the loss launch keeps the online

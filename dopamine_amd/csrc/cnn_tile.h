@@ -367,6 +367,56 @@ struct EpiGradAdam {
   }
 };
 
+// gradient + TF1 RMSProp in one pass (dq_rmsprop_tf1's arithmetic, rms1): m = ms,
+// v = mom, g2 = mg (centered only)
+struct RmsDev {
+  float lr, omr, mu, eps;
+  int centered;
+};
+__host__ inline RmsDev rms_dev(const dq_adam_args* a) {
+  // 1 - rho in host float32 arithmetic: the value k_rmsprop's __fsub_rn forms
+  return RmsDev{a->lr, 1.0f - a->decay, a->momentum, a->epsilon, a->centered != 0};
+}
+struct EpiGradRms {
+  float* gw;
+  float* gb;
+  int nw;
+  float *w, *mw, *vw, *gw2;   // parameter / ms / mom / mg slices at the same offsets as gw
+  float *b, *mb, *vb, *gb2;   // ... and as gb
+  RmsDev o;
+  static constexpr bool kPre = true;
+  struct Pre {
+    float w, m, v, g2;
+  };
+  __device__ __forceinline__ Pre pre(int m, int n) const {
+    if (n < nw) {
+      const int64_t i = (int64_t)m * nw + n;
+      return Pre{w[i], mw[i], vw[i], o.centered ? gw2[i] : 0.0f};
+    }
+    return Pre{b[m], mb[m], vb[m], o.centered ? gb2[m] : 0.0f};
+  }
+  __device__ __forceinline__ void commit(int m, int n, float g, Pre q) const {
+    rms1(q.w, g, q.m, q.g2, q.v, o.lr, o.omr, o.mu, o.eps, o.centered != 0);
+    if (n < nw) {
+      const int64_t i = (int64_t)m * nw + n;
+      gw[i] = g;
+      w[i] = q.w;
+      mw[i] = q.m;
+      vw[i] = q.v;
+      if (o.centered) gw2[i] = q.g2;
+    } else {
+      gb[m] = g;
+      b[m] = q.w;
+      mb[m] = q.m;
+      vb[m] = q.v;
+      if (o.centered) gb2[m] = q.g2;
+    }
+  }
+  __device__ __forceinline__ void operator()(int m, int n, float g, int) const {
+    commit(m, n, g, pre(m, n));
+  }
+};
+
 template <class EP, class = void>
 struct HasPf {
   static constexpr bool value = false;
@@ -397,26 +447,38 @@ struct HasVec<EP, decltype((void)EP::kVec)> {
   static constexpr bool value = EP::kVec;
 };
 
-// host-side: EpiGrad, or EpiGradAdam with the moment slices of the same parameter
+// host-side: EpiGrad, or EpiGradAdam / EpiGradRms with the optimizer slots of the same
+// parameter.  kOpt: 0 none, 1 TF1 Adam, 2 TF1 RMSProp (a compile-time choice, so each
+// optimizer's kernels are exactly its own code)
 struct AdamHost {
   const dq_adam_args* a;
 };
-template <bool kAdam>
+template <int kOpt>
 struct GradEpi;
 template <>
-struct GradEpi<false> {
+struct GradEpi<0> {
   static EpiGrad make(float* gw, float* gb, int nw, float*, float*, const AdamHost&, int) {
     return EpiGrad{gw, gb, nw};
   }
 };
 template <>
-struct GradEpi<true> {
+struct GradEpi<1> {
   static EpiGradAdam make(float* gw, float* gb, int nw, float* w, float* b, const AdamHost& h,
                           int bump) {
     const dq_adam_args* a = h.a;
     const ptrdiff_t ow = w - a->var, ob = b - a->var;
     return EpiGradAdam{gw, gb, nw, w, a->m + ow, a->v + ow, b, a->m + ob, a->v + ob,
                        AdamDev{a->state, a->slot, a->lr, a->beta1, a->beta2, a->epsilon}, bump};
+  }
+};
+template <>
+struct GradEpi<2> {
+  static EpiGradRms make(float* gw, float* gb, int nw, float* w, float* b, const AdamHost& h, int) {
+    const dq_adam_args* a = h.a;
+    const ptrdiff_t ow = w - a->var, ob = b - a->var;
+    float* mg = a->centered ? a->mg : a->m;    // never null: the (unused) loads stay valid
+    return EpiGradRms{gw, gb, nw, w, a->m + ow, a->v + ow, mg + ow,
+                      b, a->m + ob, a->v + ob, mg + ob, rms_dev(a)};
   }
 };
 

@@ -86,4 +86,21 @@ __device__ __forceinline__ void adam1(float& var, float g, float& m, float& v, f
   var = __fsub_rn(var, __fdiv_rn(__fmul_rn(m, alpha), __fadd_rn(__fsqrt_rn(v), eps)));
 }
 
+// ---- TF1 ApplyRMSProp / ApplyCenteredRMSProp (omr = 1 - rho), shared by k_rmsprop and
+// the fused CNN optimizer ops: ms += (g^2 - ms)(1 - rho); centered: mg += (g - mg)(1 - rho),
+// denom = ms - mg^2 + eps (else ms + eps); mom = mu mom + lr g / sqrt(denom); var -= mom.
+__device__ __forceinline__ void rms1(float& var, float g, float& ms, float& mg, float& mom,
+                                     float lr, float omr, float mu, float eps, bool centered) {
+  ms = __fadd_rn(ms, __fmul_rn(__fsub_rn(__fmul_rn(g, g), ms), omr));
+  float denom;
+  if (centered) {
+    mg = __fadd_rn(mg, __fmul_rn(__fsub_rn(g, mg), omr));
+    denom = __fadd_rn(__fsub_rn(ms, __fmul_rn(mg, mg)), eps);
+  } else {
+    denom = __fadd_rn(ms, eps);
+  }
+  mom = __fadd_rn(__fmul_rn(mom, mu), __fdiv_rn(__fmul_rn(g, lr), __fsqrt_rn(denom)));
+  var = __fsub_rn(var, mom);
+}
+
 }  // namespace dq

@@ -427,6 +427,64 @@ __global__ __launch_bounds__(256) void k_dqn(const float* oq, const float* tq, c
   }
 }
 
+// The fused DQN head (the DQN counterpart of k_c51<LogitsParts>): one 128-thread block
+// per sample b.  Q(s, .) and Q'(s', .) are fc2's 16 k-band partials summed in band
+// order plus the bias (bitwise dq_cnn_forward's outputs), the Bellman max target and
+// Huber(1) follow k_dqn operation for operation (the max in action order), and since
+// only the chosen action's output has a gradient, fc2's input gradient is one product
+// per element: d h[b][k] = (h[b][k] > 0) ? g * W2[a_b][k] : 0 -- exactly what the
+// backward's K = A GEMM forms (every other product is a zero).
+struct DqnFusedArgs {
+  LogitsParts ol, tl;
+  const int32_t* act;
+  const float* rew;
+  const uint8_t* term;
+  int B, A, H;
+  float cg;
+  float* grad;        // (B, A)
+  float* loss_out;    // (B,)
+  const float* w2;    // (A, H) online fc2 weights
+  const float* h;     // (B, H) online fc1 activation (ReLU mask)
+  float* dh;          // (B, H)
+  float* oq_out;      // (B, A) or NULL
+  float* tq_out;      // (B, A) or NULL
+};
+
+__global__ __launch_bounds__(128) void k_dqn_fused(DqnFusedArgs a) {
+  const int b = blockIdx.x, t = threadIdx.x, A = a.A, H = a.H;
+  const int ab = a.act[b];
+  // the d h operands first: they depend on the action only, not on the loss chain
+  const int k4 = 4 * t;
+  float4 w = make_float4(0.f, 0.f, 0.f, 0.f), hv = w;
+  if (k4 < H) {
+    w = *reinterpret_cast<const float4*>(a.w2 + (int64_t)ab * H + k4);
+    hv = *reinterpret_cast<const float4*>(a.h + (int64_t)b * H + k4);
+  }
+  const int j = t & 63;
+  const int64_t i = (int64_t)b * A + min(j, A - 1);
+  const float oq = a.ol.get(i), tq = a.tl.get(i);
+  const float r = a.rew[b], tm = (float)a.term[b];
+  float mx = rl(tq, 0);
+  for (int c = 1; c < A; ++c) mx = fmaxf(mx, rl(tq, c));
+  // r + cumulative_gamma * max_a Q' * (1 - terminal)   (dqn:298-299)
+  const float target = __fadd_rn(r, __fmul_rn(__fmul_rn(a.cg, mx), __fsub_rn(1.0f, tm)));
+  const float err = __fsub_rn(rl(oq, ab), target);       // predictions - labels
+  const float ae = fabsf(err);
+  const float quad = fminf(ae, 1.0f);
+  const float lin = __fsub_rn(ae, quad);
+  const float g = __fmul_rn(fminf(fmaxf(err, -1.0f), 1.0f), __fdiv_rn(1.0f, (float)a.B));
+  if (t < A) {
+    a.grad[(int64_t)b * A + t] = (t == ab) ? g : 0.0f;
+    if (a.oq_out) a.oq_out[(int64_t)b * A + t] = oq;
+    if (a.tq_out) a.tq_out[(int64_t)b * A + t] = tq;
+  }
+  if (t == 0 && a.loss_out) a.loss_out[b] = __fadd_rn(__fmul_rn(__fmul_rn(0.5f, quad), quad), lin);
+  if (k4 < H)
+    *reinterpret_cast<float4*>(a.dh + (int64_t)b * H + k4) =
+        make_float4(hv.x > 0.0f ? __fmul_rn(g, w.x) : 0.0f, hv.y > 0.0f ? __fmul_rn(g, w.y) : 0.0f,
+                    hv.z > 0.0f ? __fmul_rn(g, w.z) : 0.0f, hv.w > 0.0f ? __fmul_rn(g, w.w) : 0.0f);
+}
+
 // ---------------------------------------------------------------------------
 // IQN quantile-Huber.  One 64-thread block per sample b; lane = online quantile.
 // ---------------------------------------------------------------------------
@@ -586,20 +644,12 @@ __global__ __launch_bounds__(256) void k_rmsprop(float* var, const float* grad, 
   const float omr = __fsub_rn(1.0f, rho);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const float g = grad[i];
-    const float s = __fadd_rn(ms[i], __fmul_rn(__fsub_rn(__fmul_rn(g, g), ms[i]), omr));
+    float p = var[i], s = ms[i], a = centered ? mg[i] : 0.0f, mo = mom[i];
+    rms1(p, grad[i], s, a, mo, lr, omr, mu, eps, centered != 0);
     ms[i] = s;
-    float denom;
-    if (centered) {
-      const float a = __fadd_rn(mg[i], __fmul_rn(__fsub_rn(g, mg[i]), omr));
-      mg[i] = a;
-      denom = __fadd_rn(__fsub_rn(s, __fmul_rn(a, a)), eps);
-    } else {
-      denom = __fadd_rn(s, eps);
-    }
-    const float mo = __fadd_rn(__fmul_rn(mom[i], mu), __fdiv_rn(__fmul_rn(g, lr), __fsqrt_rn(denom)));
+    if (centered) mg[i] = a;
     mom[i] = mo;
-    var[i] = __fsub_rn(var[i], mo);
+    var[i] = p;
   }
 }
 
@@ -706,6 +756,29 @@ int dq_dqn_huber_loss(const float* online_q, const float* target_q, const int32_
                      actions, rewards, terminals, batch, num_actions, cumulative_gamma, grad_q,
                      loss_out, mean_loss_out);
   DQ_CHECK_LAUNCH("k_dqn");
+  return DQ_OK;
+}
+
+int dq_dqn_huber_loss_fused(const float* online_parts, const float* online_bias,
+                            const float* target_parts, const float* target_bias, int32_t n_parts,
+                            const int32_t* actions, const float* rewards,
+                            const uint8_t* terminals, int32_t batch, int32_t num_actions,
+                            float cumulative_gamma, float* grad_q, float* loss_out,
+                            const float* fc2_w, const float* h, float* dh, int32_t hidden,
+                            float* online_q_out, float* target_q_out, void* stream) {
+  DQ_CHECK_ARG(online_parts && online_bias && target_parts && target_bias && actions && rewards &&
+                   terminals && grad_q && fc2_w && h && dh,
+               "null argument");
+  DQ_CHECK_ARG(n_parts >= 1 && n_parts <= 16, "n_parts must be in [1, 16]");
+  DQ_CHECK_ARG(batch >= 1 && num_actions >= 1 && num_actions <= 64, "bad batch / num_actions");
+  DQ_CHECK_ARG(hidden >= 4 && hidden <= 512 && hidden % 4 == 0, "hidden must be a multiple of 4 <= 512");
+  const int64_t stride = (int64_t)batch * num_actions;
+  DqnFusedArgs a{LogitsParts{online_parts, online_bias, stride, n_parts, num_actions},
+                 LogitsParts{target_parts, target_bias, stride, n_parts, num_actions},
+                 actions, rewards, terminals, batch, num_actions, hidden, cumulative_gamma,
+                 grad_q, loss_out, fc2_w, h, dh, online_q_out, target_q_out};
+  hipLaunchKernelGGL(k_dqn_fused, dim3(batch), dim3(128), 0, (hipStream_t)stream, a);
+  DQ_CHECK_LAUNCH("k_dqn_fused");
   return DQ_OK;
 }
 

@@ -216,6 +216,86 @@ struct AdamOp {
   int blocks() const { return nb; }
 };
 
+// TF1 RMSProp (the arithmetic of dq_rmsprop_tf1) over a contiguous range, as AdamOp
+struct RmsOp {
+  static constexpr int kT = kGroupT;
+  static constexpr int kLds = 0;
+  float* var;
+  const float* grad;
+  float* ms;
+  float* mom;
+  float* mg;            // centered only (else any valid pointer)
+  int64_t n;
+  RmsDev o;
+  int nb;
+  static constexpr int kU = DQ_ADAM_U;
+  __device__ __forceinline__ void run(int blk, float*) const {
+    const bool c = o.centered != 0;
+    const int64_t n4 = n >> 2, stride = (int64_t)nb * kT * kU;
+    for (int64_t i0 = (int64_t)blk * kT * kU + threadIdx.x; i0 < n4; i0 += stride) {
+      float4 p[kU], g[kU], s[kU], mo[kU], a[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int64_t i = min(i0 + (int64_t)u * kT, n4 - 1);   // clamped: loads never branch
+        p[u] = reinterpret_cast<float4*>(var)[i];
+        g[u] = reinterpret_cast<const float4*>(grad)[i];
+        s[u] = reinterpret_cast<float4*>(ms)[i];
+        mo[u] = reinterpret_cast<float4*>(mom)[i];
+        a[u] = c ? reinterpret_cast<float4*>(mg)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int64_t i = i0 + (int64_t)u * kT;
+        if (i >= n4) break;
+        rms1(p[u].x, g[u].x, s[u].x, a[u].x, mo[u].x, o.lr, o.omr, o.mu, o.eps, c);
+        rms1(p[u].y, g[u].y, s[u].y, a[u].y, mo[u].y, o.lr, o.omr, o.mu, o.eps, c);
+        rms1(p[u].z, g[u].z, s[u].z, a[u].z, mo[u].z, o.lr, o.omr, o.mu, o.eps, c);
+        rms1(p[u].w, g[u].w, s[u].w, a[u].w, mo[u].w, o.lr, o.omr, o.mu, o.eps, c);
+        reinterpret_cast<float4*>(var)[i] = p[u];
+        reinterpret_cast<float4*>(ms)[i] = s[u];
+        reinterpret_cast<float4*>(mom)[i] = mo[u];
+        if (c) reinterpret_cast<float4*>(mg)[i] = a[u];
+      }
+    }
+    if (blk == 0 && threadIdx.x < (n & 3)) {
+      const int64_t i = (n4 << 2) + threadIdx.x;
+      float q = c ? mg[i] : 0.0f;
+      rms1(var[i], grad[i], ms[i], q, mom[i], o.lr, o.omr, o.mu, o.eps, c);
+      if (c) mg[i] = q;
+    }
+  }
+  int blocks() const { return nb; }
+};
+
+// the fused optimizer's range op (kOpt 1: AdamOp, 2: RmsOp) over [w0, w1) of the flat buffer
+template <int kOpt>
+struct OptPart;
+template <>
+struct OptPart<1> {
+  static AdamOp make(const dq_cnn_params* p, const dq_cnn_params* g, const dq_adam_args* o,
+                     float* w0, float* w1) {
+    const ptrdiff_t off = w0 - o->var;
+    const int64_t n = (int64_t)(w1 - w0);
+    const int64_t per = (int64_t)kGroupT * AdamOp::kU;
+    const int nb = (int)std::max<int64_t>(1, ((n >> 2) + per - 1) / per);
+    const AdamDev od{o->state, o->slot, o->lr, o->beta1, o->beta2, o->epsilon};
+    return AdamOp{w0, g->conv1_w + (w0 - p->conv1_w), o->m + off, o->v + off, n, od, nb};
+  }
+};
+template <>
+struct OptPart<2> {
+  static RmsOp make(const dq_cnn_params* p, const dq_cnn_params* g, const dq_adam_args* o,
+                    float* w0, float* w1) {
+    const ptrdiff_t off = w0 - o->var;
+    const int64_t n = (int64_t)(w1 - w0);
+    const int64_t per = (int64_t)kGroupT * RmsOp::kU;
+    const int nb = (int)std::max<int64_t>(1, ((n >> 2) + per - 1) / per);
+    float* mg = o->centered ? o->mg : o->m;
+    return RmsOp{w0, g->conv1_w + (w0 - p->conv1_w), o->m + off, o->v + off, mg + off, n,
+                 rms_dev(o), nb};
+  }
+};
+
 // A recorded replay operation (replay_dev.h) riding in a grouped launch: its
 // blocks come first in the launch so the single-wave sum-tree update / sampler
 // chains start before the GEMM blocks fill the machine.
@@ -593,7 +673,8 @@ bool backward_layer(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int 
 // or, kHeadFrom = 5, in 6 (the Rainbow fast path starts at 1, dh coming from the loss):
 //   4: sum conv3 slabs | dW conv2 slabs | dW conv1 slabs       [+ Adam fc1, 2nd third]
 //   5: sum conv2 slabs | sum conv1 slabs               [+ Adam fc1, 3rd third, conv3]
-// With kAdam the TF1 Adam step is spread as bracketed: float4 AdamOps over ranges
+// With kOpt (1 TF1 Adam, 2 TF1 RMSProp) the optimizer step is spread as bracketed: float4
+// AdamOps / RmsOps over ranges
 // whose gradients are final and whose weights have had their last read; conv1's
 // split-K sum applies it in its epilogue (and advances the beta powers).  The
 // optimizer's 47 MB of traffic then overlaps the latency-bound GEMM launches
@@ -605,14 +686,14 @@ bool backward_layer(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int 
 // forward_fused; 5: conv1, conv2 in launches 4, 5 of the six-launch schedule, conv3
 // and the fc1 slabs left to forward_fused).  Riders are numbered from launch `first`: rider i rides in launch
 // first + i.
-template <bool kAdam, int kHeadFrom = 3>
+template <int kOpt, int kHeadFrom = 3>
 void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int B,
                       const float* x, const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d,
                       const AdamHost& opt, int first = 0, int last = 7,
                       const RiderDesc* riders = nullptr, int n_riders = 0,
                       const FwdOps* head = nullptr) {
   const int NO = p->n_out;
-  using GE = GradEpi<kAdam>;
+  using GE = GradEpi<kOpt>;
   using W16 = Tile<1, 1, 16>;
   // workspace regions (ops of one launch never share one)
   const int K3 = B * 121, K1 = B * 441;
@@ -656,20 +737,12 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
   auto rd = [&](int i) {   // rider of launch i
     return i >= first && i - first < n_riders ? riders + (i - first) : nullptr;
   };
-  if constexpr (kAdam) {
+  if constexpr (kOpt != 0) {
     {
       // The optimizer spread over the launches after each gradient is final (fc2 after
       // launch 2, fc1 after launch 3) and each weight's last read: fc2 rides in launch 3,
       // fc1 in thirds in launches 4-6, conv2..conv3 with conv1's epilogue in launch 7.
-      const dq_adam_args* o = opt.a;
-      const AdamDev od{o->state, o->slot, o->lr, o->beta1, o->beta2, o->epsilon};
-      auto part = [&](float* w0, float* w1) {
-        const ptrdiff_t off = w0 - o->var;
-        const int64_t n = (int64_t)(w1 - w0);
-        const int64_t per = (int64_t)kGroupT * AdamOp::kU;
-        const int nb = (int)std::max<int64_t>(1, ((n >> 2) + per - 1) / per);
-        return AdamOp{w0, g->conv1_w + (w0 - p->conv1_w), o->m + off, o->v + off, n, od, nb};
-      };
+      auto part = [&](float* w0, float* w1) { return OptPart<kOpt>::make(p, g, opt.a, w0, w1); };
       float* f0 = p->fc1_w;
       float* f3 = p->fc2_w;                          // fc1_w .. fc1_b (+ pad)
 #ifndef DQ_FC1_A      // fc1's Adam split points, in 24ths of the range
@@ -786,6 +859,25 @@ if constexpr (kHeadFrom == 4) {
   if (in(6)) group_r(c, rd(6), sum_c1);
 }
 
+// backward_grouped with the runtime head_from (7: the whole target head runs in the next
+// forward, so the five-launch schedule carries none of it)
+template <int kOpt>
+void backward_head_from(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int B,
+                        const float* x, const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d,
+                        const AdamHost& opt, int first, int last, const RiderDesc* r, int n_riders,
+                        const FwdOps* hp, int head_from) {
+  if (head_from == 7)
+    backward_grouped<kOpt, 5>(c, p, g, B, x, a, dout, d, opt, first, last, r, n_riders, nullptr);
+  else if (head_from == 6)
+    backward_grouped<kOpt, 6>(c, p, g, B, x, a, dout, d, opt, first, last, r, n_riders, hp);
+  else if (head_from == 5)
+    backward_grouped<kOpt, 5>(c, p, g, B, x, a, dout, d, opt, first, last, r, n_riders, hp);
+  else if (head_from == 4)
+    backward_grouped<kOpt, 4>(c, p, g, B, x, a, dout, d, opt, first, last, r, n_riders, hp);
+  else
+    backward_grouped<kOpt>(c, p, g, B, x, a, dout, d, opt, first, last, r, n_riders, hp);
+}
+
 }  // namespace cnn
 }  // namespace dq
 
@@ -795,8 +887,13 @@ using namespace dq::cnn;
 // the fused optimizer needs the parameters (and gradients) in one flat buffer, in
 // conv1..fc2 order, with the float4 Adam range 16-byte aligned
 static int check_adam(const dq_cnn_params* p, const dq_cnn_params* g, const dq_adam_args* opt) {
-  DQ_CHECK_ARG(opt->var && opt->m && opt->v && opt->state && (opt->slot == 0 || opt->slot == 1),
-               "adam args: var, m, v, state and slot 0/1 required");
+  DQ_CHECK_ARG(opt->kind == DQ_OPT_ADAM || opt->kind == DQ_OPT_RMSPROP, "unknown optimizer kind");
+  if (opt->kind == DQ_OPT_ADAM)
+    DQ_CHECK_ARG(opt->var && opt->m && opt->v && opt->state && (opt->slot == 0 || opt->slot == 1),
+                 "adam args: var, m, v, state and slot 0/1 required");
+  else
+    DQ_CHECK_ARG(opt->var && opt->m && opt->v && (!opt->centered || opt->mg),
+                 "rmsprop args: var, ms (m), mom (v) and, centered, mg required");
   const float* w[10] = {p->conv1_w, p->conv1_b, p->conv2_w, p->conv2_b, p->conv3_w,
                         p->conv3_b, p->fc1_w,  p->fc1_b,  p->fc2_w,  p->fc2_b};
   const float* gw[10] = {g->conv1_w, g->conv1_b, g->conv2_w, g->conv2_b, g->conv3_w,
@@ -911,7 +1008,7 @@ int dq_cnn_backward(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batc
   DQ_CHECK_ARG(p && g && a && d && x && dout && ws && batch >= 1, "null argument");
   DQ_CHECK_ARG(p->in_channels == 4 && p->n_out >= 1, "the Nature CNN takes 84x84x4 NHWC input");
   Ctx c{(hipStream_t)stream, ws, false, 0};
-  backward_grouped<false>(c, p, g, batch, x, a, dout, d, AdamHost{nullptr});
+  backward_grouped<0>(c, p, g, batch, x, a, dout, d, AdamHost{nullptr});
   DQ_CHECK_LAUNCH("dq_cnn_backward");
   return DQ_OK;
 }
@@ -924,7 +1021,10 @@ int dq_cnn_backward_adam(const dq_cnn_params* p, const dq_cnn_params* g, int32_t
   const int rc = check_adam(p, g, opt);
   if (rc != DQ_OK) return rc;
   Ctx c{(hipStream_t)stream, ws, false, 0};
-  backward_grouped<true>(c, p, g, batch, x, a, dout, d, AdamHost{opt});
+  if (opt->kind == DQ_OPT_RMSPROP)
+    backward_grouped<2>(c, p, g, batch, x, a, dout, d, AdamHost{opt});
+  else
+    backward_grouped<1>(c, p, g, batch, x, a, dout, d, AdamHost{opt});
   DQ_CHECK_LAUNCH("dq_cnn_backward_adam");
   return DQ_OK;
 }
@@ -936,7 +1036,7 @@ int dq_cnn_backward_groups(const dq_cnn_params* p, const dq_cnn_params* g, int32
   DQ_CHECK_ARG(p->in_channels == 4 && p->n_out >= 1, "the Nature CNN takes 84x84x4 NHWC input");
   DQ_CHECK_ARG(0 <= first && first <= last && last <= 7, "groups must satisfy 0 <= first <= last <= 7");
   Ctx c{(hipStream_t)stream, ws, false, 0};
-  backward_grouped<false>(c, p, g, batch, x, a, dout, d, AdamHost{nullptr}, first, last);
+  backward_grouped<0>(c, p, g, batch, x, a, dout, d, AdamHost{nullptr}, first, last);
   DQ_CHECK_LAUNCH("dq_cnn_backward_groups");
   return DQ_OK;
 }
@@ -970,37 +1070,15 @@ int dq_cnn_backward_riders(const dq_cnn_params* p, const dq_cnn_params* g, int32
   if (opt) {
     const int rc = check_adam(p, g, opt);
     if (rc != DQ_OK) return rc;
-    if (head_from == 7)       // the whole target head runs in the next forward
-      backward_grouped<true, 5>(c, p, g, batch, x, a, dout, d, AdamHost{opt}, first, last, r,
-                                n_riders, nullptr);
-    else if (head_from == 6)
-      backward_grouped<true, 6>(c, p, g, batch, x, a, dout, d, AdamHost{opt}, first, last, r,
-                                n_riders, hp);
-    else if (head_from == 5)
-      backward_grouped<true, 5>(c, p, g, batch, x, a, dout, d, AdamHost{opt}, first, last, r,
-                                n_riders, hp);
-    else if (head_from == 4)
-      backward_grouped<true, 4>(c, p, g, batch, x, a, dout, d, AdamHost{opt}, first, last, r,
-                                n_riders, hp);
+    if (opt->kind == DQ_OPT_RMSPROP)
+      backward_head_from<2>(c, p, g, batch, x, a, dout, d, AdamHost{opt}, first, last, r, n_riders,
+                            hp, head_from);
     else
-      backward_grouped<true>(c, p, g, batch, x, a, dout, d, AdamHost{opt}, first, last, r,
-                             n_riders, hp);
+      backward_head_from<1>(c, p, g, batch, x, a, dout, d, AdamHost{opt}, first, last, r, n_riders,
+                            hp, head_from);
   } else {
-    if (head_from == 7)
-      backward_grouped<false, 5>(c, p, g, batch, x, a, dout, d, AdamHost{nullptr}, first, last, r,
-                                 n_riders, nullptr);
-    else if (head_from == 6)
-      backward_grouped<false, 6>(c, p, g, batch, x, a, dout, d, AdamHost{nullptr}, first, last, r,
-                                 n_riders, hp);
-    else if (head_from == 5)
-      backward_grouped<false, 5>(c, p, g, batch, x, a, dout, d, AdamHost{nullptr}, first, last, r,
-                                 n_riders, hp);
-    else if (head_from == 4)
-      backward_grouped<false, 4>(c, p, g, batch, x, a, dout, d, AdamHost{nullptr}, first, last, r,
-                                 n_riders, hp);
-    else
-      backward_grouped<false>(c, p, g, batch, x, a, dout, d, AdamHost{nullptr}, first, last, r,
-                              n_riders, hp);
+    backward_head_from<0>(c, p, g, batch, x, a, dout, d, AdamHost{nullptr}, first, last, r,
+                          n_riders, hp, head_from);
   }
   DQ_CHECK_LAUNCH("dq_cnn_backward_riders");
   return DQ_OK;
@@ -1062,7 +1140,7 @@ size_t dq_cnn_workspace_floats(int32_t batch, int32_t n_out) {
       need = l.need > need ? l.need : need;
     }
   Ctx g{nullptr, nullptr, true, 0};
-  backward_grouped<false>(g, &p, &p, batch, nullptr, &a, nullptr, &a, AdamHost{nullptr});
+  backward_grouped<0>(g, &p, &p, batch, nullptr, &a, nullptr, &a, AdamHost{nullptr});
   need = g.need > need ? g.need : need;
   Ctx f0{nullptr, nullptr, true, 0}, f1{nullptr, nullptr, true, 0};
   forward_fused(f0, f1, FwdOps{&p, nullptr, &a, nullptr, batch}, FwdOps{&p, nullptr, &a, nullptr, batch},

@@ -105,6 +105,30 @@ def dqn_huber_loss(online_q, target_q, actions, rewards, terminals, cumulative_g
   return out
 
 
+def dqn_huber_loss_fused(online, target, actions, rewards, terminals, cumulative_gamma, out=None,
+                         q_out=False):
+  """dqn_huber_loss on the HIP CNN's fc2 k-band partials (cnn.forward_fused) of the
+  online and target executors: Q and Q' are summed inside the loss kernel, which also
+  writes fc2's input gradient into ``online.dacts['h']`` (bitwise the backward's launch
+  0), so ``online.backward(..., groups=(1, 7))`` starts at launch 1.  q_out: also store
+  both nets' outputs in their ``acts['out']``.  Returns dict(grad, loss)."""
+  from dopamine_amd import cnn
+  B, A = online.B, online.n_out
+  f32 = torch.float32
+  dev = rewards.device
+  if out is None:
+    out = dict(grad=torch.empty((B, A), dtype=f32, device=dev),
+               loss=torch.empty(B, dtype=f32, device=dev))
+  po, pt = cnn.fc2_parts(online), cnn.fc2_parts(target)
+  _lib.call('dq_dqn_huber_loss_fused', p(po), online._p.fc2_b, p(pt), target._p.fc2_b,
+            po.shape[0], p(_c(actions, torch.int32)), p(_c(rewards, f32)),
+            p(_c(terminals, torch.uint8)), B, A, float(cumulative_gamma), p(out['grad']),
+            p(out['loss']), online._p.fc2_w, p(online.acts['h']), p(online.dacts['h']), 512,
+            p(online.acts['out']) if q_out else None, p(target.acts['out']) if q_out else None,
+            _stream(rewards))
+  return out
+
+
 def iqn_loss(online_qv, target_qv, target_qv_action, taus, actions, rewards, terminals,
              cumulative_gamma, kappa=1.0, out=None):
   """implicit_quantile_agent.py:190-321 (rows ordered q*B + b)."""

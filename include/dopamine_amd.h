@@ -257,6 +257,20 @@ int dq_dqn_huber_loss(const float* online_q, const float* target_q, const int32_
                       const float* rewards, const uint8_t* terminals, int32_t batch,
                       int32_t num_actions, float cumulative_gamma, float* grad_q,
                       float* loss_out, float* mean_loss_out, void* stream);
+/* dq_dqn_huber_loss on the CNN's fc2 k-band partials (dq_cnn_forward_fused), the DQN fast
+   path (dqn_agent.py:283-322): Q / Q' = the n_parts partial slabs [n_parts][B][A] summed in
+   order + bias (bitwise dq_cnn_forward's outputs, written to *_q_out when non-NULL); target,
+   loss and gradient bitwise dq_dqn_huber_loss's; also writes the fc2 input gradient
+   dh = (grad_q . fc2_w) * (h > 0), (B, hidden), bitwise the backward's launch 0, so the CNN
+   backward starts at its launch 1.  num_actions <= 64, hidden <= 512 and a multiple of 4.
+   The mean-loss summary is not produced here. */
+int dq_dqn_huber_loss_fused(const float* online_parts, const float* online_bias,
+                            const float* target_parts, const float* target_bias, int32_t n_parts,
+                            const int32_t* actions, const float* rewards,
+                            const uint8_t* terminals, int32_t batch, int32_t num_actions,
+                            float cumulative_gamma, float* grad_q, float* loss_out,
+                            const float* fc2_w, const float* h, float* dh, int32_t hidden,
+                            float* online_q_out, float* target_q_out, void* stream);
 
 /* IQN quantile-Huber loss (implicit_quantile_agent.py:190-321).  Row order of
  * the tiled tensors is q*B + b (atari_lib.py:174).  grad (N*B, A) fully written. */
@@ -333,14 +347,22 @@ int dq_cnn_forward_pair(const dq_cnn_params* p0, const float* x0, dq_cnn_acts* a
 int dq_cnn_backward(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch, const float* x,
                     const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d, float* ws,
                     void* stream);
-/* TF1 Adam (as dq_adam_tf1) applied inside the backward's gradient epilogues. */
+/* The optimizer applied inside the backward's grouped launches: TF1 Adam (as dq_adam_tf1,
+   kind DQ_OPT_ADAM -- a zero-initialised tail) or TF1 RMSProp (as dq_rmsprop_tf1, kind
+   DQ_OPT_RMSPROP: the gin-bound optimizer of dqn.gin:19-25). */
+#define DQ_OPT_ADAM 0
+#define DQ_OPT_RMSPROP 1
 typedef struct dq_adam_args {
   float* var;        /* flat parameter buffer the dq_cnn_params pointers point into */
-  float* m;          /* moments, same layout as var */
-  float* v;
-  float* state;      /* {beta1^t, beta2^t} x 2 slots, as dq_adam_tf1 */
-  int32_t slot;      /* step parity: reads state slot, writes the other */
+  float* m;          /* Adam: moments, same layout as var; RMSProp: m = ms (the rms slot), */
+  float* v;          /*   v = mom (the momentum slot) */
+  float* state;      /* Adam: {beta1^t, beta2^t} x 2 slots, as dq_adam_tf1 */
+  int32_t slot;      /* Adam: step parity: reads state slot, writes the other */
   float lr, beta1, beta2, epsilon;
+  int32_t kind;      /* DQ_OPT_ADAM / DQ_OPT_RMSPROP */
+  int32_t centered;  /* RMSProp: ApplyCenteredRMSProp (reads / writes mg) */
+  float* mg;         /* RMSProp, centered: the mean-gradient slot, same layout as var */
+  float decay, momentum;   /* RMSProp: rho, mu */
 } dq_adam_args;
 /* backward + optimizer step in one pass (single-replica training: no gradient
    all-reduce between them).  Gradients are still written to g. */

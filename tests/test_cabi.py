@@ -35,12 +35,12 @@ def test_struct_layouts_match_c():
 #include <stddef.h>
 #include "dopamine_amd.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(dq_replay_meta),
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(dq_replay_meta),
          sizeof(dq_replay_config), sizeof(dq_replay_storage), offsetof(dq_replay_meta, status),
          offsetof(dq_replay_config, gamma), offsetof(dq_replay_storage, discount),
          sizeof(dq_adam_args), offsetof(dq_adam_args, epsilon), sizeof(dq_iqn_head),
          offsetof(dq_iqn_head, fc2_b), sizeof(dq_iqn_acts), sizeof(dq_iqn_grads),
-         sizeof(dq_cnn_params));
+         sizeof(dq_cnn_params), offsetof(dq_adam_args, mg), offsetof(dq_adam_args, momentum));
   return 0;
 }
 '''
@@ -54,7 +54,7 @@ int main(void) {
          _lib.Meta.status.offset, _lib.Config.gamma.offset, _lib.Storage.discount.offset,
          ctypes.sizeof(_lib.AdamArgs), _lib.AdamArgs.epsilon.offset, ctypes.sizeof(_lib.IqnHead),
          _lib.IqnHead.fc2_b.offset, ctypes.sizeof(_lib.IqnActs), ctypes.sizeof(_lib.IqnGrads),
-         ctypes.sizeof(_lib.CnnParams)]
+         ctypes.sizeof(_lib.CnnParams), _lib.AdamArgs.mg.offset, _lib.AdamArgs.momentum.offset]
   assert got == exp
 
 

@@ -239,3 +239,82 @@ def test_fused_forward_and_c51_equal_separate_path(B, A):
   for k in ('grad', 'loss', 'priorities'):
     assert torch.equal(got8[k], ref6[k]), k
   assert torch.equal(ho.dacts['h'], dh6)
+
+
+@pytest.mark.parametrize('centered', [True, False])
+def test_fused_rmsprop_backward_equals_backward_then_rmsprop(centered):
+  """The backward with TF1 RMSProp spread over its launches (dq_adam_args kind
+  DQ_OPT_RMSPROP) == dq_cnn_backward + dq_rmsprop_tf1, bitwise, over two steps, for
+  the seven-launch schedule and the fused head's six-launch one (head_from 6)."""
+  from dopamine_amd import ops
+  from dopamine_amd.agents.networks import NatureDQNNetwork
+  from dopamine_amd.cnn import HipNatureCNN
+  nets = [NatureDQNNetwork(6, device='cuda', seed=5) for _ in range(2)]
+  hips = [HipNatureCNN(n, 32) for n in nets]
+  opts = [ops.TF1RMSProp(n.fp.flat, learning_rate=2.5e-4, decay=0.95, momentum=0.1,
+                         epsilon=1e-5, centered=centered) for n in nets]
+  torch.manual_seed(1)
+  for step, groups in enumerate([None, (0, 7), None]):
+    x = torch.rand(32, 84, 84, 4, device='cuda')
+    gout = torch.randn(32, 6, device='cuda')
+    for h in hips:
+      h.forward(x)
+    if groups is None:
+      hips[0].backward(gout, adam=opts[0])
+    else:   # the ride form: dq_cnn_backward_riders with no riders (head_from 6)
+      hips[0].backward(gout, adam=opts[0], groups=groups, head_from=6)
+    hips[1].backward(gout)
+    opts[1].step(nets[1].fp.grad)
+    torch.cuda.synchronize()
+    for a, b in zip(nets[0].fp.grad_views, nets[1].fp.grad_views):
+      assert torch.equal(a, b), step
+    for n in ('params', 'ms', 'mg', 'mom'):       # on the parameters (k_rmsprop also
+      for o, m in nets[0].fp.segments():          # moves ms of the alignment pads)
+        assert torch.equal(getattr(opts[0], n)[o:o + m], getattr(opts[1], n)[o:o + m]), (step, n)
+
+
+@pytest.mark.parametrize('B,A', [(32, 6), (7, 18)])
+def test_fused_forward_and_dqn_loss_equal_separate_path(B, A):
+  """The DQN fast path: forward_fused's fc2 partials summed by dqn_huber_loss_fused give
+  bitwise dq_cnn_forward's Q-values and therefore bitwise dq_dqn_huber_loss's gradient
+  and loss; its fused fc2 input gradient is bitwise the backward's launch 0 (one
+  nonzero product per element), so the backward from launch 1 equals the full one."""
+  from dopamine_amd import ops
+  from dopamine_amd.agents.networks import NatureDQNNetwork
+  from dopamine_amd.cnn import HipNatureCNN, forward_fused
+  on, tg = NatureDQNNetwork(A, device='cuda', seed=1), NatureDQNNetwork(A, device='cuda', seed=2)
+  with torch.no_grad():
+    for net in (on, tg):
+      for n, prm in net.fp.params.items():
+        if n.endswith('_b'):
+          prm.uniform_(-0.05, 0.1)
+  ho, ht = HipNatureCNN(on, B), HipNatureCNN(tg, B)
+  torch.manual_seed(3)
+  x, nx = torch.rand(B, 84, 84, 4, device='cuda'), torch.rand(B, 84, 84, 4, device='cuda')
+  act = torch.randint(0, A, (B,), device='cuda', dtype=torch.int32)
+  rew = torch.randn(B, device='cuda') * 3     # some |TD error| > 1: both Huber branches
+  term = (torch.rand(B, device='cuda') < 0.2).to(torch.uint8)
+  ref_t = ht.forward(nx).clone()
+  ref_o = ho.forward(x).clone()
+  ref_h = ho.acts['h'].clone()
+  ref = ops.dqn_huber_loss(ref_o, ref_t, act, rew, term, 0.99)
+  ref = {k: v.clone() for k, v in ref.items()}
+  ho.backward(ref['grad'])
+  ref_dh = ho.dacts['h'].clone()
+  ref_g = torch.cat([v.reshape(-1) for v in on.fp.grad_views]).clone()
+  for t in (ho.acts['out'], ht.acts['out'], ho.acts['h'], ho.dacts['h']):
+    t.fill_(float('nan'))
+  forward_fused(ho, x, ht)
+  got = ops.dqn_huber_loss_fused(ho, ht, act, rew, term, 0.99, q_out=True)
+  torch.cuda.synchronize()
+  assert torch.equal(ho.acts['h'], ref_h)
+  assert torch.equal(ho.acts['out'], ref_o) and torch.equal(ht.acts['out'], ref_t)
+  for k in ('grad', 'loss'):
+    assert torch.equal(got[k], ref[k]), k
+  assert torch.equal(ho.dacts['h'], ref_dh)
+  assert abs(float(got['loss'].double().mean()) - float(ref['mean_loss'])) <= 1e-6 * (
+      1 + abs(float(ref['mean_loss'])))
+  on.fp.grad.fill_(float('nan'))
+  ho.backward(got['grad'], groups=(1, 7), head_from=6)
+  torch.cuda.synchronize()
+  assert torch.equal(torch.cat([v.reshape(-1) for v in on.fp.grad_views]), ref_g)
