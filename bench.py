@@ -42,6 +42,8 @@ def parse():
   ap.add_argument('--no-graph', action='store_true')
   ap.add_argument('--cpu-seconds', type=float, default=12.0)
   ap.add_argument('--skip-cpu-baseline', action='store_true')
+  ap.add_argument('--skip-configs', action='store_true',
+                  help='do not time BASELINE configs 2 and 5 after the headline (N = 1)')
   ap.add_argument('--per-call', action='store_true',
                   help='drive the agent by update_period _train_step() calls per gradient '
                        'step (one graph replay per step) instead of train_gradient_steps')
@@ -86,6 +88,95 @@ def build_agent(actions, capacity, batch, device, pg=None, **kw):
                       optimizer=AdamOptimizer(learning_rate=0.0000625, epsilon=0.00015),
                       replay_capacity=capacity, batch_size=batch, device=device, seed=0,
                       process_group=pg, **kw)
+
+
+def build_dqn_pong(device, **kw):
+  """BASELINE config 2: DQN as dqn.gin binds it (6 actions, uniform replay, n = 1, TF1
+  centered RMSProp 2.5e-4 / 0.95 / 1e-5, target period 8000, update period 4), B = 32."""
+  from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
+  return DQNAgent(num_actions=6, min_replay_history=20000, update_period=4,
+                  target_update_period=8000, replay_capacity=1_000_000, batch_size=32,
+                  device=device, seed=0, **kw)
+
+
+def build_iqn_breakout(device, **kw):
+  """BASELINE config 5: IQN as implicit_quantile.gin binds it (4 actions, N = N' = 64,
+  K = 32, n = 3, uniform replay, Adam 5e-5 / 3.125e-4, kappa 1, embedding 64), B = 64."""
+  from dopamine_amd.agents.implicit_quantile.implicit_quantile_agent import ImplicitQuantileAgent
+  from dopamine_amd.agents.optimizers import AdamOptimizer
+  return ImplicitQuantileAgent(
+      num_actions=4, num_tau_samples=64, num_tau_prime_samples=64, num_quantile_samples=32,
+      update_horizon=3, replay_scheme='uniform', min_replay_history=20000, update_period=4,
+      target_update_period=8000, optimizer=AdamOptimizer(learning_rate=0.00005, epsilon=0.0003125),
+      replay_capacity=1_000_000, batch_size=64, device=device, seed=0, **kw)
+
+
+MIN_PRE_STEPS = 100
+
+
+def timed_steps(agent, steps, warmup, per_call=False, pg=None):
+  """The bench protocol on one agent: untimed priming, whatever ``warmup`` is, until every
+  graph the timed loop replays is captured (both step parities, the 4-step chunk graphs of
+  both starting parities) and the device has been busy for at least MIN_PRE_STEPS steps
+  (its clocks ramp under load: a 20-step window after 5 warmup steps read 7% low); then
+  the warmup; then exactly ``steps`` gradient steps between barriers + synchronize.  No
+  cyclic-garbage collection pass inside the window (a full pass over a torch process's
+  objects takes milliseconds).  Returns (elapsed seconds, priming steps)."""
+  def grad_steps(n):
+    if per_call:
+      for _ in range(n):
+        for _ in range(agent.update_period):   # the reference's _train_step cadence
+          agent._train_step()
+    else:   # the same calls, consecutive steps replayed K per HIP graph (learner-only loop)
+      agent.train_gradient_steps(n)
+
+  gc.collect()
+  gc.disable()
+  prime = 0
+  while ((not agent.graphs_primed() or prime + warmup < MIN_PRE_STEPS) and prime < 400):
+    grad_steps(5)
+    prime += 5
+  grad_steps(warmup)
+  torch.cuda.synchronize()
+  if pg is not None:
+    dist.barrier()
+  torch.cuda.synchronize()
+  t0 = time.perf_counter()
+  grad_steps(steps)
+  torch.cuda.synchronize()
+  if pg is not None:
+    dist.barrier()
+  elapsed = time.perf_counter() - t0
+  gc.enable()
+  return elapsed, prime
+
+
+def other_configs(device, steps):
+  """Supplementary, rank 0 at N = 1: BASELINE configs 2 and 5 on their own synthetic 1M
+  buffers, same protocol as the headline (so the driver's run clocks them too)."""
+  res = {}
+  for name, make, A, n in (('dqn_pong', build_dqn_pong, 6, max(steps, 1000)),
+                           ('iqn_breakout', build_iqn_breakout, 4, max(steps // 3, 50))):
+    agent = make(device)
+    import random
+    random.seed(0)
+    fill_synthetic(agent._replay.memory, A, seed=1)
+    torch.cuda.synchronize()
+    elapsed, prime = timed_steps(agent, n, 10)
+    agent._replay.memory.sync_rng()
+    loss = agent.mean_loss()
+    assert np.isfinite(loss), 'non-finite loss (%s)' % name
+    res[name] = {'value': round(n / elapsed, 2), 'unit': 'gradient-steps/s', 'steps': n,
+                 'ms_per_step': round(1e3 * elapsed / n, 4), 'batch': agent._batch_size,
+                 'final_mean_loss': round(loss, 5)}
+    del agent
+    gc.collect()
+    torch.cuda.empty_cache()
+  res['dqn_pong']['workload'] = ('config 2: DQN Pong (6 actions), uniform replay, n=1, TF1 '
+                                 'centered RMSProp, 1M-transition buffer')
+  res['iqn_breakout']['workload'] = ('config 5: IQN Breakout (4 actions), N=N\'=64, K=32, n=3, '
+                                     'uniform replay, Adam, 1M-transition buffer')
+  return res
 
 
 def time_gather(agent, iters):
@@ -268,39 +359,7 @@ def main():
   fill_synthetic(agent._replay.memory, args.actions, seed=1 + rank)
   torch.cuda.synchronize()
 
-  def grad_steps(n):
-    if args.per_call:
-      for _ in range(n):
-        for _ in range(agent.update_period):   # the reference's _train_step cadence
-          agent._train_step()
-    else:   # the same calls, consecutive steps replayed K per HIP graph (learner-only loop)
-      agent.train_gradient_steps(n)
-
-  # No cyclic-garbage collection pass inside the timed window (a full pass over a torch
-  # process's objects takes milliseconds: one would dominate a short window).
-  gc.collect()
-  gc.disable()
-  # Untimed, whatever --warmup is: run until every graph the timed loop replays is captured
-  # (both step parities, the 4-step chunk graphs of both starting parities) and the device
-  # has been busy for at least MIN_PRE_STEPS steps before the window (its clocks ramp under
-  # load: a 20-step window after 5 warmup steps read 7% low); then the warmup.
-  MIN_PRE_STEPS = 100
-  prime = 0
-  while ((not agent.graphs_primed() or prime + args.warmup < MIN_PRE_STEPS) and prime < 400):
-    grad_steps(5)
-    prime += 5
-  grad_steps(args.warmup)
-  torch.cuda.synchronize()
-  if pg is not None:
-    dist.barrier()
-  torch.cuda.synchronize()
-  t0 = time.perf_counter()
-  grad_steps(args.steps)
-  torch.cuda.synchronize()
-  if pg is not None:
-    dist.barrier()
-  elapsed = time.perf_counter() - t0
-  gc.enable()
+  elapsed, prime = timed_steps(agent, args.steps, args.warmup, args.per_call, pg)
   if pg is not None:
     t = torch.tensor([elapsed], dtype=torch.float64, device='cpu' if rehearse else dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -313,6 +372,13 @@ def main():
   large = time_gather_large(agent)
   traffic, traffic_src = gather_traffic(args.batch)
   achieved = algo_bytes / (graph_us * 1e-6) / 1e9
+
+  configs = None
+  if rank == 0 and world == 1 and not args.skip_configs and not args.force_dist:
+    del agent
+    gc.collect()
+    torch.cuda.empty_cache()
+    configs = other_configs(dev, args.steps)
 
   cpu = None
   if rank == 0 and world == 1 and not args.skip_cpu_baseline:
@@ -345,6 +411,8 @@ def main():
         'step_mfma': step_mfma(args.actions, args.batch, elapsed / args.steps),
         'cpu_baseline': cpu,
         'final_mean_loss': round(loss, 5),
+        # supplementary: BASELINE configs 2 and 5 (N = 1), same protocol, not the metric
+        'other_configs': configs,
     }
     print(json.dumps(line), flush=True)
   if pg is not None:

@@ -51,21 +51,12 @@ def main():
     k, v = a.split('=')
     extra[k] = bool(int(v))
   dev = torch.device('cuda', 0)
-  from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
-  from dopamine_amd.agents.implicit_quantile.implicit_quantile_agent import ImplicitQuantileAgent
   res = {}
   if which in ('all', 'dqn_pong'):
-    res['dqn_pong'] = measure(lambda: DQNAgent(num_actions=6, min_replay_history=20000,
-                                               update_period=4, target_update_period=8000,
-                                               replay_capacity=1_000_000, batch_size=32,
-                                               device=dev, **extra), 6, steps)
-  from dopamine_amd.agents.optimizers import AdamOptimizer
+    res['dqn_pong'] = measure(lambda: bench.build_dqn_pong(dev, **extra), 6, steps)
   if which in ('all', 'iqn_breakout'):
-    res['iqn_breakout'] = measure(lambda: ImplicitQuantileAgent(   # implicit_quantile.gin
-      num_actions=4, num_tau_samples=64, num_tau_prime_samples=64, num_quantile_samples=32,
-      update_horizon=3, replay_scheme='uniform', min_replay_history=20000, update_period=4,
-      target_update_period=8000, optimizer=AdamOptimizer(learning_rate=0.00005, epsilon=0.0003125),
-      replay_capacity=1_000_000, batch_size=64, device=dev, **extra), 4, max(steps // 3, 50))
+    res['iqn_breakout'] = measure(lambda: bench.build_iqn_breakout(dev, **extra), 4,
+                                  max(steps // 3, 50))
   print(json.dumps(res))
 
 
