@@ -55,6 +55,9 @@ def parse():
   ap.add_argument('--split-c51', type=int, default=None,
                   help='override RainbowAgent.split_c51 (0/1): the C51 target half riding in '
                        'the forward (head_from 8) or inside the loss kernel')
+  ap.add_argument('--zero', type=int, default=0,
+                  help='N > 1: ZeRO-1 for the fc bucket (DQNAgent shard_optimizer): '
+                       'reduce-scatter, TF1 Adam on the rank\'s slice, all-gather (0/1)')
   ap.add_argument('--force-dist', action='store_true',
                   help='one rank only: run the N > 1 learner schedule over a one-rank RCCL group '
                        'with every collective executed (a hardware check of the data-parallel '
@@ -353,7 +356,8 @@ def main():
   agent = build_agent(args.actions, args.capacity, args.batch, dev, pg=pg,
                       use_hip_graph=not args.no_graph,
                       **({} if args.fuse_opt is None else {'fuse_optimizer': bool(args.fuse_opt)}),
-                      **({} if args.ride is None else {'ride_replay': bool(args.ride)}))
+                      **({} if args.ride is None else {'ride_replay': bool(args.ride)}),
+                      **({'shard_optimizer': True} if args.zero else {}))
   import random
   random.seed(0 + rank)
   fill_synthetic(agent._replay.memory, args.actions, seed=1 + rank)
@@ -397,7 +401,8 @@ def main():
                    'global_batch': args.batch * world, 'per_gpu_batch': args.batch,
                    'replay_capacity': args.capacity,
                    'parallelism': 'dp%d' % world + (' (one-rank RCCL group, --force-dist)'
-                                                    if args.force_dist and world == 1 else ''),
+                                                    if args.force_dist and world == 1 else '')
+                                  + (', ZeRO-1 fc bucket' if args.zero else ''),
                    'hip_graph': not args.no_graph},
         'roofline': {'kernel': gname + ' (frame-stack gather + /255, state+next_state)',
                      'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,

@@ -89,7 +89,8 @@ class DQNAgent(object):
                fused_head=True,
                device=None,
                seed=0,
-               process_group=None):
+               process_group=None,
+               shard_optimizer=False):
     assert num_actions is not None
     assert isinstance(observation_shape, tuple)      # abstract_agent.py:34
     self.num_actions = num_actions
@@ -119,6 +120,9 @@ class DQNAgent(object):
     self._device = _device_of(tf_device, device)
     self._seed = seed
     self._pg = process_group
+    # N > 1 with TF1 Adam: ZeRO-1 for the fc bucket (reduce-scatter, each rank's Adam on
+    # its 1/N slice, all-gather of the parameters) instead of all-reduce + a full update
+    self.shard_optimizer = bool(shard_optimizer)
     self._pg_conv = None           # a second communicator for the conv bucket (see _split_step)
     self._fc_pending = None        # event: the previous step's fc all-reduce + update are done
     self._defer_fc = False         # set by train_gradient_steps (learner-only loop)
@@ -586,6 +590,34 @@ class DQNAgent(object):
                                      backend=dist.get_backend(self._pg))
     return self._pg_conv
 
+  def _sharded(self):
+    """shard_optimizer in effect: N > 1 (or forced collectives) with TF1 Adam."""
+    return (self.shard_optimizer and self._pg is not None and isinstance(self._opt, ops.TF1Adam)
+            and (self._world() > 1 or parallel.FORCE_COLLECTIVES))
+
+  def _world(self):
+    import torch.distributed as dist
+    return dist.get_world_size(self._pg)
+
+  def _shard_bounds(self):
+    """(lo, n): the sharded range [lo, n) of the flat buffer -- the fc bucket minus a head
+    of fewer than 4N floats, so that it splits into N equal 16-byte-aligned slices; the
+    head joins the conv bucket (all-reduced, replicated update)."""
+    n = self.online_convnet.fp.grad.numel()
+    o = n - self._grad_buckets()[0].numel()
+    return o + (n - o) % (4 * self._world()), n
+
+  def _gather_opt_state(self):
+    """ZeRO-1: every rank's Adam moments of the sharded range, slice r from rank r (a
+    collective: every rank calls it, e.g. from bundle_and_checkpoint)."""
+    if not self._sharded():
+      return
+    lo, n = self._shard_bounds()
+    torch.cuda.synchronize(self._device)
+    for t in (self._opt.m, self._opt.v):
+      parallel.all_gather_(t[lo:n], self._pg)
+    torch.cuda.synchronize(self._device)
+
   def _split_step(self, head_a, head_b, tail, opt, k=0):
     """head | tail on the main stream with the fc bucket's all-reduce on the comm
     stream beside the tail; with TF1 Adam the fc parameters' update follows their
@@ -622,18 +654,39 @@ class DQNAgent(object):
     # next piece's (an HBM-bound update beside a link-bound collective).  Elementwise
     # ops: bitwise the one-bucket result.  (Blocking collectives + events rather than
     # async work handles, which graph capture does not survive.)
-    pieces = self._fc_pieces(o, grad.numel()) if split_opt else [(o, grad.numel())]
     last = self._comm
-    for lo, hi in pieces:
+    if self._sharded():
+      # ZeRO-1: reduce-scatter the fc bucket, TF1 Adam on this rank's slice only (1/N of
+      # the fc update's 112 MB), all-gather the updated parameters -- the same bytes over
+      # the links as the all-reduce; the other slices' moments live on their owners
+      lo, n = self._shard_bounds()
+      S = (n - lo) // self._world()
+      r = torch.distributed.get_rank(self._pg)
       with torch.cuda.stream(self._comm):
-        parallel.allreduce_mean_(grad[lo:hi], self._pg)
-      if split_opt:
-        e = torch.cuda.Event()
-        e.record(self._comm)
-        self._comm_opt.wait_event(e)
-        with torch.cuda.stream(self._comm_opt):
-          self._opt.step_part(grad, lo, hi, slot=k, bump=False)
-        last = self._comm_opt
+        parallel.reduce_scatter_mean_(grad[lo:n], self._pg)
+      e = torch.cuda.Event()
+      e.record(self._comm)
+      self._comm_opt.wait_event(e)
+      with torch.cuda.stream(self._comm_opt):
+        self._opt.step_part(grad, lo + r * S, lo + (r + 1) * S, slot=k, bump=False)
+      e = torch.cuda.Event()
+      e.record(self._comm_opt)
+      self._comm.wait_event(e)
+      with torch.cuda.stream(self._comm):
+        parallel.all_gather_(self._opt.params[lo:n], self._pg)
+      conv, o = grad[:lo], lo                 # the head of the fc bucket joins the conv bucket
+    else:
+      pieces = self._fc_pieces(o, grad.numel()) if split_opt else [(o, grad.numel())]
+      for lo, hi in pieces:
+        with torch.cuda.stream(self._comm):
+          parallel.allreduce_mean_(grad[lo:hi], self._pg)
+        if split_opt:
+          e = torch.cuda.Event()
+          e.record(self._comm)
+          self._comm_opt.wait_event(e)
+          with torch.cuda.stream(self._comm_opt):
+            self._opt.step_part(grad, lo, hi, slot=k, bump=False)
+          last = self._comm_opt
     if defer:
       parallel.allreduce_mean_(conv, self._conv_group())
       self._fc_pending = torch.cuda.Event()
@@ -933,9 +986,16 @@ class DQNAgent(object):
     if self._pg is None:
       return False
     import torch.distributed as dist
+    # ZeRO-1's reduce-scatter / all-gather replay as a captured 4-step chunk ended in a
+    # segfault at capture end on ROCm 7.2 (one-rank RCCL; the same collectives captured
+    # alone replay correctly, parallel.collectives_capturable(sharded=True)): the sharded
+    # path runs per-step graphs with its collectives issued between them
+    if self._sharded():
+      return False
     return (dist.get_backend(self._pg) == 'nccl' and self._split_allreduce() and
             self._head_splits() and isinstance(self._opt, ops.TF1Adam) and
-            parallel.collectives_capturable(self._pg, self._device, self._comm))
+            parallel.collectives_capturable(self._pg, self._device, self._comm,
+                                            sharded=False))
 
   def _chunks_apply(self):
     return (self._hip is not None and self.pipeline and
@@ -1049,6 +1109,8 @@ class DQNAgent(object):
     """dqn_agent.py:482-510 (torch tensors instead of a tf.train.Saver)."""
     if not os.path.isdir(checkpoint_dir):
       return None
+    self._join_fc()
+    self._gather_opt_state()          # ZeRO-1: complete moments on every rank (collective)
     torch.save({k: v.detach().cpu() for k, v in self._ckpt_tensors().items()},
                os.path.join(checkpoint_dir, 'tf_ckpt-{}'.format(iteration_number)))
     stale = iteration_number - self.max_tf_checkpoints_to_keep

@@ -33,6 +33,45 @@ def allreduce_mean_(flat_grad, group=None):
   return flat_grad
 
 
+def _active(group):
+  return dist.get_world_size(group) > 1 or FORCE_COLLECTIVES
+
+
+def reduce_scatter_mean_(flat, group=None):
+  """In place: slice r of ``flat`` (numel divisible by the group size; slice r = the r-th
+  equal part) becomes the mean of that slice over the ranks, on group rank r.  RCCL
+  reduce-scatters in place (output = input + r * count, ReduceOp.AVG); over gloo the
+  whole range is all-reduced (every slice holds its mean: the replicated path's bits)."""
+  world = dist.get_world_size(group)
+  if not _active(group):
+    return flat
+  assert flat.numel() % world == 0
+  if dist.get_backend(group) == 'nccl':
+    n = flat.numel() // world
+    r = dist.get_rank(group)
+    dist.reduce_scatter_tensor(flat[r * n:(r + 1) * n], flat, op=dist.ReduceOp.AVG, group=group)
+    return flat
+  return allreduce_mean_(flat, group)
+
+
+def all_gather_(flat, group=None):
+  """In place: slice r of ``flat`` (as reduce_scatter_mean_) on every rank becomes group
+  rank r's slice.  RCCL all-gathers in place; over gloo, one broadcast per slice."""
+  world = dist.get_world_size(group)
+  if not _active(group):
+    return flat
+  assert flat.numel() % world == 0
+  n = flat.numel() // world
+  if dist.get_backend(group) == 'nccl':
+    r = dist.get_rank(group)
+    dist.all_gather_into_tensor(flat, flat[r * n:(r + 1) * n], group=group)
+    return flat
+  ranks = dist.get_process_group_ranks(group) if group is not None else list(range(world))
+  for i, src in enumerate(ranks):
+    dist.broadcast(flat[i * n:(i + 1) * n], src=src, group=group)
+  return flat
+
+
 def replicas_in_sync(flat_params, group=None):
   """Checksum-broadcast check that every rank holds identical parameters."""
   s = torch.stack([flat_params.double().sum(), (flat_params.double() ** 2).sum()])
@@ -46,14 +85,14 @@ def replicas_in_sync(flat_params, group=None):
 _CAPTURABLE = {}
 
 
-def collectives_capturable(group, device, stream=None):
+def collectives_capturable(group, device, stream=None, sharded=False):
   """Whether every rank of ``group`` can capture this backend's all-reduce into a HIP
   graph and replay it correctly -- probed once per group on a small tensor, the ranks
   agreeing (eager MIN all-reduces) after each phase so no rank replays a collective the
   others did not capture.  False for gloo (host-side collectives).  The learner loop
   captures its all-reduces only where this holds, else it replays per-step graphs with
   the collectives issued between them."""
-  key = id(group)
+  key = (id(group), bool(sharded))
   if key in _CAPTURABLE:
     return _CAPTURABLE[key]
   if dist.get_backend(group) != 'nccl':
@@ -66,17 +105,25 @@ def collectives_capturable(group, device, stream=None):
     return bool(t.item() == 1.0)
 
   rank = dist.get_rank(group)
-  x = torch.full((1024,), float(rank + 1), device=device)
+  world = dist.get_world_size(group)
+  x = torch.full((1024 * world,), float(rank + 1), device=device)
+
+  def collectives():     # sharded: the ZeRO-1 pair (reduce-scatter, all-gather) as well
+    allreduce_mean_(x, group)
+    if sharded:
+      reduce_scatter_mean_(x, group)
+      all_gather_(x, group)
+
   s = stream or torch.cuda.Stream(device)
   g = torch.cuda.CUDAGraph()
   ok = True
   try:
-    allreduce_mean_(x, group)                     # the communicator is warm before capture
+    collectives()                                 # the communicator is warm before capture
     torch.cuda.synchronize(device)
     s.wait_stream(torch.cuda.current_stream(device))
     with torch.cuda.stream(s):
       with torch.cuda.graph(g, stream=s, capture_error_mode='thread_local'):
-        allreduce_mean_(x, group)
+        collectives()
   except Exception:                               # noqa: BLE001 -- any failure means "no"
     ok = False
   ok = agree(ok)
@@ -85,7 +132,6 @@ def collectives_capturable(group, device, stream=None):
       x.fill_(float(rank + 1))
       g.replay()
       torch.cuda.synchronize(device)
-      world = dist.get_world_size(group)
       want = sum(range(1, world + 1)) / world if (world > 1 or FORCE_COLLECTIVES) else 1.0
       ok = bool(torch.allclose(x, torch.full_like(x, want)))
     except Exception:                             # noqa: BLE001

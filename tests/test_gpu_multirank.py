@@ -48,7 +48,7 @@ def _run(agent, loop=False):
   return agent.online_convnet.fp.flat.detach().cpu().clone()
 
 
-def _worker(rank, world, port, same_seed, q, loop=False, net_seed_per_rank=False):
+def _worker(rank, world, port, same_seed, q, loop=False, net_seed_per_rank=False, shard=False):
   import sys
   sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
   import torch.distributed as dist
@@ -58,13 +58,16 @@ def _worker(rank, world, port, same_seed, q, loop=False, net_seed_per_rank=False
   dist.init_process_group('gloo', rank=rank, world_size=world)
   from dopamine_amd import parallel
   agent = _agent(dist.group.WORLD, 0 if same_seed else rank,
-                 net_seed=1000 * rank if net_seed_per_rank else 0)
+                 net_seed=1000 * rank if net_seed_per_rank else 0, shard_optimizer=shard)
+  assert agent._sharded() == shard
   flat = _run(agent, loop)
   assert agent.graphs_primed()      # the later steps replayed the captured split graphs
   ok = parallel.replicas_in_sync(agent.online_convnet.fp.flat)
   ok = ok and parallel.replicas_in_sync(agent.target_convnet.fp.flat)
+  agent._gather_opt_state()         # ZeRO-1: the moments of every slice, as a checkpoint sees them
+  ok = ok and parallel.replicas_in_sync(agent._opt.m) and parallel.replicas_in_sync(agent._opt.v)
   if rank == 0:
-    q.put((ok, flat.numpy()))
+    q.put((ok, flat.numpy(), agent._opt.m.cpu().numpy(), agent._opt.v.cpu().numpy()))
   dist.barrier()
   dist.destroy_process_group()
 
@@ -77,19 +80,20 @@ def _free_port():
   return p
 
 
-def _two_ranks(same_seed, loop=False, net_seed_per_rank=False):
+def _two_ranks(same_seed, loop=False, net_seed_per_rank=False, shard=False, moments=False):
   ctx = mp.get_context('spawn')
   q = ctx.Queue()
   port = _free_port()
-  procs = [ctx.Process(target=_worker, args=(r, 2, port, same_seed, q, loop, net_seed_per_rank))
+  procs = [ctx.Process(target=_worker, args=(r, 2, port, same_seed, q, loop, net_seed_per_rank,
+                                             shard))
            for r in range(2)]
   for p in procs:
     p.start()
-  ok, flat = q.get(timeout=400)
+  ok, flat, m, v = q.get(timeout=400)
   for p in procs:
     p.join(timeout=120)
     assert p.exitcode == 0
-  return ok, flat
+  return (ok, flat, m, v) if moments else (ok, flat)
 
 
 @pytest.mark.timeout(600)
@@ -114,7 +118,7 @@ def test_two_ranks_learner_loop_equal_single_learner_bitwise():
   assert np.array_equal(flat, single)
 
 
-def _mean_gradient_reference(loop=False):
+def _mean_gradient_reference(loop=False, moments=False):
   """Both ranks' learners in ONE process, no collective: each _train_step computes
   its own gradient (the optimizer deferred), the two flat gradients are averaged
   ((gA + gB) * 0.5, what gloo's sum + scale gives), and the TF1 Adam step is applied
@@ -149,6 +153,8 @@ def _mean_gradient_reference(loop=False):
   torch.cuda.synchronize()
   a, b = (ag.online_convnet.fp.flat.cpu().numpy() for ag in agents)
   assert np.array_equal(a, b)
+  if moments:
+    return a, agents[0]._opt.m.cpu().numpy(), agents[0]._opt.v.cpu().numpy()
   return a
 
 
@@ -165,3 +171,18 @@ def test_two_ranks_different_data_equal_mean_gradient_reference(loop):
   assert np.array_equal(flat, ref)
   lone = _run(_agent(None, 0)).numpy()        # rank 0 alone differs: the reduction did something
   assert not np.array_equal(flat, lone)
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize('loop', [False, True])
+def test_two_ranks_sharded_optimizer_equal_mean_gradient_reference(loop):
+  """ZeRO-1 (shard_optimizer): the fc bucket reduce-scattered, each rank's TF1 Adam on its
+  half only, the parameters all-gathered -- different buffers and network seeds per rank:
+  parameters AND (gathered) Adam moments bitwise those of the replicated mean-gradient
+  update."""
+  ok, flat, m, v = _two_ranks(same_seed=False, loop=loop, net_seed_per_rank=True, shard=True,
+                              moments=True)
+  assert ok
+  ref, rm, rv = _mean_gradient_reference(loop, moments=True)
+  assert np.array_equal(flat, ref)
+  assert np.array_equal(m, rm) and np.array_equal(v, rv)

@@ -61,11 +61,25 @@ def test_rccl_one_rank_schedule_equals_single_learner_bitwise(rccl_group, loop):
   assert np.array_equal(flat, single)
 
 
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize('loop', [False, True])
+def test_rccl_one_rank_sharded_optimizer_equals_single_learner_bitwise(rccl_group, loop):
+  """ZeRO-1 over RCCL (in-place reduce-scatter, TF1 Adam on the rank's slice, in-place
+  all-gather, between the per-step graphs): one rank owns every slice, so the parameters
+  equal a single learner's bit for bit."""
+  agent = _agent(rccl_group, 0, shard_optimizer=True)
+  assert agent._sharded()
+  flat = _run(agent, loop).numpy()
+  single = _run(_agent(None, 0), loop).numpy()
+  assert np.array_equal(flat, single)
+
+
 def test_collective_capture_probe(rccl_group):
   """The probe that gates captured all-reduces in the learner loop says yes on RCCL."""
   from dopamine_amd import parallel
   parallel._CAPTURABLE.clear()
   assert parallel.collectives_capturable(rccl_group, torch.device('cuda', 0))
+  assert parallel.collectives_capturable(rccl_group, torch.device('cuda', 0), sharded=True)
 
 
 def test_allreduce_mean_over_rccl_is_identity_for_one_rank(rccl_group):

@@ -83,3 +83,45 @@ def test_two_rank_allreduce_matches_mean_gradient():
     g = sum(_rank_grad(r + 10 * step, net) for r in range(world)) / world
     adam.step(params, g.numpy())
   np.testing.assert_allclose(flat.numpy(), params, rtol=1e-6, atol=1e-9)
+
+
+def _shard_worker(rank, world, port, q):
+  os.environ['MASTER_ADDR'] = '127.0.0.1'
+  os.environ['MASTER_PORT'] = str(port)
+  dist.init_process_group('gloo', rank=rank, world_size=world)
+  from dopamine_amd import parallel
+  n = 4 * world * 5
+  g = torch.arange(n, dtype=torch.float32) * (rank + 1)
+  parallel.reduce_scatter_mean_(g)
+  S = n // world
+  mine = g[rank * S:(rank + 1) * S].clone()          # this rank's slice of the mean
+  p = torch.full((n,), -1.0)
+  p[rank * S:(rank + 1) * S] = mine * 10 + rank       # the owner's update of its slice
+  parallel.all_gather_(p)
+  q.put((rank, mine, p))
+  dist.barrier()
+  dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_reduce_scatter_and_all_gather_slices():
+  """The ZeRO-1 pair (parallel.reduce_scatter_mean_ / all_gather_): rank r holds the mean
+  of slice r, and after each owner rewrites its slice every rank holds all of them."""
+  world = 2
+  ctx = mp.get_context('spawn')
+  q = ctx.Queue()
+  port = _free_port()
+  procs = [ctx.Process(target=_shard_worker, args=(r, world, port, q)) for r in range(world)]
+  for p in procs:
+    p.start()
+  res = dict((r, (m, p)) for r, m, p in (q.get(timeout=240) for _ in range(world)))
+  for p in procs:
+    p.join(timeout=60)
+    assert p.exitcode == 0
+  n = 4 * world * 5
+  S = n // world
+  mean = torch.arange(n, dtype=torch.float32) * sum(r + 1 for r in range(world)) / world
+  want = torch.cat([mean[r * S:(r + 1) * S] * 10 + r for r in range(world)])
+  for r in range(world):
+    assert torch.equal(res[r][0], mean[r * S:(r + 1) * S])
+    assert torch.equal(res[r][1], want)
