@@ -106,6 +106,13 @@ class RNGTape:
     unless the tape might run dry; returns True if it had to sync."""
     if self.valid and self._probe is not None:
       self._poll()
+    if self.valid and self._budget < worst_case and self._probe is not None:
+      # The host ran further ahead of the device than the worst-case budget allows: wait
+      # for the device to reach the probe point (the work queued behind it keeps the
+      # device busy) and re-base, instead of draining the queue for a refill (a sync plus
+      # a 1 Mi-word host rebuild: ~6 ms of device idle every ~250 uniform-replay steps)
+      self._probe[0].synchronize()
+      self._poll()
     if self.valid and self._budget >= worst_case:
       self._budget -= worst_case
       self._reserved += worst_case

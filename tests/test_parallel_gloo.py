@@ -47,7 +47,7 @@ def _worker(rank, world, port, q):
     adam.step(params, net.fp.grad.numpy())
   in_sync = parallel.replicas_in_sync(net.fp.flat)
   if rank == 0:
-    q.put((in_sync, net.fp.flat.clone()))
+    q.put((in_sync, net.fp.flat.numpy().copy()))    # by value: the child may exit first
   dist.barrier()
   dist.destroy_process_group()
 
@@ -82,7 +82,7 @@ def test_two_rank_allreduce_matches_mean_gradient():
   for step in range(2):
     g = sum(_rank_grad(r + 10 * step, net) for r in range(world)) / world
     adam.step(params, g.numpy())
-  np.testing.assert_allclose(flat.numpy(), params, rtol=1e-6, atol=1e-9)
+  np.testing.assert_allclose(flat, params, rtol=1e-6, atol=1e-9)
 
 
 def _shard_worker(rank, world, port, q):
@@ -98,7 +98,7 @@ def _shard_worker(rank, world, port, q):
   p = torch.full((n,), -1.0)
   p[rank * S:(rank + 1) * S] = mine * 10 + rank       # the owner's update of its slice
   parallel.all_gather_(p)
-  q.put((rank, mine, p))
+  q.put((rank, mine.numpy(), p.numpy()))     # by value: the child may exit before the read
   dist.barrier()
   dist.destroy_process_group()
 
@@ -123,5 +123,5 @@ def test_reduce_scatter_and_all_gather_slices():
   mean = torch.arange(n, dtype=torch.float32) * sum(r + 1 for r in range(world)) / world
   want = torch.cat([mean[r * S:(r + 1) * S] * 10 + r for r in range(world)])
   for r in range(world):
-    assert torch.equal(res[r][0], mean[r * S:(r + 1) * S])
-    assert torch.equal(res[r][1], want)
+    assert np.array_equal(res[r][0], mean[r * S:(r + 1) * S].numpy())
+    assert np.array_equal(res[r][1], want.numpy())
