@@ -271,6 +271,19 @@ def gather_traffic(batch):
     return None, None
 
 
+def gather_in_step():
+  """The gather's marginal cost where the step runs it (a rider of backward launch B3):
+  B3's mean duration with and without the gather's blocks, from the committed rocprof A/B
+  (profiles/r2_gather_in_step.json, tools/gpu_r2s3i.sh), or None."""
+  path = os.path.join(ROOT, 'profiles', 'r2_gather_in_step.json')
+  try:
+    d = json.load(open(path))
+    return {k: d[k] for k in ('in_step_us', 'achieved_GBs', 'frac', 'b3_with_gather_us',
+                              'b3_without_gather_us')} | {'source': os.path.relpath(path, ROOT)}
+  except (OSError, KeyError, ValueError):
+    return None
+
+
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
 
 
@@ -410,7 +423,9 @@ def main():
                      'traffic': traffic, 'traffic_source': traffic_src,
                      'algo_bytes_per_launch': algo_bytes,
                      'avg_launch_us': round(graph_us, 3), 'avg_launch_us_eager': round(eager_us, 3),
-                     'same_kernel_batch_1024': large},
+                     'same_kernel_batch_1024': large,
+                     # the same kernel riding in the step (not the measured launch above)
+                     'in_step_marginal': gather_in_step()},
         # supplementary: the whole step against the fp32 matrix peak (the CNN's fp32 MFMA
         # work; the step is launch- and latency-bound at B = 32, not MFMA-bound)
         'step_mfma': step_mfma(args.actions, args.batch, elapsed / args.steps),

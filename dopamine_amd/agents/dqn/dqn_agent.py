@@ -390,11 +390,17 @@ class DQNAgent(object):
   # write-back -> sample -> gather in consecutive backward launches; k > 0 moves the gather
   # k launches later (it must still precede the target head's first launch).
   _GATHER_SHIFT = int(os.environ.get('DQ_GATHER_SHIFT', '0'))
+  # Timing experiment only (tools/gpu_r2s3i.sh): DQ_EXP_SKIP_GATHER=1 replaces the gather
+  # rider by an empty one -- the same launches without the gather's blocks, so the rider's
+  # in-step cost can be read off the profile; the batches then go stale (wrong results).
+  _SKIP_GATHER = os.environ.get('DQ_EXP_SKIP_GATHER') == '1'
 
   def _place_riders(self, riders):
+    from dopamine_amd import _lib
+    if self._SKIP_GATHER and riders:
+      riders = riders[:-1] + [_lib.Rider()]
     if not self._GATHER_SHIFT or not riders:
       return riders
-    from dopamine_amd import _lib
     return riders[:-1] + [_lib.Rider() for _ in range(self._GATHER_SHIFT)] + riders[-1:]
 
   def _forward_fused_c51(self, c, part=None):
