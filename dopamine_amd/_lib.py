@@ -186,6 +186,7 @@ SIGNATURES = {
                              ctypes.POINTER(IqnActs), _P, ctypes.POINTER(IqnGrads), _P, _P, _P],
     'dq_iqn_workspace_floats': [_I32, _I32, _I32, _I32],
     'dq_uniform_draw': [_P, ctypes.c_uint64, _I64, _P, _P],
+    'dq_iqn_tau_cos': [_P, ctypes.c_uint64, _I32, _I32, _P, _P, _P],
 }
 RESTYPES = {'dq_last_error': ctypes.c_char_p, 'dq_cnn_workspace_floats': ctypes.c_size_t,
             'dq_iqn_workspace_floats': ctypes.c_size_t,

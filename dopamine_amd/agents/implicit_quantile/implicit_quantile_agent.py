@@ -71,12 +71,13 @@ class ImplicitQuantileAgent(rainbow_agent.RainbowAgent):
 
   def _build_train_op(self):
     B, A, dev = self._batch_size, self.num_actions, self._device
+    # mean_loss None: the summary mean is not on the gradient path (computed on demand)
     self._loss_out = dict(grad=torch.empty((self.num_tau_samples * B, A), device=dev),
-                          loss=torch.empty(B, device=dev), mean_loss=torch.empty(1, device=dev))
+                          loss=torch.empty(B, device=dev), mean_loss=None)
 
   def mean_loss(self):
     """mean over the batch of the quantile loss (the QuantileLoss summary, iqn:316-319)."""
-    return float(self._loss_out['mean_loss'].item())
+    return float(self._loss_out['loss'].double().mean().item())
 
   def _needs_flat_grad(self):
     return self._iqn is not None or super()._needs_flat_grad()
@@ -101,15 +102,15 @@ class ImplicitQuantileAgent(rainbow_agent.RainbowAgent):
     ex = self._iqn['act']
     scale = 1.0 / 255.0 if np.dtype(self.observation_dtype) == np.uint8 else 1.0
     x = torch.as_tensor(np.asarray(state_np) * scale, dtype=torch.float32, device=self._device)
-    self._taus.draw(ex.taus)
-    q, _ = ex.forward(x.reshape(1, 84, 84, 4).contiguous())
+    self._taus.draw_cos(ex)
+    q, _ = ex.forward(x.reshape(1, 84, 84, 4).contiguous(), cos_ready=True)
     return q.view(self.num_quantile_samples, 1, -1).mean(0)
 
   def _target_forward(self, t, slot):
     if self._iqn is not None:
       ex = self._iqn['target'][slot]
-      self._taus.draw(ex.taus)          # N' tau' (iqn:197-199) then K argmax samples (:200-204)
-      q, _ = ex.forward(t['next_state'])
+      self._taus.draw_cos(ex)           # N' tau' (iqn:197-199) then K argmax samples (:200-204)
+      q, _ = ex.forward(t['next_state'], cos_ready=True)
       npb = self.num_tau_prime_samples * self._batch_size
       out = {'tq': q[:npb]}
       if not self.double_dqn:
@@ -128,11 +129,11 @@ class ImplicitQuantileAgent(rainbow_agent.RainbowAgent):
     if self._iqn is not None:
       if ta is None:
         ex = self._iqn['online_next']
-        self._taus.draw(ex.taus)
-        ta, _ = ex.forward(t['next_state'])
+        self._taus.draw_cos(ex)
+        ta, _ = ex.forward(t['next_state'], cos_ready=True)
       on = self._iqn['online']
-      self._taus.draw(on.taus)
-      qv, taus = on.forward(t['state'])
+      self._taus.draw_cos(on)
+      qv, taus = on.forward(t['state'], cos_ready=True)
     else:
       if ta is None:
         with torch.no_grad():

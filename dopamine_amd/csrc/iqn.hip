@@ -37,15 +37,42 @@ constexpr int kSplitW1 = DQ_IQN_SPLIT_W1;   // dW1: K = R
 constexpr int kSplitWe = 8;       // dWe: K = R, 61 row tiles
 constexpr int kSplitW2 = 32;      // dW2: M = A, K = R
 
+__device__ __forceinline__ float uniform_of(uint64_t seed, int64_t call, int64_t i) {
+  // a splitmix64 hash of (seed, call, i), 24 random bits -> k * 2^-24
+  uint64_t z = seed + (uint64_t)call * 0x9E3779B97F4A7C15ull + (uint64_t)(i + 1) * 0xD1B54A32D192ED03ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(z >> 40) * (1.0f / 16777216.0f);
+}
+
+__device__ __forceinline__ float cos_feature(int k, float tau) {
+  const float pi = 3.14159265358979323846f;           // tf.constant(math.pi), float32
+  // tf.cast(tf.range(1, E + 1), float32) * pi * quantile_net, left to right, then tf.cos
+  return cosf(__fmul_rn(__fmul_rn((float)(k + 1), pi), tau));
+}
+
 __global__ __launch_bounds__(256) void k_cos_embedding(const float* __restrict__ tau, int64_t n,
                                                         int E, float* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t r = i / E;
+  out[i] = cos_feature((int)(i - r * E), tau[r]);
+}
+
+// tau (k_uniform_draw's draws of call counter[0]) and their cosine embedding in one launch
+// (the counter is bumped by the next launch, k_bump_counter: a last-block ticket on one
+// counter costs ~12 ns per arriving block, more than the launch it would save)
+__global__ __launch_bounds__(256) void k_tau_cos(const int64_t* __restrict__ counter, uint64_t seed,
+                                                 int64_t R, int E, float* __restrict__ tau_out,
+                                                 float* __restrict__ cos_out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= R * E) return;
+  const int64_t r = i / E;
   const int k = (int)(i - r * E);
-  const float pi = 3.14159265358979323846f;           // tf.constant(math.pi), float32
-  // tf.cast(tf.range(1, E + 1), float32) * pi * quantile_net, left to right, then tf.cos
-  out[i] = cosf(__fmul_rn(__fmul_rn((float)(k + 1), pi), tau[r]));
+  const float tau = uniform_of(seed, counter[0], r);
+  if (k == 0) tau_out[r] = tau;
+  cos_out[i] = cos_feature(k, tau);
 }
 
 // emb = relu(acc + be[n]) (kept for the backward if emb != null); x = state[r % B][n] * emb
@@ -115,7 +142,7 @@ __global__ __launch_bounds__(256) void k_tile_grad(const float* __restrict__ dtl
 void forward(Ctx& c, const dq_iqn_head* hp, int B, int nq, const float* state, const float* tau,
              const dq_iqn_acts* a) {
   const int R = nq * B, E = hp->embed_dim, A = hp->num_actions;
-  if (!c.dry) {
+  if (!c.dry && tau) {               // tau NULL: a->cos came with the draws (k_tau_cos)
     const int64_t n = (int64_t)R * E;
     hipLaunchKernelGGL(k_cos_embedding, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c.s, tau,
                        n, E, a->cos);
@@ -164,11 +191,7 @@ __global__ __launch_bounds__(256) void k_uniform_draw(const int64_t* __restrict_
                                                        float* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  uint64_t z = seed + (uint64_t)counter[0] * 0x9E3779B97F4A7C15ull + (uint64_t)(i + 1) * 0xD1B54A32D192ED03ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  out[i] = (float)(z >> 40) * (1.0f / 16777216.0f);
+  out[i] = uniform_of(seed, counter[0], i);
 }
 
 __global__ void k_bump_counter(int64_t* counter) { counter[0] += 1; }
@@ -187,7 +210,7 @@ extern "C" {
 
 int dq_iqn_head_forward(const dq_iqn_head* hp, int32_t batch, int32_t nq, const float* state,
                         const float* taus, dq_iqn_acts* a, float* ws, void* stream) {
-  DQ_CHECK_ARG(head_ok(hp) && state && taus && a && ws && batch >= 1 && nq >= 1, "bad arguments");
+  DQ_CHECK_ARG(head_ok(hp) && state && a && ws && batch >= 1 && nq >= 1, "bad arguments");
   DQ_CHECK_ARG(a->cos && a->x && a->h && a->q, "null activation buffer");
   DQ_CHECK_ARG((int64_t)batch * nq * iqn::F < ((int64_t)1 << 31), "R * 7744 must fit int32");
   cnn::Ctx c{(hipStream_t)stream, ws, false, 0};
@@ -218,6 +241,17 @@ int dq_uniform_draw(int64_t* counter, uint64_t seed, int64_t n, float* out, void
                        (hipStream_t)stream, counter, seed, n, out);
   hipLaunchKernelGGL(iqn::k_bump_counter, dim3(1), dim3(1), 0, (hipStream_t)stream, counter);
   DQ_CHECK_LAUNCH("dq_uniform_draw");
+  return DQ_OK;
+}
+
+int dq_iqn_tau_cos(int64_t* counter, uint64_t seed, int32_t rows, int32_t embed_dim, float* taus,
+                   float* cos_out, void* stream) {
+  DQ_CHECK_ARG(counter && taus && cos_out && rows >= 1 && embed_dim >= 1, "bad arguments");
+  const int64_t n = (int64_t)rows * embed_dim;
+  hipLaunchKernelGGL(iqn::k_tau_cos, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, counter, seed, (int64_t)rows, (int)embed_dim, taus, cos_out);
+  hipLaunchKernelGGL(iqn::k_bump_counter, dim3(1), dim3(1), 0, (hipStream_t)stream, counter);
+  DQ_CHECK_LAUNCH("dq_iqn_tau_cos");
   return DQ_OK;
 }
 

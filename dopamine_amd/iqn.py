@@ -41,6 +41,13 @@ class TauSampler(object):
               _lib.ptr(out), _stream(out.device))
     return out
 
+  def draw_cos(self, ex):
+    """draw(ex.taus) fused with their cosine embedding into ex.acts['cos']
+    (dq_iqn_tau_cos: the same draws, one launch); then ex.forward(x, cos_ready=True)."""
+    _lib.call('dq_iqn_tau_cos', _lib.ptr(self.counter), ctypes.c_uint64(self.seed), ex.R, ex.E,
+              _lib.ptr(ex.taus), _lib.ptr(ex.acts['cos']), _stream(ex.taus.device))
+    return ex.taus
+
 
 class HipIqnNet(object):
   """One (batch, nq) configuration of an ImplicitQuantileNetwork's parameters on the
@@ -69,9 +76,10 @@ class HipIqnNet(object):
     n = int(_lib.lib.dq_iqn_workspace_floats(self.B, self.nq, self.A, self.E))
     self.ws = mk(max(n, 1) + 64)
 
-  def forward(self, x, taus=None):
+  def forward(self, x, taus=None, cos_ready=False):
     """x: (B, 84, 84, 4) NHWC float32 (or its channels_last NCHW view); taus (R,) or
-    None (use self.taus as filled by the caller).  Returns (q (R, A), taus)."""
+    None (use self.taus as filled by the caller); cos_ready: acts['cos'] already holds
+    their embedding (TauSampler.draw_cos).  Returns (q (R, A), taus)."""
     x = self.torso._nhwc(x)
     self.torso._x = x
     t = self.torso
@@ -81,7 +89,8 @@ class HipIqnNet(object):
     if taus is not None and taus.data_ptr() != self.taus.data_ptr():
       self.taus.copy_(taus.reshape(-1))
     _lib.check(_lib.lib.dq_iqn_head_forward(ctypes.byref(self._p), self.B, self.nq,
-                                            t.acts['a3'].data_ptr(), self.taus.data_ptr(),
+                                            t.acts['a3'].data_ptr(),
+                                            None if cos_ready else self.taus.data_ptr(),
                                             ctypes.byref(self._a), self.ws.data_ptr(),
                                             _stream(self.device)), 'dq_iqn_head_forward')
     return self.acts['q'], self.taus

@@ -492,7 +492,8 @@ typedef struct dq_iqn_grads {
   float* dpre;                    /* (R, 7744) d loss / d (cos We^T + be) */
   float* dtl;                     /* (R, 7744) d loss / d tiled state */
 } dq_iqn_grads;
-/* forward: state = the torso's (B, 7744) output, taus (R). ws: dq_iqn_workspace_floats. */
+/* forward: state = the torso's (B, 7744) output, taus (R). ws: dq_iqn_workspace_floats.
+   taus NULL: a->cos already holds the cosine embedding (dq_iqn_tau_cos). */
 int dq_iqn_head_forward(const dq_iqn_head* hp, int32_t batch, int32_t nq, const float* state,
                         const float* taus, dq_iqn_acts* a, float* ws, void* stream);
 /* backward from dq = d loss / d q (R, A) (dq_iqn_loss): head weight / bias gradients into hg,
@@ -506,6 +507,11 @@ size_t dq_iqn_workspace_floats(int32_t batch, int32_t nq, int32_t num_actions, i
    generator `seed` (a splitmix64 hash of seed, call, index; 24 random bits), then
    counter[0] += 1 on the device -- graph replays continue the eager sequence. */
 int dq_uniform_draw(int64_t* counter, uint64_t seed, int64_t n, float* out, void* stream);
+/* dq_uniform_draw of `rows` taus (bitwise the same draws, then counter[0] += 1) fused with
+   their cosine embedding cos[r][i] = cos((i + 1) * pi * tau[r]) (atari_lib.py:176-178), for
+   dq_iqn_head_forward with taus NULL: two launches instead of three. */
+int dq_iqn_tau_cos(int64_t* counter, uint64_t seed, int32_t rows, int32_t embed_dim, float* taus,
+                   float* cos_out, void* stream);
 
 /* _build_sync_op (dqn_agent.py:324-339): online -> target copy of the flat buffer. */
 int dq_sync_copy(void* dst, const void* src, int64_t bytes, void* stream);
