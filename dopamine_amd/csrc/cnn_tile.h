@@ -195,6 +195,17 @@ struct ColK {
     return bload4(p, k * ld + r, r < rlim && k < klim);
   }
 };
+// RowK over rows taken b-major: GEMM row m = b * nq + q reads row q * B + b of p (the IQN
+// quantile rows are q-major), so a tile of 128 rows holds whole samples (nq | 128)
+struct RowKQ {
+  static constexpr bool kFast = true;
+  const float* p;
+  int ld, B, nq;
+  __device__ __forceinline__ float4 get(int m, int k, int rlim, int klim) const {
+    const int b = m / nq, r = (m - b * nq) * B + b;
+    return bload4(p, r * ld + k, m < rlim && k < klim);
+  }
+};
 // FC dW's B operand: B(n, k = batch) = x[k][n], with the bias ones-column at n == ld
 struct ColKOnes {
   static constexpr bool kFast = false;
@@ -445,6 +456,17 @@ struct HasVec {
 template <class EP>
 struct HasVec<EP, decltype((void)EP::kVec)> {
   static constexpr bool value = EP::kVec;
+};
+
+// EP::kBlock: the epilogue takes the block's whole (32 WM) x (32 WN) accumulator tile from
+// LDS (E.block(tile, ld, m0, n0, M, N), all threads), e.g. to reduce across rows
+template <class EP, class = void>
+struct HasBlock {
+  static constexpr bool value = false;
+};
+template <class EP>
+struct HasBlock<EP, decltype((void)EP::kBlock)> {
+  static constexpr bool value = EP::kBlock;
 };
 
 // host-side: EpiGrad, or EpiGradAdam / EpiGradRms with the optimizer slots of the same
@@ -728,6 +750,17 @@ __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& 
   }
   }
   // C/D layout of the 32x32 f32 MFMA: col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5)
+  if constexpr (HasBlock<EP>::value) {
+    static_assert(WK == 1, "block epilogues take whole tiles (WK == 1)");
+    // the block's tile -> LDS [BM][BN + 1] (the K loop's last barrier freed the staging)
+    constexpr int LDT = BN + 1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      smem[(wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * LDT + wn * 32 + (lane & 31)] = acc[r];
+    __syncthreads();
+    E.block(smem, LDT, m0, n0, M, N);
+    return;
+  }
   if constexpr (HasVec<EP>::value) {
     static_assert(WK == 1, "vector epilogues take whole tiles (WK == 1)");
     // the wave's tile -> its own LDS window (rows padded to 33), then 8 lanes per row
@@ -819,7 +852,9 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_igemm(AL A, BL B, EP E, i
                                                              int kchunk) {
   constexpr int kTile = Tile<WM, WN, WK>::template lds<AL, BL>();
   constexpr int kVecW = HasVec<EP>::value ? WM * WN * WK * 32 * 33 : 0;   // vector epilogue windows
-  __shared__ __attribute__((aligned(16))) float smem[kTile > kVecW ? kTile : kVecW];
+  constexpr int kBlkW = HasBlock<EP>::value ? 32 * WM * (32 * WN + 1) : 0;  // block epilogue tile
+  constexpr int kEpi = kVecW > kBlkW ? kVecW : kBlkW;
+  __shared__ __attribute__((aligned(16))) float smem[kTile > kEpi ? kTile : kEpi];
   igemm_block<WM, WN, WK>(A, B, E, M, N, K, kchunk, blockIdx.x, blockIdx.y, blockIdx.z, smem);
 }
 

@@ -128,6 +128,51 @@ struct EpiDx {
   }
 };
 
+// dX with the rows taken b-major (RowKQ, nq | 128): the block holds whole samples, so
+// tf.tile's gradient -- d state[b] = sum over q in order of dx * emb, then the torso's
+// last ReLU -- is summed in LDS and d tiled never goes to HBM (k_tile_grad's order and
+// arithmetic, without its 127 MB write + read and launch); d pre as EpiDx.
+struct EpiDxQ {
+  static constexpr bool kBlock = true;
+  float* dpre;
+  float* dstate;
+  const float* emb;
+  const float* state;
+  int B, nq;
+  // the per-element form is never reached (kBlock takes the block path); it only has to compile
+  __device__ __forceinline__ void operator()(int, int, float, int) const {}
+  __device__ __forceinline__ void block(float* T, int ldt, int m0, int n0, int M, int N) const {
+    constexpr int BM = 128, BN = 128;
+    for (int idx = threadIdx.x; idx < BM * BN / 4; idx += blockDim.x) {
+      const int t = idx / (BN / 4), c = 4 * (idx % (BN / 4));
+      const int m = m0 + t, n = n0 + c;
+      if (m >= M || n >= N) continue;
+      const int b = m / nq, r = (m - b * nq) * B + b;
+      const int64_t i = (int64_t)r * F + n;
+      const float4 e = ld4(emb + i), s = ld4(state + (int64_t)b * F + n);
+      float* v = T + t * ldt + c;
+      *reinterpret_cast<float4*>(dpre + i) =
+          make_float4(e.x > 0.0f ? __fmul_rn(v[0], s.x) : 0.0f, e.y > 0.0f ? __fmul_rn(v[1], s.y) : 0.0f,
+                      e.z > 0.0f ? __fmul_rn(v[2], s.z) : 0.0f, e.w > 0.0f ? __fmul_rn(v[3], s.w) : 0.0f);
+      v[0] = __fmul_rn(v[0], e.x);        // d tiled, kept in LDS
+      v[1] = __fmul_rn(v[1], e.y);
+      v[2] = __fmul_rn(v[2], e.z);
+      v[3] = __fmul_rn(v[3], e.w);
+    }
+    __syncthreads();
+    const int nb = BM / nq;
+    for (int j = threadIdx.x; j < nb * BN; j += blockDim.x) {
+      const int bl = j / BN, c = j - bl * BN;
+      const int b = m0 / nq + bl, n = n0 + c;
+      if (b * nq >= M || n >= N) continue;
+      float acc = 0.0f;
+      for (int q = 0; q < nq; ++q) acc = __fadd_rn(acc, T[(bl * nq + q) * ldt + c]);
+      const int64_t i = (int64_t)b * F + n;
+      dstate[i] = state[i] > 0.0f ? acc : 0.0f;
+    }
+  }
+};
+
 // tf.tile's gradient (the sum over the nq copies, q in order) and the torso's last ReLU
 __global__ __launch_bounds__(256) void k_tile_grad(const float* __restrict__ dtl,
                                                     const float* __restrict__ state, int B, int nq,
@@ -162,8 +207,16 @@ void backward(Ctx& c, const dq_iqn_head* hp, const dq_iqn_head* hg, int B, int n
   gemm<1, 1, 16>(c, RowKScalar{dq, A}, ColK{hp->fc2_w, H}, EpiMask{d->dh, a->h, H}, R, H, A);
   gemm<1, 4, 4>(c, ColKScalar{dq, A}, ColKOnes{a->h, H}, EpiGrad{hg->fc2_w, hg->fc2_b, H}, A,
                 H + 1, R, kSplitW2);
-  gemm<4, 4, 1>(c, RowK{d->dh, H}, ColK{hp->fc1_w, F}, EpiDx{d->dtl, d->dpre, a->emb, state, B},
-                R, F, H);
+  const bool fuse_tile = 128 % nq == 0;   // whole samples per 128-row tile
+  if (fuse_tile) {
+    if (!c.dry)
+      hipLaunchKernelGGL((k_igemm<4, 4, 1, RowKQ, ColK, EpiDxQ>), dim3((R + 127) / 128, (F + 127) / 128),
+                         dim3(1024), 0, c.s, RowKQ{d->dh, H, B, nq}, ColK{hp->fc1_w, F},
+                         EpiDxQ{d->dpre, dstate, a->emb, state, B, nq}, R, F, H, H);
+  } else {
+    gemm<4, 4, 1>(c, RowK{d->dh, H}, ColK{hp->fc1_w, F}, EpiDx{d->dtl, d->dpre, a->emb, state, B},
+                  R, F, H);
+  }
   gemm<4, 4, 1>(c, ColK{d->dh, H}, ColKOnes{a->x, F}, EpiGrad{hg->fc1_w, hg->fc1_b, F}, H, F + 1,
                 R, kSplitW1);
 #ifndef DQ_IQN_WE_NARROW
@@ -175,7 +228,7 @@ void backward(Ctx& c, const dq_iqn_head* hp, const dq_iqn_head* hg, int B, int n
   else
     gemm<4, 4, 1>(c, ColK{d->dpre, F}, ColKOnes{a->cos, E}, EpiGrad{hg->emb_w, hg->emb_b, E}, F,
                   E + 1, R, kSplitWe);
-  if (!c.dry) {
+  if (!c.dry && !fuse_tile) {
     const int64_t n = (int64_t)B * F;
     hipLaunchKernelGGL(k_tile_grad, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c.s, d->dtl,
                        state, B, nq, dstate);
