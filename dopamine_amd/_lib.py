@@ -130,6 +130,7 @@ SIGNATURES = {
     'dq_replay_read_meta': [_P, ctypes.POINTER(Meta), _P],
     'dq_replay_read_meta_async': [_P, _P, _P],
     'dq_replay_rewind_last_sample': [_P, _P],
+    'dq_replay_egreedy': [_P, _P, _I32, _D, _P, _P],
     'dq_replay_record_sumtree_set': [_P, _P, _P, _I64, ctypes.POINTER(Rider)],
     'dq_replay_record_sample': [_P, _I32, _P, ctypes.POINTER(Rider)],
     'dq_replay_record_gather_nhwc': [_P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P,

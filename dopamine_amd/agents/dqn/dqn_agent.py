@@ -15,6 +15,7 @@ import random
 import numpy as np
 import torch
 
+from dopamine_amd import _lib
 from dopamine_amd import ops
 from dopamine_amd import parallel
 from dopamine_amd.agents import networks
@@ -921,22 +922,48 @@ class DQNAgent(object):
     g.replay()
     return q
 
+  # Words reserved on the replay's RNG tape per device action: random.random() takes 2,
+  # randint's getrandbits rejection at most 2 per try (P(reject) < 1/2); 64 more cover it
+  # but for a (2^-64-rare) run, which falls back to the host draw.
+  _EGREEDY_WORDS = 66
+  device_egreedy = True
+
   def _select_action(self):
-    """dqn_agent.py:394-416.  The replay's RNG tape is brought in step first so
-    Python's `random` stream is consumed exactly as by the reference."""
+    """dqn_agent.py:394-416.  With a prioritized replay, whose sampler draws from Python's
+    `random` as epsilon-greedy does, the draws come from the replay's RNG tape on the
+    device (dq_replay_egreedy): the stream is consumed exactly as by the reference with no
+    host synchronisation per action.  Otherwise (or if the tape runs out) the tape is
+    brought in step and the host draws."""
     mem = self._replay.memory
-    if mem._rng.stream is random:   # PER samples from Python's `random`, as epsilon-greedy does
-      self._selects_since_train += 1
-      self._discard_prefetch()      # its draws would precede ours: give them back first
-      mem.sync_rng()
     if self.eval_mode:
       epsilon = self.epsilon_eval
     else:
       epsilon = self.epsilon_fn(self.epsilon_decay_period, self.training_steps,
                                 self.min_replay_history, self.epsilon_train)
+    if mem._rng.stream is random:   # PER samples from Python's `random`, as epsilon-greedy does
+      self._selects_since_train += 1
+      self._discard_prefetch()      # its draws would precede ours: give them back first
+      if self.device_egreedy:
+        a = self._select_action_device(mem, epsilon)
+        if a >= 0:
+          return a
+      mem.sync_rng()
     if random.random() <= epsilon:
       return random.randint(0, self.num_actions - 1)
     return int(torch.argmax(self._q_values(self.state), dim=1)[0].item())
+
+  def _select_action_device(self, mem, epsilon):
+    """The epsilon test, the explore draw and the greedy argmax as one kernel on the
+    tape (dq_replay_egreedy) after the Q-values; -1 if the tape ran out."""
+    mem._rng.reserve(self._EGREEDY_WORDS, mem._stream)
+    q = self._q_values(self.state).reshape(-1)
+    if q.dtype != torch.float32 or not q.is_contiguous():
+      q = q.float().contiguous()
+    if getattr(self, '_act_out', None) is None:
+      self._act_out = torch.empty(1, dtype=torch.int32, device=self._device)
+    _lib.call('dq_replay_egreedy', mem._h, _lib.ptr(q), self.num_actions, float(epsilon),
+              _lib.ptr(self._act_out), mem._stream)
+    return int(self._act_out.item())
 
   # ------------------------------------------------------ learner-only loop
   _UNROLL = 4

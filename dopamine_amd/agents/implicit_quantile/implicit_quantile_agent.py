@@ -48,6 +48,9 @@ class ImplicitQuantileAgent(rainbow_agent.RainbowAgent):
                      summary_writing_frequency=summary_writing_frequency, **kwargs)
 
   _loss_name = 'QuantileLoss'
+  # the act path's Q-values draw taus from the device counter, so evaluating them on every
+  # action (the device epsilon-greedy does) would move the tau stream: host draws here
+  device_egreedy = False
 
   def _make_network(self, seed):
     return self.network(self.num_actions, quantile_embedding_dim=self.quantile_embedding_dim,

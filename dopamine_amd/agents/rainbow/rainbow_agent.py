@@ -13,6 +13,7 @@ from dopamine_amd import ops
 from dopamine_amd.agents import networks
 from dopamine_amd.agents.dqn import dqn_agent
 from dopamine_amd.agents.optimizers import AdamOptimizer
+from dopamine_amd.replay_memory import circular_replay_buffer
 from dopamine_amd.replay_memory import prioritized_replay_buffer
 
 
@@ -205,11 +206,12 @@ class RainbowAgent(dqn_agent.DQNAgent):
       self._replay.tf_set_priority(t['indices'], self._loss_out['priorities'])
 
   def _store_transition(self, last_observation, action, reward, is_terminal, priority=None):
-    """rainbow_agent.py:307-337."""
+    """rainbow_agent.py:307-337.  The default prioritized-scheme priority, the sum tree's
+    max_recorded_priority, is read by the add kernel on the device (no host round trip)."""
     if priority is None:
       if self._replay_scheme == 'uniform':
         priority = 1.
       else:
-        priority = self._replay.memory.sum_tree.max_recorded_priority
+        priority = circular_replay_buffer.MAX_RECORDED
     if not self.eval_mode:
       self._replay.add(last_observation, action, reward, is_terminal, priority)

@@ -109,6 +109,44 @@ __global__ __launch_bounds__(256) void k_sumtree_sample(ReplayView v, int mode, 
 // lets a speculatively prefetched batch be re-drawn after adds / host RNG use.
 __global__ void k_rewind(dq_replay_meta* m) { m->tape_pos = m->reserved[0]; }
 
+// _select_action (dqn_agent.py:394-416) for a replay that samples from Python's `random`
+// (PER), on the tape: u = random.random() (genrand_res53, 2 words); u <= epsilon:
+// random.randint(0, A - 1) = Python's _randbelow(A): getrandbits(k = A.bit_length()) =
+// word >> (32 - k), redrawn while >= A; else the first argmax of q (dqn:416).  The tape
+// advances by exactly the words the reference consumes, so the host's `random` needs no
+// synchronisation per action.  A run past the tape consumes nothing and returns -1.
+__global__ void k_egreedy(dq_replay_meta* meta, const uint32_t* tape, const float* q, int A,
+                          double epsilon, int32_t* action) {
+  int64_t pos = meta->tape_pos;
+  const int64_t len = meta->tape_len;
+  int32_t a = -1;
+  if (meta->status == 0 && pos + 2 <= len) {
+    const double u = res53(tape[pos], tape[pos + 1]);
+    pos += 2;
+    if (u <= epsilon) {
+      const int k = 32 - __clz(A);
+      while (pos < len) {
+        const uint32_t r = tape[pos++] >> (32 - k);
+        if (r < (uint32_t)A) {
+          a = (int32_t)r;
+          break;
+        }
+      }
+    } else {
+      int best = 0;
+      float bq = q[0];
+      for (int j = 1; j < A; ++j)
+        if (q[j] > bq) {
+          bq = q[j];
+          best = j;
+        }
+      a = best;
+    }
+  }
+  if (a >= 0) meta->tape_pos = pos;
+  action[0] = a;
+}
+
 
 // NCHW float32: grid.y = (b, which, k) frame; each thread converts kGatherR dwords
 // strided by the block (kGatherR independent loads in flight before the stores;
@@ -419,11 +457,14 @@ int dq_replay_add(dq_replay* h, int64_t n, const uint8_t* frames, const int32_t*
   DQ_CHECK_ARG(!h->tree_only, "a standalone sum tree has no transition store");
   if (n == 0) return DQ_OK;
   DQ_CHECK_ARG(frames && actions && rewards && terminals, "null transition array");
-  DQ_CHECK_ARG(!h->cfg.prioritized || priorities, "prioritized add needs priorities");
+  DQ_CHECK_ARG(!h->cfg.prioritized || priorities || n == 1,
+               "prioritized add needs priorities (NULL: one transition at the max recorded one)");
   hipStream_t s = (hipStream_t)stream;
   ReplayView v = h->view();
   if (h->cfg.prioritized) {  // _add: sum_tree.set(cursor, p) before the write (prb:139)
-    SetArgs a{nullptr, priorities, n};
+    // priorities NULL: p = SumTree.max_recorded_priority as the set kernel finds it in the
+    // control block (float64, as rainbow_agent.py:331 reads it), no host round trip
+    SetArgs a{nullptr, priorities, n, priorities ? nullptr : &h->st.meta->max_recorded_priority};
     hipLaunchKernelGGL(k_sumtree_set, dim3(1), dim3(kTreeT), 0, s, v, a);
     DQ_CHECK_LAUNCH("k_sumtree_set");
   }
@@ -590,6 +631,16 @@ int dq_replay_rewind_last_sample(dq_replay* h, void* stream) {
   DQ_CHECK_ARG(h, "null handle");
   hipLaunchKernelGGL(k_rewind, dim3(1), dim3(1), 0, (hipStream_t)stream, h->st.meta);
   DQ_CHECK_LAUNCH("k_rewind");
+  return DQ_OK;
+}
+
+int dq_replay_egreedy(dq_replay* h, const float* q, int32_t num_actions, double epsilon,
+                      int32_t* action_out, void* stream) {
+  DQ_CHECK_ARG(h && q && action_out && num_actions >= 1, "bad arguments");
+  DQ_CHECK_ARG(h->st.tape, "RNG tape not attached");
+  hipLaunchKernelGGL(k_egreedy, dim3(1), dim3(1), 0, (hipStream_t)stream, h->st.meta,
+                     (const uint32_t*)h->st.tape, q, num_actions, epsilon, action_out);
+  DQ_CHECK_LAUNCH("k_egreedy");
   return DQ_OK;
 }
 

@@ -83,6 +83,15 @@ def _default_device(device):
   return torch.device('cuda', torch.cuda.current_device())
 
 
+class _MaxRecorded(float):
+  """The priority argument meaning "SumTree.max_recorded_priority at the time of the add"
+  (rainbow_agent.py:326-335 reads it on the host); the prioritized buffer resolves it on
+  the device for a single transition, so the add needs no host round trip."""
+
+
+MAX_RECORDED = _MaxRecorded(float('nan'))
+
+
 def _stream_handle(device):
   return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
@@ -293,6 +302,47 @@ class OutOfGraphReplayBuffer(object):
   def _priority_column(self, rows):
     return None
 
+  # add() of up to _STAGE_ROWS rows goes up as ONE asynchronous copy from a ring of pinned
+  # staging slots (obs | actions | rewards | terminals | priorities), so an env step never
+  # waits on the device queue (five pageable copies each did: ~110 us per add behind a
+  # training step); a slot is reused once its copy has run (event).
+  _STAGE_ROWS = 16
+  _STAGE_SLOTS = 8
+
+  def _stage_rows(self, obs, act, rew, term, prio):
+    n, ob = obs.shape[0], self._obs_bytes
+    up = lambda x: (x + 15) // 16 * 16
+    o_act = up(n * ob)
+    o_rew = o_act + up(4 * n)
+    o_term = o_rew + up(4 * n)
+    o_prio = o_term + up(n)
+    total = o_prio + up(4 * n)
+    if getattr(self, '_stage_host', None) is None:
+      R = self._STAGE_ROWS
+      cap = up(R * ob) + 3 * up(4 * R) + up(R)
+      self._stage_host = [torch.empty(cap, dtype=torch.uint8).pin_memory()
+                          for _ in range(self._STAGE_SLOTS)]
+      self._stage_ev = [None] * self._STAGE_SLOTS
+      self._stage_dev = torch.empty(cap, dtype=torch.uint8, device=self._device)
+      self._stage_i = 0
+    k = self._stage_i % self._STAGE_SLOTS
+    self._stage_i += 1
+    if self._stage_ev[k] is not None:
+      self._stage_ev[k].synchronize()
+    h = self._stage_host[k].numpy()
+    h[:n * ob] = obs.reshape(-1)
+    h[o_act:o_act + 4 * n] = np.ascontiguousarray(act, np.int32).view(np.uint8)
+    h[o_rew:o_rew + 4 * n] = np.ascontiguousarray(rew, np.float32).view(np.uint8)
+    h[o_term:o_term + n] = np.ascontiguousarray(term).view(np.uint8).reshape(-1)
+    if prio is not None:
+      h[o_prio:o_prio + 4 * n] = np.ascontiguousarray(prio, np.float32).view(np.uint8)
+    d = self._stage_dev
+    d[:total].copy_(self._stage_host[k][:total], non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(self._device))
+    self._stage_ev[k] = ev
+    return (d, d[o_act:], d[o_rew:], d[o_term:], None if prio is None else d[o_prio:])
+
   def _add_rows(self, rows):
     n = len(rows)
     obs = np.empty((n, self._obs_bytes), np.uint8)
@@ -317,14 +367,20 @@ class OutOfGraphReplayBuffer(object):
       term = (raw != 0).astype(np.uint8)
     else:
       term = raw.view(np.uint8)
-    prio = self._priority_column(rows)
+    prio = self._priority_column(rows)   # None, an array, or MAX_RECORDED (device-side max)
+    if prio is MAX_RECORDED:
+      prio = None                          # dq_replay_add: NULL = the max recorded priority
     dev = self._device
-    d_obs = torch.from_numpy(obs).to(dev, non_blocking=False)
-    d_act = torch.from_numpy(act).to(dev)
-    d_rew = torch.from_numpy(rew).to(dev)
-    d_term = torch.from_numpy(np.ascontiguousarray(term)).to(dev)
-    d_prio = torch.from_numpy(prio).to(dev) if prio is not None else None
-    if self._extra_storage_types or self._generic_action or self._generic_reward:
+    generic = self._extra_storage_types or self._generic_action or self._generic_reward
+    if not generic and n <= self._STAGE_ROWS and dev.type == 'cuda':
+      d_obs, d_act, d_rew, d_term, d_prio = self._stage_rows(obs, act, rew, term, prio)
+    else:
+      d_obs = torch.from_numpy(obs).to(dev, non_blocking=False)
+      d_act = torch.from_numpy(act).to(dev)
+      d_rew = torch.from_numpy(rew).to(dev)
+      d_term = torch.from_numpy(np.ascontiguousarray(term)).to(dev)
+      d_prio = torch.from_numpy(prio).to(dev) if prio is not None else None
+    if generic:
       slots = torch.tensor([(base + i) % self._replay_capacity for i in range(n)], device=dev)
       if self._generic_action and act_rows.shape[1]:
         self._act_rows[slots] = torch.from_numpy(act_rows).to(dev)

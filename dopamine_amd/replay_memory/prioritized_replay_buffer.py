@@ -31,7 +31,13 @@ class OutOfGraphPrioritizedReplayBuffer(circular_replay_buffer.OutOfGraphReplayB
     return super().get_add_args_signature() + [ReplayElement('priority', (), np.float32)]
 
   def _priority_column(self, rows):
-    return np.array([r[-1] for r in rows], dtype=np.float32)
+    pr = [r[-1] for r in rows]
+    if any(p is circular_replay_buffer.MAX_RECORDED for p in pr):
+      if len(pr) == 1:
+        return circular_replay_buffer.MAX_RECORDED      # read by the add kernel itself
+      m = self.sum_tree.max_recorded_priority           # padding rows too: the host value
+      pr = [m if p is circular_replay_buffer.MAX_RECORDED else p for p in pr]
+    return np.array(pr, dtype=np.float32)
 
   def get_transition_elements(self, batch_size=None):
     B = self._batch_size if batch_size is None else batch_size

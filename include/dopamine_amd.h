@@ -112,7 +112,9 @@ int dq_sumtree_create(int64_t capacity, double* tree, dq_replay_meta* meta, uint
 
 /* add() / _add() for n consecutive transitions at the cursor
  * (circular_replay_buffer.py:234-287, prioritized_replay_buffer.py:117-140).
- * Inputs are device arrays; priorities NULL for the uniform buffer.  Padding
+ * Inputs are device arrays; priorities NULL for the uniform buffer, or, for the
+ * prioritized one with n == 1, "the maximum priority recorded so far" read on the device
+ * (rainbow_agent.py:326-335: SumTree.max_recorded_priority as float64).  Padding
  * (zero transitions) is decided by the host, which passes them explicitly. */
 int dq_replay_add(dq_replay* h, int64_t n, const uint8_t* frames, const int32_t* actions,
                   const float* rewards, const uint8_t* terminals, const float* priorities,
@@ -190,6 +192,14 @@ int dq_replay_set_tape(dq_replay* h, int64_t len, void* stream);
  * redrawn when transitions were added or the host stream was used in between, so
  * the draw order stays the reference's. */
 int dq_replay_rewind_last_sample(dq_replay* h, void* stream);
+/* _select_action (dqn_agent.py:394-416) on the device for a buffer whose sampler draws from
+   Python's `random` (the prioritized one): the epsilon test random.random() <= epsilon and
+   the explore draw random.randint(0, num_actions - 1) consume the tape's next words exactly
+   as CPython would (genrand_res53; _randbelow by getrandbits(bit_length) rejection), else
+   the first argmax of q (num_actions floats, device); *action_out (device) = the action, or
+   -1 if the tape ran out (nothing consumed: sync and draw on the host). */
+int dq_replay_egreedy(dq_replay* h, const float* q, int32_t num_actions, double epsilon,
+                      int32_t* action_out, void* stream);
 /* synchronous: copies the control block to host memory. */
 int dq_replay_read_meta(dq_replay* h, dq_replay_meta* out, void* stream);
 /* the same copy, stream-ordered and NOT waited for: `out` must be pinned host memory and is

@@ -256,3 +256,41 @@ def test_learner_loop_chunks_equal_per_call_loop(kind):
       np.testing.assert_array_equal(x, y)
     else:
       assert x == y
+
+
+@pytest.mark.parametrize('kind', ['rainbow'])
+def test_device_epsilon_greedy_consumes_random_as_the_host_path(kind):
+  """_select_action with a prioritized replay: the epsilon test, the explore draw and the
+  greedy argmax as one kernel on the replay's RNG tape (dq_replay_egreedy) give the same
+  actions, batches, parameters and Python `random` state as the host path (sync + draw),
+  over 64 actions at epsilon 0.5 interleaved with adds and gradient steps."""
+  from dopamine_amd.agents.implicit_quantile.implicit_quantile_agent import ImplicitQuantileAgent
+  res = []
+  for dev in (False, True):
+    random.seed(13); np.random.seed(13); torch.manual_seed(13)
+    if kind == 'rainbow':
+      a = _rainbow(use_hip_graph=True)
+    else:
+      a = ImplicitQuantileAgent(num_actions=4, replay_capacity=3000, batch_size=16,
+                                num_tau_samples=8, num_tau_prime_samples=8, num_quantile_samples=4,
+                                min_replay_history=100, update_horizon=3)
+      _fill(a._replay.memory, 4, 3)
+    a.device_egreedy = dev
+    a.epsilon_fn = lambda *args: 0.5
+    rs = np.random.RandomState(0)
+    acts, idx = [], []
+    for i in range(64):
+      a.state = rs.randint(0, 256, (1, 84, 84, 4)).astype(np.float64)
+      acts.append(a._select_action())
+      if i % 4 == 3:
+        a._store_transition(np.full((84, 84), i, np.uint8), acts[-1], 0.5, False)
+        a._run_train_op()
+        idx.append(a._replay.transition['indices'].cpu().numpy().copy())
+    a._discard_prefetch()
+    a._replay.memory.sync_rng()
+    res.append((acts, np.stack(idx), random.getstate(), a.online_convnet.fp.flat.cpu().numpy()))
+  assert res[0][0] == res[1][0]
+  assert len(set(res[1][0])) > 1
+  np.testing.assert_array_equal(res[0][1], res[1][1])
+  assert res[0][2] == res[1][2]
+  np.testing.assert_array_equal(res[0][3], res[1][3])

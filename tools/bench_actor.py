@@ -16,7 +16,7 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 
 
-def run(kind, steps, train):
+def run(kind, steps, train, device_egreedy=True):
   from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
   from dopamine_amd.agents.rainbow.rainbow_agent import RainbowAgent
   from dopamine_amd.agents.optimizers import AdamOptimizer
@@ -30,6 +30,7 @@ def run(kind, steps, train):
                      device=dev)
   bench.fill_synthetic(agent._replay.memory, agent.num_actions, seed=1)
   agent.eval_mode = not train
+  agent.device_egreedy = device_egreedy
   rs = np.random.RandomState(0)
   frames = rs.randint(0, 256, (64, 84, 84)).astype(np.uint8)
   agent.begin_episode(frames[0])
@@ -49,6 +50,9 @@ def main():
   for kind in ('rainbow', 'dqn'):
     print('%-8s train: %8.1f env steps/s   eval (act only): %8.1f env steps/s' % (
         kind, run(kind, steps, True), run(kind, steps, False)))
+  # PER's epsilon-greedy draws on the host (sync + draw per action) instead of on the tape
+  print('%-8s train: %8.1f env steps/s   eval (act only): %8.1f env steps/s  (host epsilon-greedy)' % (
+      'rainbow', run('rainbow', steps, True, False), run('rainbow', steps, False, False)))
 
 
 if __name__ == '__main__':
