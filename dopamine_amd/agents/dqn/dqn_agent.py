@@ -395,11 +395,14 @@ class DQNAgent(object):
   # rider by an empty one -- the same launches without the gather's blocks, so the rider's
   # in-step cost can be read off the profile; the batches then go stale (wrong results).
   _SKIP_GATHER = os.environ.get('DQ_EXP_SKIP_GATHER') == '1'
+  # ... and DQ_EXP_SKIP_RIDERS=0,1 (recorded order: PER set, sample, gather) likewise
+  _SKIP_RIDERS = [int(x) for x in os.environ.get('DQ_EXP_SKIP_RIDERS', '').split(',') if x]
 
   def _place_riders(self, riders):
-    from dopamine_amd import _lib
     if self._SKIP_GATHER and riders:
       riders = riders[:-1] + [_lib.Rider()]
+    if self._SKIP_RIDERS and riders:
+      riders = [_lib.Rider() if i in self._SKIP_RIDERS else r for i, r in enumerate(riders)]
     if not self._GATHER_SHIFT or not riders:
       return riders
     return riders[:-1] + [_lib.Rider() for _ in range(self._GATHER_SHIFT)] + riders[-1:]
