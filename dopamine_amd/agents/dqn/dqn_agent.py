@@ -672,17 +672,12 @@ class DQNAgent(object):
       lo, n = self._shard_bounds()
       S = (n - lo) // self._world()
       r = torch.distributed.get_rank(self._pg)
+      # all three on the comm stream (1/N of the update is small beside the collectives;
+      # with the update on the second stream, comm -> comm_opt -> comm, the captured 4-step
+      # chunk graphs ended in a segfault at capture end on ROCm 7.2)
       with torch.cuda.stream(self._comm):
         parallel.reduce_scatter_mean_(grad[lo:n], self._pg)
-      e = torch.cuda.Event()
-      e.record(self._comm)
-      self._comm_opt.wait_event(e)
-      with torch.cuda.stream(self._comm_opt):
         self._opt.step_part(grad, lo + r * S, lo + (r + 1) * S, slot=k, bump=False)
-      e = torch.cuda.Event()
-      e.record(self._comm_opt)
-      self._comm.wait_event(e)
-      with torch.cuda.stream(self._comm):
         parallel.all_gather_(self._opt.params[lo:n], self._pg)
       conv, o = grad[:lo], lo                 # the head of the fc bucket joins the conv bucket
     else:
@@ -818,7 +813,9 @@ class DQNAgent(object):
           gr = None
           if fn is not None:
             gr = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gr, pool=pool):
+            # thread_local: the process group's watchdog may still be querying the events
+            # of the collectives issued just before (global mode fails its queries)
+            with torch.cuda.graph(gr, pool=pool, capture_error_mode='thread_local'):
               fn()
             pool = gr.pool()
           parts.append(gr)
@@ -829,7 +826,7 @@ class DQNAgent(object):
     for k in (0, 1):
       c = k
       g = torch.cuda.CUDAGraph()
-      with torch.cuda.graph(g, pool=pool):
+      with torch.cuda.graph(g, pool=pool, capture_error_mode='thread_local'):
         self._grad_step(c, k, pipe)
         if self._pg is None:
           self._device_opt_step(k)
@@ -838,7 +835,7 @@ class DQNAgent(object):
       graphs.append(g)
       if self._pg is not None:
         go = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(go, pool=pool):
+        with torch.cuda.graph(go, pool=pool, capture_error_mode='thread_local'):
           self._device_opt_step(k)
         graphs_opt.append(go)
     # capture records without executing: tape cursor and buffers are unchanged
@@ -1022,16 +1019,10 @@ class DQNAgent(object):
     if self._pg is None:
       return False
     import torch.distributed as dist
-    # ZeRO-1's reduce-scatter / all-gather replay as a captured 4-step chunk ended in a
-    # segfault at capture end on ROCm 7.2 (one-rank RCCL; the same collectives captured
-    # alone replay correctly, parallel.collectives_capturable(sharded=True)): the sharded
-    # path runs per-step graphs with its collectives issued between them
-    if self._sharded():
-      return False
     return (dist.get_backend(self._pg) == 'nccl' and self._split_allreduce() and
             self._head_splits() and isinstance(self._opt, ops.TF1Adam) and
             parallel.collectives_capturable(self._pg, self._device, self._comm,
-                                            sharded=False))
+                                            sharded=self._sharded()))
 
   def _chunks_apply(self):
     return (self._hip is not None and self.pipeline and

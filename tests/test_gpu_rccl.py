@@ -65,11 +65,13 @@ def test_rccl_one_rank_schedule_equals_single_learner_bitwise(rccl_group, loop):
 @pytest.mark.parametrize('loop', [False, True])
 def test_rccl_one_rank_sharded_optimizer_equals_single_learner_bitwise(rccl_group, loop):
   """ZeRO-1 over RCCL (in-place reduce-scatter, TF1 Adam on the rank's slice, in-place
-  all-gather, between the per-step graphs): one rank owns every slice, so the parameters
-  equal a single learner's bit for bit."""
+  all-gather; captured in the chunk graphs in the learner loop): one rank owns every
+  slice, so the parameters equal a single learner's bit for bit."""
   agent = _agent(rccl_group, 0, shard_optimizer=True)
   assert agent._sharded()
   flat = _run(agent, loop).numpy()
+  if loop:
+    assert any(k[0] == 'chunk' for k in agent._graph_sets if isinstance(k, tuple))
   single = _run(_agent(None, 0), loop).numpy()
   assert np.array_equal(flat, single)
 
