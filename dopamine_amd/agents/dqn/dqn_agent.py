@@ -682,10 +682,13 @@ class DQNAgent(object):
       conv, o = grad[:lo], lo                 # the head of the fc bucket joins the conv bucket
     else:
       pieces = self._fc_pieces(o, grad.numel()) if split_opt else [(o, grad.numel())]
+      one = len(pieces) == 1 and os.environ.get('DQ_EXP_FC_OPT_STREAM') != '1'
       for lo, hi in pieces:
         with torch.cuda.stream(self._comm):
           parallel.allreduce_mean_(grad[lo:hi], self._pg)
-        if split_opt:
+          if split_opt and one:     # one piece: its update right behind it, no second stream
+            self._opt.step_part(grad, lo, hi, slot=k, bump=False)
+        if split_opt and not one:
           e = torch.cuda.Event()
           e.record(self._comm)
           self._comm_opt.wait_event(e)
