@@ -1028,7 +1028,8 @@ class DQNAgent(object):
     return (dist.get_backend(self._pg) == 'nccl' and self._split_allreduce() and
             self._head_splits() and isinstance(self._opt, ops.TF1Adam) and
             parallel.collectives_capturable(self._pg, self._device, self._comm,
-                                            sharded=self._sharded()))
+                                            sharded=self._sharded(),
+                                            group2=self._conv_group()))
 
   def _chunks_apply(self):
     return (self._hip is not None and self.pipeline and

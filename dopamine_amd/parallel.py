@@ -85,14 +85,14 @@ def replicas_in_sync(flat_params, group=None):
 _CAPTURABLE = {}
 
 
-def collectives_capturable(group, device, stream=None, sharded=False):
+def collectives_capturable(group, device, stream=None, sharded=False, group2=None):
   """Whether every rank of ``group`` can capture this backend's all-reduce into a HIP
   graph and replay it correctly -- probed once per group on a small tensor, the ranks
   agreeing (eager MIN all-reduces) after each phase so no rank replays a collective the
   others did not capture.  False for gloo (host-side collectives).  The learner loop
   captures its all-reduces only where this holds, else it replays per-step graphs with
   the collectives issued between them."""
-  key = (id(group), bool(sharded))
+  key = (id(group), bool(sharded), id(group2) if group2 is not None else None)
   if key in _CAPTURABLE:
     return _CAPTURABLE[key]
   if dist.get_backend(group) != 'nccl':
@@ -107,33 +107,51 @@ def collectives_capturable(group, device, stream=None, sharded=False):
   rank = dist.get_rank(group)
   world = dist.get_world_size(group)
   x = torch.full((1024 * world,), float(rank + 1), device=device)
+  y = torch.full((1024,), float(rank + 1), device=device)
+  comm = stream or torch.cuda.Stream(device)
+  cap = torch.cuda.Stream(device)
 
-  def collectives():     # sharded: the ZeRO-1 pair (reduce-scatter, all-gather) as well
-    allreduce_mean_(x, group)
-    if sharded:
-      reduce_scatter_mean_(x, group)
-      all_gather_(x, group)
+  def collectives(origin):
+    """As the learner loop captures them: the fc bucket's collectives on the comm stream
+    forked from the origin stream and joined back (sharded: the ZeRO-1 pair as well),
+    the second communicator's all-reduce on the origin stream meanwhile."""
+    e = torch.cuda.Event()
+    e.record(origin)
+    comm.wait_event(e)
+    with torch.cuda.stream(comm):
+      allreduce_mean_(x, group)
+      if sharded:
+        reduce_scatter_mean_(x, group)
+        all_gather_(x, group)
+    if group2 is not None:
+      with torch.cuda.stream(origin):
+        allreduce_mean_(y, group2)
+    e = torch.cuda.Event()
+    e.record(comm)
+    origin.wait_event(e)
 
-  s = stream or torch.cuda.Stream(device)
   g = torch.cuda.CUDAGraph()
   ok = True
   try:
-    collectives()                                 # the communicator is warm before capture
+    collectives(torch.cuda.current_stream(device))   # the communicators are warm before capture
     torch.cuda.synchronize(device)
-    s.wait_stream(torch.cuda.current_stream(device))
-    with torch.cuda.stream(s):
-      with torch.cuda.graph(g, stream=s, capture_error_mode='thread_local'):
-        collectives()
+    cap.wait_stream(torch.cuda.current_stream(device))
+    with torch.cuda.stream(cap):
+      with torch.cuda.graph(g, stream=cap, capture_error_mode='thread_local'):
+        collectives(cap)
   except Exception:                               # noqa: BLE001 -- any failure means "no"
     ok = False
   ok = agree(ok)
   if ok:
     try:
       x.fill_(float(rank + 1))
+      y.fill_(float(rank + 1))
       g.replay()
       torch.cuda.synchronize(device)
       want = sum(range(1, world + 1)) / world if (world > 1 or FORCE_COLLECTIVES) else 1.0
       ok = bool(torch.allclose(x, torch.full_like(x, want)))
+      if group2 is not None:
+        ok = ok and bool(torch.allclose(y, torch.full_like(y, want)))
     except Exception:                             # noqa: BLE001
       ok = False
     ok = agree(ok)

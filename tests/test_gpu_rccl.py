@@ -82,6 +82,10 @@ def test_collective_capture_probe(rccl_group):
   parallel._CAPTURABLE.clear()
   assert parallel.collectives_capturable(rccl_group, torch.device('cuda', 0))
   assert parallel.collectives_capturable(rccl_group, torch.device('cuda', 0), sharded=True)
+  import torch.distributed as dist
+  second = dist.new_group(ranks=[0], backend='nccl')
+  assert parallel.collectives_capturable(rccl_group, torch.device('cuda', 0), sharded=True,
+                                         group2=second)
 
 
 def test_allreduce_mean_over_rccl_is_identity_for_one_rank(rccl_group):
