@@ -75,7 +75,40 @@ __global__ __launch_bounds__(256) void k_tau_cos(const int64_t* __restrict__ cou
   cos_out[i] = cos_feature(k, tau);
 }
 
+__device__ __forceinline__ float4 mul4(float4 a, float4 b) {
+  return make_float4(__fmul_rn(a.x, b.x), __fmul_rn(a.y, b.y), __fmul_rn(a.z, b.z), __fmul_rn(a.w, b.w));
+}
+
+// x = tiled state * emb (atari_lib.py:185) formed by the operand loaders from the kept emb
+// and the (B, 7744) state instead of read from a stored x: the online network's forward
+// then writes emb only (one 127 MB stream instead of two) and its FC1 forward / dW1 read
+// emb + state (L2-resident, 2 MB) in place of x -- the same products, bitwise.
+// FC1 forward's A operand: x[r][k..k+3]
+struct RowKHad {
+  static constexpr bool kFast = true;
+  const float* emb;
+  const float* state;
+  int B;
+  __device__ __forceinline__ float4 get(int r, int k, int rlim, int klim) const {
+    const bool ok = r < rlim && k < klim;
+    return mul4(bload4(state, (r % B) * F + k, ok), bload4(emb, r * F + k, ok));
+  }
+};
+// dW1's B operand (ColKOnes over x): B(n, k = quantile row) = x[k][n], ones column at n == F
+struct ColKOnesHad {
+  static constexpr bool kFast = false;
+  const float* emb;
+  const float* state;
+  int B;
+  __device__ __forceinline__ float4 get(int n, int k, int, int klim) const {
+    const bool ok = n < F && k < klim;
+    const float4 v = mul4(bload4(state, (k % B) * F + n, ok), bload4(emb, k * F + n, ok));
+    return (n == F && k < klim) ? make_float4(1.0f, 0.0f, 0.0f, 0.0f) : v;
+  }
+};
+
 // emb = relu(acc + be[n]) (kept for the backward if emb != null); x = state[r % B][n] * emb
+// (not stored if x == null: the loaders above form it)
 struct EpiEmb {
   float* emb;
   float* x;
@@ -87,10 +120,10 @@ struct EpiEmb {
     const float e = fmaxf(__fadd_rn(v, bias[n]), 0.0f);
     const int64_t i = (int64_t)m * F + n;
     if (emb) emb[i] = e;
-    x[i] = __fmul_rn(state[(int64_t)(m % B) * F + n], e);
+    if (x) x[i] = __fmul_rn(state[(int64_t)(m % B) * F + n], e);
   }
   __device__ __forceinline__ void vec4(int m, int n, float4 v) const {
-    const float4 b = ld4(bias + n), s = ld4(state + (int64_t)(m % B) * F + n);
+    const float4 b = ld4(bias + n);
     float4 e;
     e.x = fmaxf(__fadd_rn(v.x, b.x), 0.0f);
     e.y = fmaxf(__fadd_rn(v.y, b.y), 0.0f);
@@ -98,8 +131,7 @@ struct EpiEmb {
     e.w = fmaxf(__fadd_rn(v.w, b.w), 0.0f);
     const int64_t i = (int64_t)m * F + n;
     if (emb) *reinterpret_cast<float4*>(emb + i) = e;
-    *reinterpret_cast<float4*>(x + i) = make_float4(__fmul_rn(s.x, e.x), __fmul_rn(s.y, e.y),
-                                                    __fmul_rn(s.z, e.z), __fmul_rn(s.w, e.w));
+    if (x) *reinterpret_cast<float4*>(x + i) = mul4(ld4(state + (int64_t)(m % B) * F + n), e);
   }
 };
 
@@ -194,8 +226,12 @@ void forward(Ctx& c, const dq_iqn_head* hp, int B, int nq, const float* state, c
   }
   gemm<4, 4, 1>(c, RowK{a->cos, E}, RowK{hp->emb_w, E}, EpiEmb{a->emb, a->x, hp->emb_b, state, B},
                 R, F, E);
-  gemm<4, 4, 1>(c, RowK{a->x, F}, RowK{hp->fc1_w, F}, EpiBiasAct{a->h, hp->fc1_b, H, true}, R, H,
-                F, kSplitFc1);
+  if (a->x)
+    gemm<4, 4, 1>(c, RowK{a->x, F}, RowK{hp->fc1_w, F}, EpiBiasAct{a->h, hp->fc1_b, H, true}, R, H,
+                  F, kSplitFc1);
+  else                               // x formed from emb and state by the loader
+    gemm<4, 4, 1>(c, RowKHad{a->emb, state, B}, RowK{hp->fc1_w, F},
+                  EpiBiasAct{a->h, hp->fc1_b, H, true}, R, H, F, kSplitFc1);
   gemm<1, 1, 16>(c, RowK{a->h, H}, RowK{hp->fc2_w, H}, EpiBiasAct{a->q, hp->fc2_b, A, false}, R,
                  A, H);
 }
@@ -217,8 +253,12 @@ void backward(Ctx& c, const dq_iqn_head* hp, const dq_iqn_head* hg, int B, int n
     gemm<4, 4, 1>(c, RowK{d->dh, H}, ColK{hp->fc1_w, F}, EpiDx{d->dtl, d->dpre, a->emb, state, B},
                   R, F, H);
   }
-  gemm<4, 4, 1>(c, ColK{d->dh, H}, ColKOnes{a->x, F}, EpiGrad{hg->fc1_w, hg->fc1_b, F}, H, F + 1,
-                R, kSplitW1);
+  if (a->x)
+    gemm<4, 4, 1>(c, ColK{d->dh, H}, ColKOnes{a->x, F}, EpiGrad{hg->fc1_w, hg->fc1_b, F}, H,
+                  F + 1, R, kSplitW1);
+  else
+    gemm<4, 4, 1>(c, ColK{d->dh, H}, ColKOnesHad{a->emb, state, B},
+                  EpiGrad{hg->fc1_w, hg->fc1_b, F}, H, F + 1, R, kSplitW1);
 #ifndef DQ_IQN_WE_NARROW
 #define DQ_IQN_WE_NARROW 0
 #endif
@@ -264,7 +304,7 @@ extern "C" {
 int dq_iqn_head_forward(const dq_iqn_head* hp, int32_t batch, int32_t nq, const float* state,
                         const float* taus, dq_iqn_acts* a, float* ws, void* stream) {
   DQ_CHECK_ARG(head_ok(hp) && state && a && ws && batch >= 1 && nq >= 1, "bad arguments");
-  DQ_CHECK_ARG(a->cos && a->x && a->h && a->q, "null activation buffer");
+  DQ_CHECK_ARG(a->cos && (a->x || a->emb) && a->h && a->q, "null activation buffer");
   DQ_CHECK_ARG((int64_t)batch * nq * iqn::F < ((int64_t)1 << 31), "R * 7744 must fit int32");
   cnn::Ctx c{(hipStream_t)stream, ws, false, 0};
   iqn::forward(c, hp, batch, nq, state, taus, a);
@@ -279,7 +319,7 @@ int dq_iqn_head_backward(const dq_iqn_head* hp, const dq_iqn_head* hg, int32_t b
                nq >= 1, "bad arguments");
   DQ_CHECK_ARG(hg->embed_dim == hp->embed_dim && hg->num_actions == hp->num_actions,
                "gradient head shape differs");
-  DQ_CHECK_ARG(a->cos && a->emb && a->x && a->h && d->dh && d->dtl && d->dpre,
+  DQ_CHECK_ARG(a->cos && a->emb && a->h && d->dh && d->dtl && d->dpre,
                "the backward needs the forward's emb (kept) and gradient buffers");
   cnn::Ctx c{(hipStream_t)stream, ws, false, 0};
   iqn::backward(c, hp, hg, batch, nq, state, a, dq, d, dstate);

@@ -6,6 +6,7 @@ from a counter-based device generator, so a captured HIP graph draws exactly wha
 same calls draw eagerly.
 """
 import ctypes
+import os
 
 import torch
 
@@ -14,6 +15,7 @@ from dopamine_amd.cnn import HipNatureCNN
 
 _HEAD = ('emb_w', 'emb_b', 'fc1_w', 'fc1_b', 'fc2_w', 'fc2_b')
 F, H = 7744, 512
+_STORE_X = os.environ.get('DQ_IQN_STORE_X') == '1'    # A/B knob: the stored-x schedule
 
 
 def _head_struct(fp, buf, num_actions, embed_dim):
@@ -63,8 +65,11 @@ class HipIqnNet(object):
     mk = lambda *s: torch.empty(s, dtype=torch.float32, device=dev)
     self.torso = HipNatureCNN(net, self.B)
     R = self.R
-    self.acts = dict(cos=mk(R, self.E), emb=mk(R, F) if keep else None, x=mk(R, F), h=mk(R, H),
-                     q=mk(R, self.A))
+    # the online net keeps emb and never stores x = tiled state * emb: its FC1 forward and
+    # dW1 form x from emb and the state in their operand loaders (DQ_IQN_STORE_X=1: store it)
+    store_x = not keep or _STORE_X
+    self.acts = dict(cos=mk(R, self.E), emb=mk(R, F) if keep else None,
+                     x=mk(R, F) if store_x else None, h=mk(R, H), q=mk(R, self.A))
     self.taus = mk(R)
     self._a = _lib.IqnActs(**{k: (v.data_ptr() if v is not None else None)
                               for k, v in self.acts.items()})

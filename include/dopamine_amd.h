@@ -493,7 +493,9 @@ typedef struct dq_iqn_head {
 typedef struct dq_iqn_acts {
   float* cos;                     /* (R, E)    cos(pi * i * tau), i = 1..E   (atari_lib.py:176-178) */
   float* emb;                     /* (R, 7744) relu(cos We^T + be), kept for the backward; may be NULL */
-  float* x;                       /* (R, 7744) tiled state * emb             (atari_lib.py:185) */
+  float* x;                       /* (R, 7744) tiled state * emb             (atari_lib.py:185);
+                                     NULL with emb given: formed from emb and state by the FC1
+                                     forward / dW1 operand loaders (never stored) */
   float* h;                       /* (R, 512)  relu(x W1^T + b1) */
   float* q;                       /* (R, A)    quantile values              (atari_lib.py:189-191) */
 } dq_iqn_acts;

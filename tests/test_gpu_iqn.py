@@ -61,6 +61,37 @@ def test_iqn_executor_matches_float64(B, nq, A):
   assert max(errs.values()) <= TOL, errs
 
 
+@pytest.mark.parametrize('B,nq', [(64, 64), (3, 5)])
+def test_loader_formed_x_equals_stored_x_bitwise(B, nq, monkeypatch):
+  """The online net never stores x = tiled state * emb: the FC1 forward and dW1 loaders
+  form it from emb and the state.  Same quantile values and every gradient, bit for bit,
+  as the schedule that stores x and streams it (DQ_IQN_STORE_X=1)."""
+  from dopamine_amd import iqn
+  from dopamine_amd.agents.networks import ImplicitQuantileNetwork
+  torch.manual_seed(0)
+  net = ImplicitQuantileNetwork(4, device='cuda', seed=5)
+  with torch.no_grad():
+    for n in ('emb_b', 'fc1_b', 'fc2_b'):
+      net.fp[n].uniform_(-0.05, 0.05)
+  rs = np.random.RandomState(7)
+  x = torch.from_numpy(rs.randint(0, 256, (B, 84, 84, 4)).astype(np.float32) / np.float32(255)).cuda()
+  taus = torch.from_numpy(rs.rand(nq * B).astype(np.float32)).cuda()
+  dq = torch.from_numpy(rs.randn(nq * B, 4).astype(np.float32) / (nq * B)).cuda()
+  out = {}
+  for store in (True, False):
+    monkeypatch.setattr(iqn, '_STORE_X', store)
+    ex = iqn.HipIqnNet(net, B, nq, keep=True)
+    assert (ex.acts['x'] is None) != store
+    q, _ = ex.forward(x, taus)
+    h = ex.acts['h'].clone()
+    net.fp.grad.fill_(np.nan)
+    ex.backward(dq)
+    torch.cuda.synchronize()
+    out[store] = (q.cpu().numpy().copy(), h.cpu().numpy(), net.fp.grad.cpu().numpy().copy())
+  for a, b in zip(out[True], out[False]):
+    np.testing.assert_array_equal(a, b)
+
+
 def test_tau_sampler_is_uniform_and_replays_in_graphs():
   from dopamine_amd.iqn import TauSampler
   a = TauSampler(7, torch.device('cuda', 0))
