@@ -133,6 +133,7 @@ SIGNATURES = {
     'dq_replay_egreedy': [_P, _P, _I32, _D, _P, _P],
     'dq_replay_record_sumtree_set': [_P, _P, _P, _I64, ctypes.POINTER(Rider)],
     'dq_replay_record_sample': [_P, _I32, _P, ctypes.POINTER(Rider)],
+    'dq_rider_chain': [ctypes.POINTER(Rider), ctypes.POINTER(Rider), ctypes.POINTER(Rider)],
     'dq_replay_record_gather_nhwc': [_P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                      ctypes.POINTER(Rider)],
     'dq_c51_loss': [_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _F, _P, _P, _P, _P, _P],

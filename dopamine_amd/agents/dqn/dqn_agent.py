@@ -8,6 +8,7 @@ HIP kernel.  After a few eager warm-up steps the whole gradient step
 is captured into a HIP graph and replayed.  ``sess`` and ``tf_device`` are
 accepted for signature compatibility.
 """
+import ctypes
 import math
 import os
 import random
@@ -398,7 +399,16 @@ class DQNAgent(object):
   # ... and DQ_EXP_SKIP_RIDERS=0,1 (recorded order: PER set, sample, gather) likewise
   _SKIP_RIDERS = [int(x) for x in os.environ.get('DQ_EXP_SKIP_RIDERS', '').split(',') if x]
 
+  # DQ_SET_SAMPLE=1: PER write-back and next draw chained in ONE rider block of launch 1
+  # (dq_rider_chain), launch 2 rider-free, the gather in launch 3; =2: the gather in launch 2.
+  _SET_SAMPLE = int(os.environ.get('DQ_SET_SAMPLE', '0'))
+
   def _place_riders(self, riders):
+    if self._SET_SAMPLE and len(riders) == 3 and self._replay.memory._prioritized:
+      chained = _lib.Rider()
+      _lib.call('dq_rider_chain', ctypes.byref(riders[0]), ctypes.byref(riders[1]),
+                ctypes.byref(chained))
+      riders = [chained] + ([_lib.Rider()] if self._SET_SAMPLE == 1 else []) + riders[2:]
     if self._SKIP_GATHER and riders:
       riders = riders[:-1] + [_lib.Rider()]
     if self._SKIP_RIDERS and riders:

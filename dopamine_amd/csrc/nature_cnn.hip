@@ -1056,7 +1056,7 @@ int dq_cnn_backward_riders(const dq_cnn_params* p, const dq_cnn_params* g, int32
   RiderDesc r[7];
   for (int i = 0; i < n_riders; ++i) {
     memcpy(&r[i], &riders[i], sizeof(RiderDesc));
-    DQ_CHECK_ARG(r[i].kind >= kRiderNone && r[i].kind <= kRiderGatherNhwc, "corrupt rider");
+    DQ_CHECK_ARG(r[i].kind >= kRiderNone && r[i].kind <= kRiderSetSample, "corrupt rider");
   }
   FwdOps hf{};
   if (head) {

@@ -711,6 +711,22 @@ int dq_replay_record_gather_nhwc(dq_replay* h, const int32_t* indices, int32_t b
   return record(h, r, out);
 }
 
+int dq_rider_chain(const dq_rider* first, const dq_rider* second, dq_rider* out) {
+  DQ_CHECK_ARG(first && second && out, "null rider");
+  RiderDesc a, b;
+  memcpy(&a, first, sizeof(a));
+  memcpy(&b, second, sizeof(b));
+  DQ_CHECK_ARG(a.kind == kRiderSet && b.kind == kRiderPerSample,
+               "dq_rider_chain chains a sum-tree write-back and a prioritized sample");
+  DQ_CHECK_ARG(a.v.tree == b.v.tree && a.v.meta == b.v.meta, "riders of different buffers");
+  RiderDesc r = b;
+  r.kind = kRiderSetSample;
+  r.s = a.s;
+  memset(out, 0, sizeof(*out));
+  memcpy(out, &r, sizeof(r));
+  return DQ_OK;
+}
+
 int dq_sync_copy(void* dst, const void* src, int64_t bytes, void* stream) {
   DQ_CHECK_ARG(dst && src && bytes >= 0, "bad arguments");
   if (bytes == 0) return DQ_OK;

@@ -782,7 +782,7 @@ __device__ inline void per_sample_par(const ReplayView& v, int B, int32_t* out, 
 // opaque dq_rider of the C ABI): the sum-tree update, an index sample or the
 // NHWC gather, run by RiderOp (nature_cnn.hip) as extra blocks of a launch.
 enum RiderKind : int32_t { kRiderNone = 0, kRiderSet = 1, kRiderPerSample = 2,
-                           kRiderUniformSample = 3, kRiderGatherNhwc = 4 };
+                           kRiderUniformSample = 3, kRiderGatherNhwc = 4, kRiderSetSample = 5 };
 
 struct RiderDesc {
   int32_t kind;
@@ -808,6 +808,12 @@ __device__ __forceinline__ void run_rider(const RiderDesc& r, int blk, void* lds
       sumtree_set_par<T>(r.v, r.s, lds);
       return;
     case kRiderPerSample:
+      per_sample_par<T>(r.v, r.batch, r.out, lds);
+      return;
+    case kRiderSetSample:      // the write-back, then the next draw, in one block (dq_rider_chain)
+      sumtree_set_par<T>(r.v, r.s, lds);
+      __threadfence_block();
+      __syncthreads();         // the draw reads the nodes (and status) the write-back stored
       per_sample_par<T>(r.v, r.batch, r.out, lds);
       return;
     case kRiderUniformSample:

@@ -224,6 +224,11 @@ int dq_replay_record_gather_nhwc(dq_replay* h, const int32_t* indices, int32_t b
                                  float* reward_out, int32_t* next_action_out,
                                  float* next_reward_out, uint8_t* terminal_out,
                                  int32_t* indices_out, float* probs_out, dq_rider* out);
+/* One rider running `first` (a dq_replay_record_sumtree_set) and then `second` (a
+ * prioritized dq_replay_record_sample of the same buffer) in ONE block: the write-back
+ * (prioritized_replay_buffer.py:203-214) and the next stratified draw (:142-171) in their
+ * reference order, one launch instead of two. */
+int dq_rider_chain(const dq_rider* first, const dq_rider* second, dq_rider* out);
 
 /* ---------------- learner-side kernels (stateless) ---------------- */
 
