@@ -392,9 +392,6 @@ class DQNAgent(object):
   # write-back -> sample -> gather in consecutive backward launches; k > 0 moves the gather
   # k launches later (it must still precede the target head's first launch).
   _GATHER_SHIFT = int(os.environ.get('DQ_GATHER_SHIFT', '0'))
-  # Empty launches inserted before the whole chain (write-back, sample, gather each one
-  # launch later).
-  _RIDER_SHIFT = int(os.environ.get('DQ_RIDER_SHIFT', '0'))
   # Timing experiment only (tools/gpu_r2s3i.sh): DQ_EXP_SKIP_GATHER=1 replaces the gather
   # rider by an empty one -- the same launches without the gather's blocks, so the rider's
   # in-step cost can be read off the profile; the batches then go stale (wrong results).
@@ -416,8 +413,6 @@ class DQNAgent(object):
       riders = riders[:-1] + [_lib.Rider()]
     if self._SKIP_RIDERS and riders:
       riders = [_lib.Rider() if i in self._SKIP_RIDERS else r for i, r in enumerate(riders)]
-    if self._RIDER_SHIFT and riders:
-      riders = [_lib.Rider() for _ in range(self._RIDER_SHIFT)] + riders
     if not self._GATHER_SHIFT or not riders:
       return riders
     return riders[:-1] + [_lib.Rider() for _ in range(self._GATHER_SHIFT)] + riders[-1:]
