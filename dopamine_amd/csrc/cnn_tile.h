@@ -468,6 +468,14 @@ template <class EP>
 struct HasBlock<EP, decltype((void)EP::kBlock)> {
   static constexpr bool value = EP::kBlock;
 };
+template <class EP, class = void>
+struct BlockExtra {
+  static constexpr int value = 0;
+};
+template <class EP>
+struct BlockExtra<EP, decltype((void)EP::kBlockExtra)> {
+  static constexpr int value = EP::kBlockExtra;
+};
 
 // host-side: EpiGrad, or EpiGradAdam / EpiGradRms with the optimizer slots of the same
 // parameter.  kOpt: 0 none, 1 TF1 Adam, 2 TF1 RMSProp (a compile-time choice, so each
@@ -852,7 +860,8 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_igemm(AL A, BL B, EP E, i
                                                              int kchunk) {
   constexpr int kTile = Tile<WM, WN, WK>::template lds<AL, BL>();
   constexpr int kVecW = HasVec<EP>::value ? WM * WN * WK * 32 * 33 : 0;   // vector epilogue windows
-  constexpr int kBlkW = HasBlock<EP>::value ? 32 * WM * (32 * WN + 1) : 0;  // block epilogue tile
+  // block epilogue tile (+ EP::kBlockExtra floats of scratch after it)
+  constexpr int kBlkW = HasBlock<EP>::value ? 32 * WM * (32 * WN + 1) + BlockExtra<EP>::value : 0;
   constexpr int kEpi = kVecW > kBlkW ? kVecW : kBlkW;
   __shared__ __attribute__((aligned(16))) float smem[kTile > kEpi ? kTile : kEpi];
   igemm_block<WM, WN, WK>(A, B, E, M, N, K, kchunk, blockIdx.x, blockIdx.y, blockIdx.z, smem);

@@ -17,6 +17,7 @@
 //     dx   = dh W1  ->  d tiled = dx * emb,  d pre = (emb > 0) ? dx * state : 0     32.5 G
 //     dW1 | db1 = dh^T [x | 1]                                                     32.5 G
 //     dWe | dbe = dpre^T [cos | 1]                                                   4.1 G
+//       (dbe summed in the dX epilogue when nq | 128: dWe then a 128 x 64 tile, not 128 x 128)
 //     d state[b] = (state[b] > 0) * sum_q d tiled[q B + b]   (the torso's ReLU, then its backward)
 // The 7744-wide intermediates (emb, x, d tiled, d pre: 127 MB each at R = 4096) are
 // kept in HBM: each is written once and read by the next GEMM as a streamed operand.
@@ -164,10 +165,18 @@ struct EpiDx {
 // tf.tile's gradient -- d state[b] = sum over q in order of dx * emb, then the torso's
 // last ReLU -- is summed in LDS and d tiled never goes to HBM (k_tile_grad's order and
 // arithmetic, without its 127 MB write + read and launch); d pre as EpiDx.
+//
+// With dbe_part set it also sums the tile's d pre rows per column (the embedding's bias
+// gradient, dbe = sum over the R rows of d pre): each thread over its 4 rows, the wave's two
+// row groups by one lane exchange, the 16 waves' partials in LDS in wave order -> one row of
+// dbe_part (R/128, F) per block, summed over the row tiles in order by k_colsum.  dWe then
+// needs only the E cosine columns (a 128 x 64 tile instead of 128 x 128 for E + 1 = 65).
 struct EpiDxQ {
   static constexpr bool kBlock = true;
+  static constexpr int kBlockExtra = 16 * 128;   // per-wave column partials of d pre
   float* dpre;
   float* dstate;
+  float* dbe_part;
   const float* emb;
   const float* state;
   int B, nq;
@@ -175,6 +184,7 @@ struct EpiDxQ {
   __device__ __forceinline__ void operator()(int, int, float, int) const {}
   __device__ __forceinline__ void block(float* T, int ldt, int m0, int n0, int M, int N) const {
     constexpr int BM = 128, BN = 128;
+    float cs0 = 0.0f, cs1 = 0.0f, cs2 = 0.0f, cs3 = 0.0f;   // blockDim 1024: c is fixed per thread
     for (int idx = threadIdx.x; idx < BM * BN / 4; idx += blockDim.x) {
       const int t = idx / (BN / 4), c = 4 * (idx % (BN / 4));
       const int m = m0 + t, n = n0 + c;
@@ -183,15 +193,38 @@ struct EpiDxQ {
       const int64_t i = (int64_t)r * F + n;
       const float4 e = ld4(emb + i), s = ld4(state + (int64_t)b * F + n);
       float* v = T + t * ldt + c;
-      *reinterpret_cast<float4*>(dpre + i) =
+      const float4 dp =
           make_float4(e.x > 0.0f ? __fmul_rn(v[0], s.x) : 0.0f, e.y > 0.0f ? __fmul_rn(v[1], s.y) : 0.0f,
                       e.z > 0.0f ? __fmul_rn(v[2], s.z) : 0.0f, e.w > 0.0f ? __fmul_rn(v[3], s.w) : 0.0f);
+      *reinterpret_cast<float4*>(dpre + i) = dp;
+      cs0 = __fadd_rn(cs0, dp.x);
+      cs1 = __fadd_rn(cs1, dp.y);
+      cs2 = __fadd_rn(cs2, dp.z);
+      cs3 = __fadd_rn(cs3, dp.w);
       v[0] = __fmul_rn(v[0], e.x);        // d tiled, kept in LDS
       v[1] = __fmul_rn(v[1], e.y);
       v[2] = __fmul_rn(v[2], e.z);
       v[3] = __fmul_rn(v[3], e.w);
     }
+    float* P = T + BM * ldt;              // [16 waves][BN]
+    if (dbe_part) {
+      const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+      cs0 = __fadd_rn(cs0, __shfl_down(cs0, 32));
+      cs1 = __fadd_rn(cs1, __shfl_down(cs1, 32));
+      cs2 = __fadd_rn(cs2, __shfl_down(cs2, 32));
+      cs3 = __fadd_rn(cs3, __shfl_down(cs3, 32));
+      if (lane < 32)
+        *reinterpret_cast<float4*>(P + w * BN + 4 * lane) = make_float4(cs0, cs1, cs2, cs3);
+    }
     __syncthreads();
+    if (dbe_part && (int)threadIdx.x >= (int)blockDim.x - BN) {   // waves the q sums below leave idle
+      const int c = threadIdx.x - (blockDim.x - BN), n = n0 + c;
+      if (n < N) {
+        float acc = P[c];
+        for (int w = 1; w < 16; ++w) acc = __fadd_rn(acc, P[w * BN + c]);
+        dbe_part[(int64_t)(m0 / BM) * F + n] = acc;
+      }
+    }
     const int nb = BM / nq;
     for (int j = threadIdx.x; j < nb * BN; j += blockDim.x) {
       const int bl = j / BN, c = j - bl * BN;
@@ -214,6 +247,32 @@ __global__ __launch_bounds__(256) void k_tile_grad(const float* __restrict__ dtl
   float s = 0.0f;
   for (int q = 0; q < nq; ++q) s = __fadd_rn(s, dtl[(int64_t)q * B * F + i]);
   dstate[i] = state[i] > 0.0f ? s : 0.0f;
+}
+
+// dbe[n] = sum over the row tiles t, in order, of part[t][n]
+__global__ __launch_bounds__(256) void k_colsum(const float* __restrict__ part, int tiles, int n,
+                                                 float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float s = part[i];
+  for (int t0 = 1; t0 < tiles; t0 += 8) {     // 8 loads in flight, then the sums in order
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)min(t0 + u, tiles - 1) * n + i];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s = t0 + u < tiles ? __fadd_rn(s, v[u]) : s;
+  }
+  out[i] = s;
+}
+
+// dWe's schedule (DQ_IQN_WE): 1 (default) = 128 x 64 tiles over the E cosine columns with the
+// bias gradient from the dX epilogue's column partials; 0 = 128 x 128 tiles over [cos | 1]
+static int we_mode() {
+  static const int m = [] {
+    const char* e = getenv("DQ_IQN_WE");
+    return e ? atoi(e) : 1;
+  }();
+  return m;
 }
 
 void forward(Ctx& c, const dq_iqn_head* hp, int B, int nq, const float* state, const float* tau,
@@ -244,11 +303,15 @@ void backward(Ctx& c, const dq_iqn_head* hp, const dq_iqn_head* hg, int B, int n
   gemm<1, 4, 4>(c, ColKScalar{dq, A}, ColKOnes{a->h, H}, EpiGrad{hg->fc2_w, hg->fc2_b, H}, A,
                 H + 1, R, kSplitW2);
   const bool fuse_tile = 128 % nq == 0;   // whole samples per 128-row tile
+  // the bias gradient of the embedding from the dX epilogue (d tiled's buffer, unused when
+  // fuse_tile, holds the (R/128, F) column partials)
+  const bool we_narrow = fuse_tile && we_mode() == 1;
   if (fuse_tile) {
     if (!c.dry)
       hipLaunchKernelGGL((k_igemm<4, 4, 1, RowKQ, ColK, EpiDxQ>), dim3((R + 127) / 128, (F + 127) / 128),
                          dim3(1024), 0, c.s, RowKQ{d->dh, H, B, nq}, ColK{hp->fc1_w, F},
-                         EpiDxQ{d->dpre, dstate, a->emb, state, B, nq}, R, F, H, H);
+                         EpiDxQ{d->dpre, dstate, we_narrow ? d->dtl : nullptr, a->emb, state, B, nq},
+                         R, F, H, H);
   } else {
     gemm<4, 4, 1>(c, RowK{d->dh, H}, ColK{hp->fc1_w, F}, EpiDx{d->dtl, d->dpre, a->emb, state, B},
                   R, F, H);
@@ -262,7 +325,13 @@ void backward(Ctx& c, const dq_iqn_head* hp, const dq_iqn_head* hg, int B, int n
 #ifndef DQ_IQN_WE_NARROW
 #define DQ_IQN_WE_NARROW 0
 #endif
-  if (DQ_IQN_WE_NARROW)      // 128 x 32 tiles, K over 4 waves: 96 of 128 columns wasted -> 31
+  if (we_narrow) {           // dWe over the E cosine columns, dbe from the row-tile partials
+    gemm<4, 2, 2>(c, ColK{d->dpre, F}, ColK{a->cos, E}, EpiGrad{hg->emb_w, hg->emb_b, E}, F, E, R,
+                  kSplitWe);
+    if (!c.dry)
+      hipLaunchKernelGGL(k_colsum, dim3((F + 255) / 256), dim3(256), 0, c.s, d->dtl, (R + 127) / 128, F,
+                         hg->emb_b);
+  } else if (DQ_IQN_WE_NARROW)      // 128 x 32 tiles, K over 4 waves: 96 of 128 columns wasted -> 31
     gemm<4, 1, 4>(c, ColK{d->dpre, F}, ColKOnes{a->cos, E}, EpiGrad{hg->emb_w, hg->emb_b, E}, F,
                   E + 1, R, kSplitWe);
   else

@@ -25,6 +25,15 @@ def main():
   s = min(steps, key=lambda st: abs((st[-1][1] - st[0][0]) - med))
   t0 = s[0][0]
   print('%d steps; median step %.1f us (anchor %s)' % (len(steps), med / 1e3, anchor))
+  busy, cur = 0, None                  # the union of the step's kernel intervals (any queue)
+  for st, en in sorted((r[0], r[1]) for r in s):
+    if cur is None or st > cur[1]:
+      busy += 0 if cur is None else cur[1] - cur[0]
+      cur = [st, en]
+    else:
+      cur[1] = max(cur[1], en)
+  busy += cur[1] - cur[0]
+  print('GPU busy (some kernel running) %.1f of %.1f us' % (busy / 1e3, (s[-1][1] - s[0][0]) / 1e3))
   print('   start      dur      end  q  blocks  kernel')
   for st, en, n, q, gx, wx in s:
     print('%8.1f %8.1f %8.1f %2s %7d  %s' % ((st - t0) / 1e3, (en - st) / 1e3, (en - t0) / 1e3, q,
