@@ -864,7 +864,30 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_igemm(AL A, BL B, EP E, i
   constexpr int kBlkW = HasBlock<EP>::value ? 32 * WM * (32 * WN + 1) + BlockExtra<EP>::value : 0;
   constexpr int kEpi = kVecW > kBlkW ? kVecW : kBlkW;
   __shared__ __attribute__((aligned(16))) float smem[kTile > kEpi ? kTile : kEpi];
+#ifndef DQ_XCD_REMAP
+#define DQ_XCD_REMAP 0
+#endif
+#if DQ_XCD_REMAP
+  // XCD-aware tile order (a speed choice only): the dispatcher deals consecutive block ids
+  // round-robin over the 8 XCDs, so id % 8 labels the blocks that share an L2.  Give each
+  // such group a contiguous run of tiles (the bijective form for any grid size), ordered
+  // with the SHORTER of the two tile dimensions fastest, so the few tiles that read the same
+  // panel of the long operand (e.g. dW1's 4 row tiles over one column panel of x, FC1's 4
+  // column tiles over one row panel) run together on one XCD and share its L2.
+  // Measured OFF (0): IQN config 5 607-612 vs 614-620 steps/s plain, same box; no GEMM
+  // got faster in the serial timeline -- the operands already sit in the Infinity Cache
+  // and these fp32 tiles are matrix-core bound (profiles/r2_s5_xcd_remap_ab.log).
+  const unsigned nx = gridDim.x, ny = gridDim.y;
+  const unsigned nwg = nx * ny * gridDim.z;
+  const unsigned orig = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
+  const unsigned g = orig % 8, q = nwg / 8, r = nwg % 8;
+  const unsigned w = (g < r ? g * (q + 1) : r * (q + 1) + (g - r) * q) + orig / 8;
+  const unsigned z = w / (nx * ny), xy = w - z * nx * ny;
+  const unsigned bx = nx <= ny ? xy % nx : xy / ny, by = nx <= ny ? xy / nx : xy % ny;
+  igemm_block<WM, WN, WK>(A, B, E, M, N, K, kchunk, bx, by, z, smem);
+#else
   igemm_block<WM, WN, WK>(A, B, E, M, N, K, kchunk, blockIdx.x, blockIdx.y, blockIdx.z, smem);
+#endif
 }
 
 // ordered split-K sum + epilogue: element i of the (M x N) result, slab loads in flight together

@@ -1,0 +1,15 @@
+# XCD-aware tile order in k_igemm (DQ_XCD_REMAP, default on) vs the plain blockIdx order
+# (libdopamine_amd_noxcd.so, -DDQ_XCD_REMAP=0): IQN / CNN tests, then same-box alternating
+# config-5 and Rainbow lines
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+OUT=gpurun_out/r2s5d
+mkdir -p $OUT
+timeout -k 10 400 python -u -m pytest tests/test_gpu_iqn.py tests/test_gpu_cnn.py -m gpu -v --timeout 240 --timeout-method thread > $OUT/tests.log 2>&1 || exit 1
+for i in 1 2 3; do
+  timeout -k 10 200 python -u tools/bench_configs.py 150 iqn_breakout 2>&1 | tail -1 >> $OUT/remap.log || exit 1
+  DOPAMINE_AMD_LIB=$PWD/dopamine_amd/libdopamine_amd_noxcd.so timeout -k 10 200 python -u tools/bench_configs.py 150 iqn_breakout 2>&1 | tail -1 >> $OUT/plain.log || exit 1
+done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/prof5 -o run -- python3 tools/bench_configs.py 150 iqn_breakout pipeline=0 > $OUT/prof.log 2>&1 && \
+python3 tools/step_timeline_db.py /tmp/prof5/run_results.db k_iqn 30 > $OUT/step_timeline_one_stream.txt
