@@ -275,6 +275,18 @@ static int we_mode() {
   return m;
 }
 
+// FC1's split-K (DQ_IQN_SPLIT_FC1, default kSplitFc1): 128 x 128 tiles x splits blocks, two
+// 16-wave blocks per CU -- 4 fills the 512 slots once at R = 4096 and 1.5 times at R = 6144;
+// measured best (config 5: 4 -> 614-616, 6 -> 609-610, 8 -> 607-608 steps/s, whole rounds
+// lose to the extra slab traffic; profiles/r2_s5_iqn_fc1_split_ab.log)
+static int fc1_split() {
+  static const int s = [] {
+    const char* e = getenv("DQ_IQN_SPLIT_FC1");
+    return e ? atoi(e) : kSplitFc1;
+  }();
+  return s;
+}
+
 void forward(Ctx& c, const dq_iqn_head* hp, int B, int nq, const float* state, const float* tau,
              const dq_iqn_acts* a) {
   const int R = nq * B, E = hp->embed_dim, A = hp->num_actions;
@@ -287,10 +299,10 @@ void forward(Ctx& c, const dq_iqn_head* hp, int B, int nq, const float* state, c
                 R, F, E);
   if (a->x)
     gemm<4, 4, 1>(c, RowK{a->x, F}, RowK{hp->fc1_w, F}, EpiBiasAct{a->h, hp->fc1_b, H, true}, R, H,
-                  F, kSplitFc1);
+                  F, fc1_split());
   else                               // x formed from emb and state by the loader
     gemm<4, 4, 1>(c, RowKHad{a->emb, state, B}, RowK{hp->fc1_w, F},
-                  EpiBiasAct{a->h, hp->fc1_b, H, true}, R, H, F, kSplitFc1);
+                  EpiBiasAct{a->h, hp->fc1_b, H, true}, R, H, F, fc1_split());
   gemm<1, 1, 16>(c, RowK{a->h, H}, RowK{hp->fc2_w, H}, EpiBiasAct{a->q, hp->fc2_b, A, false}, R,
                  A, H);
 }
