@@ -135,22 +135,24 @@ def timed_steps(agent, steps, warmup, per_call=False, pg=None):
 
   gc.collect()
   gc.disable()
-  prime = 0
-  while ((not agent.graphs_primed() or prime + warmup < MIN_PRE_STEPS) and prime < 400):
-    grad_steps(5)
-    prime += 5
-  grad_steps(warmup)
-  torch.cuda.synchronize()
-  if pg is not None:
-    dist.barrier()
-  torch.cuda.synchronize()
-  t0 = time.perf_counter()
-  grad_steps(steps)
-  torch.cuda.synchronize()
-  if pg is not None:
-    dist.barrier()
-  elapsed = time.perf_counter() - t0
-  gc.enable()
+  try:
+    prime = 0
+    while ((not agent.graphs_primed() or prime + warmup < MIN_PRE_STEPS) and prime < 400):
+      grad_steps(5)
+      prime += 5
+    grad_steps(warmup)
+    torch.cuda.synchronize()
+    if pg is not None:
+      dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    grad_steps(steps)
+    torch.cuda.synchronize()
+    if pg is not None:
+      dist.barrier()
+    elapsed = time.perf_counter() - t0
+  finally:
+    gc.enable()
   return elapsed, prime
 
 
@@ -385,6 +387,9 @@ def main():
   loss = agent.mean_loss()
   assert np.isfinite(loss), 'non-finite loss'
 
+  default_schedule = (world == 1 and not args.force_dist and not args.per_call and
+                      not args.no_graph and args.fuse_opt is None and args.ride is None and
+                      args.split_c51 is None)
   graph_us, eager_us, algo_bytes, gname = time_gather(agent, args.gather_iters)
   large = time_gather_large(agent)
   traffic, traffic_src = gather_traffic(args.batch)
@@ -424,13 +429,15 @@ def main():
                      'algo_bytes_per_launch': algo_bytes,
                      'avg_launch_us': round(graph_us, 3), 'avg_launch_us_eager': round(eager_us, 3),
                      'same_kernel_batch_1024': large,
-                     # the same kernel riding in the step (not the measured launch above)
-                     'in_step_marginal': gather_in_step()},
+                     # the same kernel riding in the step (not the measured launch above):
+                     # a committed profile of the N = 1 default schedule, so only there
+                     'in_step_marginal': gather_in_step() if default_schedule else None},
         # supplementary: the whole step against the fp32 matrix peak (the CNN's fp32 MFMA
         # work; the step is launch- and latency-bound at B = 32, not MFMA-bound)
         'step_mfma': step_mfma(args.actions, args.batch, elapsed / args.steps),
         'cpu_baseline': cpu,
         'final_mean_loss': round(loss, 5),
+        'gc_disabled_in_timed_window': True,
         # supplementary: BASELINE configs 2 and 5 (N = 1), same protocol, not the metric
         'other_configs': configs,
     }

@@ -8,7 +8,6 @@ HIP kernel.  After a few eager warm-up steps the whole gradient step
 is captured into a HIP graph and replayed.  ``sess`` and ``tf_device`` are
 accepted for signature compatibility.
 """
-import ctypes
 import math
 import os
 import random
@@ -388,34 +387,11 @@ class DQNAgent(object):
     self._online_ready = on
     self._ptgt[c] = self._target_dict(tg)
 
-  # Empty launches inserted before the gather rider (the last recorded): 0 keeps the chain
-  # write-back -> sample -> gather in consecutive backward launches; k > 0 moves the gather
-  # k launches later (it must still precede the target head's first launch).
-  _GATHER_SHIFT = int(os.environ.get('DQ_GATHER_SHIFT', '0'))
-  # Timing experiment only (tools/gpu_r2s3i.sh): DQ_EXP_SKIP_GATHER=1 replaces the gather
-  # rider by an empty one -- the same launches without the gather's blocks, so the rider's
-  # in-step cost can be read off the profile; the batches then go stale (wrong results).
-  _SKIP_GATHER = os.environ.get('DQ_EXP_SKIP_GATHER') == '1'
-  # ... and DQ_EXP_SKIP_RIDERS=0,1 (recorded order: PER set, sample, gather) likewise
-  _SKIP_RIDERS = [int(x) for x in os.environ.get('DQ_EXP_SKIP_RIDERS', '').split(',') if x]
-
-  # DQ_SET_SAMPLE=1: PER write-back and next draw chained in ONE rider block of launch 1
-  # (dq_rider_chain), launch 2 rider-free, the gather in launch 3; =2: the gather in launch 2.
-  _SET_SAMPLE = int(os.environ.get('DQ_SET_SAMPLE', '0'))
-
   def _place_riders(self, riders):
-    if self._SET_SAMPLE and len(riders) == 3 and self._replay.memory._prioritized:
-      chained = _lib.Rider()
-      _lib.call('dq_rider_chain', ctypes.byref(riders[0]), ctypes.byref(riders[1]),
-                ctypes.byref(chained))
-      riders = [chained] + ([_lib.Rider()] if self._SET_SAMPLE == 1 else []) + riders[2:]
-    if self._SKIP_GATHER and riders:
-      riders = riders[:-1] + [_lib.Rider()]
-    if self._SKIP_RIDERS and riders:
-      riders = [_lib.Rider() if i in self._SKIP_RIDERS else r for i, r in enumerate(riders)]
-    if not self._GATHER_SHIFT or not riders:
-      return riders
-    return riders[:-1] + [_lib.Rider() for _ in range(self._GATHER_SHIFT)] + riders[-1:]
+    """Rider i rides in backward launch first + i, in the recorded order (PER write-back,
+    sample, gather).  Other placements were measured and not kept; a timing
+    experiment may override this method, never the product path."""
+    return riders
 
   def _forward_fused_c51(self, c, part=None):
     raise NotImplementedError
@@ -1151,10 +1127,12 @@ class DQNAgent(object):
 
   def bundle_and_checkpoint(self, checkpoint_dir, iteration_number):
     """dqn_agent.py:482-510 (torch tensors instead of a tf.train.Saver)."""
+    self._join_fc()
+    # ZeRO-1: complete moments on every rank -- a collective, so every rank reaches it
+    # before any rank-local early return
+    self._gather_opt_state()
     if not os.path.isdir(checkpoint_dir):
       return None
-    self._join_fc()
-    self._gather_opt_state()          # ZeRO-1: complete moments on every rank (collective)
     torch.save({k: v.detach().cpu() for k, v in self._ckpt_tensors().items()},
                os.path.join(checkpoint_dir, 'tf_ckpt-{}'.format(iteration_number)))
     stale = iteration_number - self.max_tf_checkpoints_to_keep

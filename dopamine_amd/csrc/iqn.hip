@@ -30,11 +30,11 @@ using namespace dq::cnn;
 
 constexpr int F = 11 * 11 * 64;   // 7744, the torso's state vector
 constexpr int H = 512;
-constexpr int kSplitFc1 = 4;      // h = relu(x W1^T + b1): K = 7744, 4 slabs (R/128 x 4 tiles x 4)
-#ifndef DQ_IQN_SPLIT_W1
-#define DQ_IQN_SPLIT_W1 2
-#endif
-constexpr int kSplitW1 = DQ_IQN_SPLIT_W1;   // dW1: K = R
+// h = relu(x W1^T + b1): K = 7744, 4 slabs (R/128 x 4 tiles x 4) -- two 16-wave blocks per
+// CU; 4 fills the 512 slots once at R = 4096 and 1.5 times at R = 6144, measured best
+// (config 5: 4 -> 614-616, 6 -> 609-610, 8 -> 607-608 steps/s, profiles/r2_s5_iqn_fc1_split_ab.log)
+constexpr int kSplitFc1 = 4;
+constexpr int kSplitW1 = 2;       // dW1: K = R (1 / 4 measured equal, profiles/r2_s5_iqn_dw1_split_ab.log)
 constexpr int kSplitWe = 8;       // dWe: K = R, 61 row tiles
 constexpr int kSplitW2 = 32;      // dW2: M = A, K = R
 
@@ -265,28 +265,6 @@ __global__ __launch_bounds__(256) void k_colsum(const float* __restrict__ part, 
   out[i] = s;
 }
 
-// dWe's schedule (DQ_IQN_WE): 1 (default) = 128 x 64 tiles over the E cosine columns with the
-// bias gradient from the dX epilogue's column partials; 0 = 128 x 128 tiles over [cos | 1]
-static int we_mode() {
-  static const int m = [] {
-    const char* e = getenv("DQ_IQN_WE");
-    return e ? atoi(e) : 1;
-  }();
-  return m;
-}
-
-// FC1's split-K (DQ_IQN_SPLIT_FC1, default kSplitFc1): 128 x 128 tiles x splits blocks, two
-// 16-wave blocks per CU -- 4 fills the 512 slots once at R = 4096 and 1.5 times at R = 6144;
-// measured best (config 5: 4 -> 614-616, 6 -> 609-610, 8 -> 607-608 steps/s, whole rounds
-// lose to the extra slab traffic; profiles/r2_s5_iqn_fc1_split_ab.log)
-static int fc1_split() {
-  static const int s = [] {
-    const char* e = getenv("DQ_IQN_SPLIT_FC1");
-    return e ? atoi(e) : kSplitFc1;
-  }();
-  return s;
-}
-
 void forward(Ctx& c, const dq_iqn_head* hp, int B, int nq, const float* state, const float* tau,
              const dq_iqn_acts* a) {
   const int R = nq * B, E = hp->embed_dim, A = hp->num_actions;
@@ -299,10 +277,10 @@ void forward(Ctx& c, const dq_iqn_head* hp, int B, int nq, const float* state, c
                 R, F, E);
   if (a->x)
     gemm<4, 4, 1>(c, RowK{a->x, F}, RowK{hp->fc1_w, F}, EpiBiasAct{a->h, hp->fc1_b, H, true}, R, H,
-                  F, fc1_split());
+                  F, kSplitFc1);
   else                               // x formed from emb and state by the loader
     gemm<4, 4, 1>(c, RowKHad{a->emb, state, B}, RowK{hp->fc1_w, F},
-                  EpiBiasAct{a->h, hp->fc1_b, H, true}, R, H, F, fc1_split());
+                  EpiBiasAct{a->h, hp->fc1_b, H, true}, R, H, F, kSplitFc1);
   gemm<1, 1, 16>(c, RowK{a->h, H}, RowK{hp->fc2_w, H}, EpiBiasAct{a->q, hp->fc2_b, A, false}, R,
                  A, H);
 }
@@ -317,7 +295,7 @@ void backward(Ctx& c, const dq_iqn_head* hp, const dq_iqn_head* hg, int B, int n
   const bool fuse_tile = 128 % nq == 0;   // whole samples per 128-row tile
   // the bias gradient of the embedding from the dX epilogue (d tiled's buffer, unused when
   // fuse_tile, holds the (R/128, F) column partials)
-  const bool we_narrow = fuse_tile && we_mode() == 1;
+  const bool we_narrow = fuse_tile;
   if (fuse_tile) {
     if (!c.dry)
       hipLaunchKernelGGL((k_igemm<4, 4, 1, RowKQ, ColK, EpiDxQ>), dim3((R + 127) / 128, (F + 127) / 128),
@@ -334,19 +312,13 @@ void backward(Ctx& c, const dq_iqn_head* hp, const dq_iqn_head* hg, int B, int n
   else
     gemm<4, 4, 1>(c, ColK{d->dh, H}, ColKOnesHad{a->emb, state, B},
                   EpiGrad{hg->fc1_w, hg->fc1_b, F}, H, F + 1, R, kSplitW1);
-#ifndef DQ_IQN_WE_NARROW
-#define DQ_IQN_WE_NARROW 0
-#endif
   if (we_narrow) {           // dWe over the E cosine columns, dbe from the row-tile partials
     gemm<4, 2, 2>(c, ColK{d->dpre, F}, ColK{a->cos, E}, EpiGrad{hg->emb_w, hg->emb_b, E}, F, E, R,
                   kSplitWe);
     if (!c.dry)
       hipLaunchKernelGGL(k_colsum, dim3((F + 255) / 256), dim3(256), 0, c.s, d->dtl, (R + 127) / 128, F,
                          hg->emb_b);
-  } else if (DQ_IQN_WE_NARROW)      // 128 x 32 tiles, K over 4 waves: 96 of 128 columns wasted -> 31
-    gemm<4, 1, 4>(c, ColK{d->dpre, F}, ColKOnes{a->cos, E}, EpiGrad{hg->emb_w, hg->emb_b, E}, F,
-                  E + 1, R, kSplitWe);
-  else
+  } else                     // 128 x 128 tiles over [cos | 1]
     gemm<4, 4, 1>(c, ColK{d->dpre, F}, ColKOnes{a->cos, E}, EpiGrad{hg->emb_w, hg->emb_b, E}, F,
                   E + 1, R, kSplitWe);
   if (!c.dry && !fuse_tile) {

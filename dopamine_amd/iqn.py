@@ -6,7 +6,6 @@ from a counter-based device generator, so a captured HIP graph draws exactly wha
 same calls draw eagerly.
 """
 import ctypes
-import os
 
 import torch
 
@@ -15,7 +14,6 @@ from dopamine_amd.cnn import HipNatureCNN
 
 _HEAD = ('emb_w', 'emb_b', 'fc1_w', 'fc1_b', 'fc2_w', 'fc2_b')
 F, H = 7744, 512
-_STORE_X = os.environ.get('DQ_IQN_STORE_X') == '1'    # A/B knob: the stored-x schedule
 
 
 def _head_struct(fp, buf, num_actions, embed_dim):
@@ -53,9 +51,11 @@ class TauSampler(object):
 
 class HipIqnNet(object):
   """One (batch, nq) configuration of an ImplicitQuantileNetwork's parameters on the
-  HIP kernels.  ``keep``: keep what the backward needs (the online network)."""
+  HIP kernels.  ``keep``: keep what the backward needs (the online network).
+  ``store_x``: the online net stores x = tiled state * emb and streams it (the stored-x
+  schedule, bitwise the default, which forms x in the FC1 / dW1 operand loaders)."""
 
-  def __init__(self, net, batch_size, nq, keep=True):
+  def __init__(self, net, batch_size, nq, keep=True, store_x=False):
     fp = net.fp
     self.net, self.B, self.nq, self.keep = net, int(batch_size), int(nq), bool(keep)
     self.A, self.E = int(net.A), int(net.E)
@@ -66,8 +66,8 @@ class HipIqnNet(object):
     self.torso = HipNatureCNN(net, self.B)
     R = self.R
     # the online net keeps emb and never stores x = tiled state * emb: its FC1 forward and
-    # dW1 form x from emb and the state in their operand loaders (DQ_IQN_STORE_X=1: store it)
-    store_x = not keep or _STORE_X
+    # dW1 form x from emb and the state in their operand loaders
+    store_x = not keep or store_x
     self.acts = dict(cos=mk(R, self.E), emb=mk(R, F) if keep else None,
                      x=mk(R, F) if store_x else None, h=mk(R, H), q=mk(R, self.A))
     self.taus = mk(R)

@@ -132,9 +132,11 @@ def collectives_capturable(group, device, stream=None, sharded=False, group2=Non
 
   g = torch.cuda.CUDAGraph()
   ok = True
+  # the communicators are warm before capture; eager collectives outside the try, so a
+  # failure there is fatal on every rank instead of one rank leaving the others blocked
+  collectives(torch.cuda.current_stream(device))
+  torch.cuda.synchronize(device)
   try:
-    collectives(torch.cuda.current_stream(device))   # the communicators are warm before capture
-    torch.cuda.synchronize(device)
     cap.wait_stream(torch.cuda.current_stream(device))
     with torch.cuda.stream(cap):
       with torch.cuda.graph(g, stream=cap, capture_error_mode='thread_local'):

@@ -9,6 +9,7 @@ include/dopamine_amd.h.  Numpy-returning methods (``sample_transition_batch``
 etc.) synchronise and return exactly what the reference returns; the learner
 uses ``sample_device`` which stays on the device and never synchronises.
 """
+import codecs
 import collections
 import contextlib
 import ctypes
@@ -34,10 +35,21 @@ class _ReferenceSumTree(object):
   SumTree): only its fields (``nodes``, ``max_recorded_priority``) are restored."""
 
 
+def _allowed_reconstructor(cls, base, state):
+  """copyreg._reconstructor (protocol 0 / 1 object pickles, e.g. a Python 2-era reference's
+  SumTree) restricted to the whitelisted classes built on ``object``."""
+  if cls not in _CheckpointUnpickler._ALLOWED.values() or base is not object:
+    raise pickle.UnpicklingError('replay checkpoint reconstructs {} on {}: not an allowed '
+                                 'type'.format(cls, base))
+  return object.__new__(cls)
+
+
 class _CheckpointUnpickler(pickle.Unpickler):
   """Unpickles replay checkpoint members with a class whitelist: the reference's and
   this package's sum-tree snapshots and numpy's array / scalar reconstructors.
-  Anything else (a callable a crafted file could name) is refused."""
+  Anything else (a callable a crafted file could name) is refused.  Every pickle
+  protocol loads: 0 / 1 (copyreg._reconstructor, restricted above), 2-4 (the reference's
+  default under Python 3, crb:643) and 5 (numpy arrays through _frombuffer)."""
 
   _ALLOWED = {
       ('dopamine.replay_memory.sum_tree', 'SumTree'): _ReferenceSumTree,
@@ -55,6 +67,14 @@ class _CheckpointUnpickler(pickle.Unpickler):
     if module in ('numpy.core.multiarray', 'numpy._core.multiarray') and name in ('_reconstruct',
                                                                                   'scalar'):
       return getattr(np._core.multiarray if hasattr(np, '_core') else np.core.multiarray, name)
+    if module in ('numpy.core.numeric', 'numpy._core.numeric') and name == '_frombuffer':
+      return getattr(np._core.numeric if hasattr(np, '_core') else np.core.numeric, name)
+    if key in (('copyreg', '_reconstructor'), ('copy_reg', '_reconstructor')):
+      return _allowed_reconstructor
+    if key in (('builtins', 'object'), ('__builtin__', 'object')):
+      return object
+    if key == ('_codecs', 'encode'):    # bytes in protocol 0-2 pickles (numpy's raw data)
+      return codecs.encode
     raise pickle.UnpicklingError('replay checkpoint names {}.{}: not an allowed type'.format(
         module, name))
 

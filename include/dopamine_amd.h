@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define DQ_ABI_VERSION 1
+#define DQ_ABI_VERSION 2
 
 /* host-side return codes */
 #define DQ_OK 0

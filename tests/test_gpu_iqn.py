@@ -62,10 +62,10 @@ def test_iqn_executor_matches_float64(B, nq, A):
 
 
 @pytest.mark.parametrize('B,nq', [(64, 64), (3, 5)])
-def test_loader_formed_x_equals_stored_x_bitwise(B, nq, monkeypatch):
+def test_loader_formed_x_equals_stored_x_bitwise(B, nq):
   """The online net never stores x = tiled state * emb: the FC1 forward and dW1 loaders
   form it from emb and the state.  Same quantile values and every gradient, bit for bit,
-  as the schedule that stores x and streams it (DQ_IQN_STORE_X=1)."""
+  as the schedule that stores x and streams it (store_x=True)."""
   from dopamine_amd import iqn
   from dopamine_amd.agents.networks import ImplicitQuantileNetwork
   torch.manual_seed(0)
@@ -79,8 +79,7 @@ def test_loader_formed_x_equals_stored_x_bitwise(B, nq, monkeypatch):
   dq = torch.from_numpy(rs.randn(nq * B, 4).astype(np.float32) / (nq * B)).cuda()
   out = {}
   for store in (True, False):
-    monkeypatch.setattr(iqn, '_STORE_X', store)
-    ex = iqn.HipIqnNet(net, B, nq, keep=True)
+    ex = iqn.HipIqnNet(net, B, nq, keep=True, store_x=store)
     assert (ex.acts['x'] is None) != store
     q, _ = ex.forward(x, taus)
     h = ex.acts['h'].clone()
