@@ -55,9 +55,14 @@ def parse():
   ap.add_argument('--split-c51', type=int, default=None,
                   help='override RainbowAgent.split_c51 (0/1): the C51 target half riding in '
                        'the forward (head_from 8) or inside the loss kernel')
-  ap.add_argument('--zero', type=int, default=0,
-                  help='N > 1: ZeRO-1 for the fc bucket (DQNAgent shard_optimizer): '
-                       'reduce-scatter, TF1 Adam on the rank\'s slice, all-gather (0/1)')
+  ap.add_argument('--zero', type=int, default=None,
+                  help='N > 1: time only the replicated all-reduce schedule (0) or only ZeRO-1 '
+                       'for the fc bucket (1: DQNAgent shard_optimizer -- reduce-scatter, TF1 '
+                       'Adam on the rank\'s slice, all-gather); default: both, headline from the '
+                       'faster')
+  ap.add_argument('--comm', choices=('native', 'torch'), default='native',
+                  help='N > 1 over RCCL: the learner\'s own communicators (parallel.RcclComm) '
+                       'or torch.distributed\'s collectives')
   ap.add_argument('--force-dist', action='store_true',
                   help='one rank only: run the N > 1 learner schedule over a one-rank RCCL group '
                        'with every collective executed (a hardware check of the data-parallel '
@@ -368,24 +373,48 @@ def main():
   if args.split_c51 is not None:
     from dopamine_amd.agents.rainbow.rainbow_agent import RainbowAgent
     RainbowAgent.split_c51 = bool(args.split_c51)
-  agent = build_agent(args.actions, args.capacity, args.batch, dev, pg=pg,
-                      use_hip_graph=not args.no_graph,
-                      **({} if args.fuse_opt is None else {'fuse_optimizer': bool(args.fuse_opt)}),
-                      **({} if args.ride is None else {'ride_replay': bool(args.ride)}),
-                      **({'shard_optimizer': True} if args.zero else {}))
-  import random
-  random.seed(0 + rank)
-  fill_synthetic(agent._replay.memory, args.actions, seed=1 + rank)
-  torch.cuda.synchronize()
-
-  elapsed, prime = timed_steps(agent, args.steps, args.warmup, args.per_call, pg)
-  if pg is not None:
-    t = torch.tensor([elapsed], dtype=torch.float64, device='cpu' if rehearse else dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
-  agent._replay.memory.sync_rng()   # raises if the device latched a sampling error
-  loss = agent.mean_loss()
-  assert np.isfinite(loss), 'non-finite loss'
+  # N > 1: the replicated all-reduce schedule and ZeRO-1 are both timed, one
+  # after the other on fresh agents, and the headline is the faster (both are reported)
+  zeros = [0, 1] if (pg is not None and args.zero is None) else [int(args.zero or 0)]
+  schedules = {}
+  agent = None
+  for zero in zeros:
+    if agent is not None:
+      del agent
+      gc.collect()
+      torch.cuda.empty_cache()
+    agent = build_agent(args.actions, args.capacity, args.batch, dev, pg=pg,
+                        use_hip_graph=not args.no_graph, native_comm=args.comm == 'native',
+                        **({} if args.fuse_opt is None else {'fuse_optimizer': bool(args.fuse_opt)}),
+                        **({} if args.ride is None else {'ride_replay': bool(args.ride)}),
+                        **({'shard_optimizer': True} if zero else {}))
+    import random
+    random.seed(0 + rank)
+    fill_synthetic(agent._replay.memory, args.actions, seed=1 + rank)
+    torch.cuda.synchronize()
+    elapsed, prime = timed_steps(agent, args.steps, args.warmup, args.per_call, pg)
+    per_rank = [elapsed]
+    if pg is not None:
+      t = torch.zeros(dist.get_world_size(pg), dtype=torch.float64,
+                      device='cpu' if rehearse else dev)
+      t[dist.get_rank(pg)] = elapsed
+      dist.all_reduce(t, op=dist.ReduceOp.SUM)
+      per_rank = [float(x) for x in t.cpu()]
+      elapsed = max(per_rank)
+    agent._replay.memory.sync_rng()   # raises if the device latched a sampling error
+    loss = agent.mean_loss()
+    assert np.isfinite(loss), 'non-finite loss'
+    schedules['zero1' if zero else 'allreduce'] = {
+        'value': round(world * args.steps / elapsed, 2), 'ms_per_step': round(1e3 * elapsed / args.steps, 4),
+        'per_rank_ms_per_step': [round(1e3 * e / args.steps, 4) for e in per_rank],
+        'prime_steps': prime, 'final_mean_loss': round(loss, 5), '_elapsed': elapsed,
+        'comm': (args.comm if agent._rccl is not None or args.comm == 'torch' else 'torch')
+        if pg is not None else None}
+  best = min(schedules, key=lambda k: schedules[k]['_elapsed'])
+  elapsed, prime, loss = (schedules[best]['_elapsed'], schedules[best]['prime_steps'],
+                          schedules[best]['final_mean_loss'])
+  for v in schedules.values():
+    del v['_elapsed']
 
   default_schedule = (world == 1 and not args.force_dist and not args.per_call and
                       not args.no_graph and args.fuse_opt is None and args.ride is None and
@@ -420,7 +449,7 @@ def main():
                    'replay_capacity': args.capacity,
                    'parallelism': 'dp%d' % world + (' (one-rank RCCL group, --force-dist)'
                                                     if args.force_dist and world == 1 else '')
-                                  + (', ZeRO-1 fc bucket' if args.zero else ''),
+                                  + (', ZeRO-1 fc bucket' if best == 'zero1' else ''),
                    'hip_graph': not args.no_graph},
         'roofline': {'kernel': gname + ' (frame-stack gather + /255, state+next_state)',
                      'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
@@ -438,6 +467,8 @@ def main():
         'cpu_baseline': cpu,
         'final_mean_loss': round(loss, 5),
         'gc_disabled_in_timed_window': True,
+        # N > 1 (or --force-dist): every data-parallel schedule timed, the headline the faster
+        'schedules': schedules if pg is not None else None,
         # supplementary: BASELINE configs 2 and 5 (N = 1), same protocol, not the metric
         'other_configs': configs,
     }

@@ -5,7 +5,7 @@ import subprocess
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # DOPAMINE_AMD_LIB: an alternate in-tree build of the same library (A/B experiments)
 LIB_PATH = os.environ.get('DOPAMINE_AMD_LIB') or os.path.join(_HERE, 'libdopamine_amd.so')
-SOURCES = [os.path.join(_HERE, 'csrc', f) for f in ('replay.hip', 'learner.hip', 'nature_cnn.hip', 'iqn.hip')]
+SOURCES = [os.path.join(_HERE, 'csrc', f) for f in ('replay.hip', 'learner.hip', 'nature_cnn.hip', 'iqn.hip', 'comm.hip')]
 HEADER = os.path.join(os.path.dirname(_HERE), 'include', 'dopamine_amd.h')
 ARCH = os.environ.get('DQ_OFFLOAD_ARCH', 'gfx950')
 
@@ -35,7 +35,7 @@ def build(verbose=False, out=None, sources=None):
   for p, cmd in procs:
     if p.wait() != 0:
       raise subprocess.CalledProcessError(p.returncode, cmd)
-  cmd = ['hipcc', '--offload-arch=' + ARCH, '-shared', '-fPIC', '-o', out] + objs
+  cmd = ['hipcc', '--offload-arch=' + ARCH, '-shared', '-fPIC', '-o', out] + objs + ['-ldl']
   if verbose:
     print(' '.join(cmd))
   subprocess.run(cmd, check=True)

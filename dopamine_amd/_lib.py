@@ -8,7 +8,7 @@ import os
 
 from dopamine_amd._build import HEADER, LIB_PATH  # noqa: F401
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 OK = 0
 (ST_OK, ST_EMPTY_TREE, ST_MAX_ATTEMPTS, ST_TAPE_EXHAUSTED, ST_NEG_PRIORITY, ST_TOO_FEW, ST_BAD_INDEX,
  ST_BROADCAST) = range(8)
@@ -189,6 +189,13 @@ SIGNATURES = {
     'dq_iqn_workspace_floats': [_I32, _I32, _I32, _I32],
     'dq_uniform_draw': [_P, ctypes.c_uint64, _I64, _P, _P],
     'dq_iqn_tau_cos': [_P, ctypes.c_uint64, _I32, _I32, _P, _P, _P],
+    'dq_comm_unique_id': [_P],
+    'dq_comm_create': [_P, _I32, _I32, _I32, ctypes.POINTER(_P)],
+    'dq_comm_destroy': [_P],
+    'dq_comm_allreduce_mean': [_P, _P, _I64, _P],
+    'dq_comm_reduce_scatter_mean': [_P, _P, _I64, _P],
+    'dq_comm_all_gather': [_P, _P, _I64, _P],
+    'dq_comm_version': [],
 }
 RESTYPES = {'dq_last_error': ctypes.c_char_p, 'dq_cnn_workspace_floats': ctypes.c_size_t,
             'dq_iqn_workspace_floats': ctypes.c_size_t,

@@ -91,7 +91,8 @@ class DQNAgent(object):
                device=None,
                seed=0,
                process_group=None,
-               shard_optimizer=False):
+               shard_optimizer=False,
+               native_comm=True):
     assert num_actions is not None
     assert isinstance(observation_shape, tuple)      # abstract_agent.py:34
     self.num_actions = num_actions
@@ -124,6 +125,11 @@ class DQNAgent(object):
     # N > 1 with TF1 Adam: ZeRO-1 for the fc bucket (reduce-scatter, each rank's Adam on
     # its 1/N slice, all-gather of the parameters) instead of all-reduce + a full update
     self.shard_optimizer = bool(shard_optimizer)
+    # N > 1 over RCCL: the gradient buckets go over the learner's own communicators
+    # (parallel.RcclComm, issued on the stream each bucket runs on) instead of
+    # torch.distributed's collectives (each forked onto the process group's own stream)
+    self.native_comm = bool(native_comm)
+    self._rccl = None
     self._pg_conv = None           # a second communicator for the conv bucket (see _split_step)
     self._fc_pending = None        # event: the previous step's fc all-reduce + update are done
     self._defer_fc = False         # set by train_gradient_steps (learner-only loop)
@@ -165,6 +171,7 @@ class DQNAgent(object):
       self._comm_opt = torch.cuda.Stream(self._device)    # ... and the Adam parts behind them
       if self._pg is not None:
         self._broadcast_replica()
+        self._rccl = self._make_native_comms()
     self._observation = None
     self._last_observation = None
     self.last_loss = None
@@ -175,6 +182,27 @@ class DQNAgent(object):
     ts += [v for k, v in sorted(vars(self._opt).items())
            if isinstance(v, torch.Tensor) and v.data_ptr() != self.online_convnet.fp.flat.data_ptr()]
     return ts
+
+  def _make_native_comms(self):
+    """(fc bucket, conv bucket) RcclComm pair for the split schedule over RCCL, or None
+    (gloo, or a schedule without buckets).  Collective: every rank constructs its agent."""
+    import torch.distributed as dist
+    if not (self.native_comm and self._split_allreduce() and dist.get_backend(self._pg) == 'nccl'):
+      return None
+    return (parallel.RcclComm(self._pg, self._device), parallel.RcclComm(self._pg, self._device))
+
+  def _ar_fc(self, t):
+    """The fc bucket's all-reduce (mean), on the current (comm) stream."""
+    if self._rccl is not None:
+      return self._rccl[0].allreduce_mean_(t)
+    return parallel.allreduce_mean_(t, self._pg)
+
+  def _ar_conv(self, t, second):
+    """The conv bucket's all-reduce (mean), on the current (main) stream: over the second
+    communicator when the fc bucket's may still be in flight on the first."""
+    if self._rccl is not None:
+      return self._rccl[1].allreduce_mean_(t)
+    return parallel.allreduce_mean_(t, self._conv_group() if second else self._pg)
 
   def _broadcast_replica(self):
     """Data-parallel replicas start from group rank 0's networks and optimizer state
@@ -603,6 +631,10 @@ class DQNAgent(object):
     o = n - self._grad_buckets()[0].numel()
     return o + (n - o) % (4 * self._world()), n
 
+  # ZeRO-1: the slice's Adam update on its own stream between the reduce-scatter and the
+  # all-gather (comm -> comm_opt -> comm) instead of on the comm stream
+  zero_update_stream = False
+
   def _gather_opt_state(self):
     """ZeRO-1: every rank's Adam moments of the sharded range, slice r from rank r (a
     collective: every rank calls it, e.g. from bundle_and_checkpoint)."""
@@ -662,9 +694,26 @@ class DQNAgent(object):
       # with the update on the second stream, comm -> comm_opt -> comm, the captured 4-step
       # chunk graphs ended in a segfault at capture end on ROCm 7.2)
       with torch.cuda.stream(self._comm):
-        parallel.reduce_scatter_mean_(grad[lo:n], self._pg)
+        if self._rccl is not None:
+          self._rccl[0].reduce_scatter_mean_(grad[lo:n])
+        else:
+          parallel.reduce_scatter_mean_(grad[lo:n], self._pg)
+      upd = self._comm_opt if self.zero_update_stream else self._comm
+      if upd is not self._comm:
+        e = torch.cuda.Event()
+        e.record(self._comm)
+        upd.wait_event(e)
+      with torch.cuda.stream(upd):
         self._opt.step_part(grad, lo + r * S, lo + (r + 1) * S, slot=k, bump=False)
-        parallel.all_gather_(self._opt.params[lo:n], self._pg)
+      if upd is not self._comm:
+        e = torch.cuda.Event()
+        e.record(upd)
+        self._comm.wait_event(e)
+      with torch.cuda.stream(self._comm):
+        if self._rccl is not None:
+          self._rccl[0].all_gather_(self._opt.params[lo:n])
+        else:
+          parallel.all_gather_(self._opt.params[lo:n], self._pg)
       conv, o = grad[:lo], lo                 # the head of the fc bucket joins the conv bucket
     else:
       pieces = self._fc_pieces(o, grad.numel()) if split_opt else [(o, grad.numel())]
@@ -674,7 +723,7 @@ class DQNAgent(object):
       one = len(pieces) == 1
       for lo, hi in pieces:
         with torch.cuda.stream(self._comm):
-          parallel.allreduce_mean_(grad[lo:hi], self._pg)
+          self._ar_fc(grad[lo:hi])
           if split_opt and one:
             self._opt.step_part(grad, lo, hi, slot=k, bump=False)
         if split_opt and not one:
@@ -685,11 +734,11 @@ class DQNAgent(object):
             self._opt.step_part(grad, lo, hi, slot=k, bump=False)
           last = self._comm_opt
     if defer:
-      parallel.allreduce_mean_(conv, self._conv_group())
+      self._ar_conv(conv, True)
       self._fc_pending = torch.cuda.Event()
       self._fc_pending.record(last)
     else:
-      parallel.allreduce_mean_(conv, self._pg)
+      self._ar_conv(conv, False)
       main.wait_stream(last)
     if split_opt:
       self._opt.step_part(grad, 0, o, slot=k, bump=True)
@@ -1013,9 +1062,9 @@ class DQNAgent(object):
     import torch.distributed as dist
     return (dist.get_backend(self._pg) == 'nccl' and self._split_allreduce() and
             self._head_splits() and isinstance(self._opt, ops.TF1Adam) and
-            parallel.collectives_capturable(self._pg, self._device, self._comm,
-                                            sharded=self._sharded(),
-                                            group2=self._conv_group()))
+            parallel.collectives_capturable(
+                self._pg, self._device, self._comm, sharded=self._sharded(),
+                group2=self._conv_group() if self._rccl is None else None, comms=self._rccl))
 
   def _chunks_apply(self):
     return (self._hip is not None and self.pipeline and

@@ -9,6 +9,7 @@ Adam update, so replicas stay bit-identical.  PER's `w /= max(w)` stays
 per-rank (rainbow_agent.py:280): the multi-GPU gradient is the mean of the
 ranks' single-GPU gradients, not a single B*N batch.
 """
+import ctypes
 import os
 
 import torch
@@ -72,6 +73,70 @@ def all_gather_(flat, group=None):
   return flat
 
 
+class RcclComm(object):
+  """One RCCL communicator over ``group``'s ranks, owned by the learner (dq_comm_*,
+  dopamine_amd/csrc/comm.hip): each collective is issued on the CURRENT stream, in place,
+  with no internal stream of its own -- so inside a captured HIP graph a bucket costs the
+  queue it runs on and nothing else (torch's ProcessGroupNCCL forks every collective onto
+  its own stream and joins it back: two more cross-queue edges per collective).  The
+  ncclUniqueId of group rank 0 reaches every rank by a broadcast over ``group``; every rank
+  must construct its RcclComm at the same point (ncclCommInitRank is collective)."""
+
+  def __init__(self, group, device):
+    from dopamine_amd import _lib
+    self._lib = _lib
+    self.world = dist.get_world_size(group)
+    self.rank = dist.get_rank(group)
+    uid = torch.zeros(128, dtype=torch.uint8)
+    if self.rank == 0:
+      _lib.call('dq_comm_unique_id', ctypes.c_void_p(uid.data_ptr()))
+    on_dev = dist.get_backend(group) == 'nccl'
+    t = uid.to(device) if on_dev else uid
+    dist.broadcast(t, src=dist.get_process_group_ranks(group)[0], group=group)
+    uid.copy_(t.cpu())
+    h = ctypes.c_void_p()
+    _lib.call('dq_comm_create', ctypes.c_void_p(uid.data_ptr()), self.world, self.rank,
+              torch.device(device).index or 0, ctypes.byref(h))
+    self._h = h
+    self.device = torch.device(device)
+
+  def _stream(self):
+    return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+  def _active(self):
+    return self.world > 1 or FORCE_COLLECTIVES
+
+  def allreduce_mean_(self, flat):
+    """As allreduce_mean_, on the current stream."""
+    assert flat.is_contiguous() and flat.dtype == torch.float32
+    if self._active():
+      self._lib.call('dq_comm_allreduce_mean', self._h, ctypes.c_void_p(flat.data_ptr()),
+                     flat.numel(), self._stream())
+    return flat
+
+  def reduce_scatter_mean_(self, flat):
+    """As reduce_scatter_mean_, on the current stream."""
+    assert flat.is_contiguous() and flat.numel() % self.world == 0
+    if self._active():
+      self._lib.call('dq_comm_reduce_scatter_mean', self._h, ctypes.c_void_p(flat.data_ptr()),
+                     flat.numel() // self.world, self._stream())
+    return flat
+
+  def all_gather_(self, flat):
+    """As all_gather_, on the current stream."""
+    assert flat.is_contiguous() and flat.numel() % self.world == 0
+    if self._active():
+      self._lib.call('dq_comm_all_gather', self._h, ctypes.c_void_p(flat.data_ptr()),
+                     flat.numel() // self.world, self._stream())
+    return flat
+
+  def destroy(self):
+    if self._h:
+      torch.cuda.synchronize(self.device)
+      self._lib.call('dq_comm_destroy', self._h)
+      self._h = None
+
+
 def replicas_in_sync(flat_params, group=None):
   """Checksum-broadcast check that every rank holds identical parameters."""
   s = torch.stack([flat_params.double().sum(), (flat_params.double() ** 2).sum()])
@@ -85,14 +150,17 @@ def replicas_in_sync(flat_params, group=None):
 _CAPTURABLE = {}
 
 
-def collectives_capturable(group, device, stream=None, sharded=False, group2=None):
+def collectives_capturable(group, device, stream=None, sharded=False, group2=None, comms=None):
   """Whether every rank of ``group`` can capture this backend's all-reduce into a HIP
   graph and replay it correctly -- probed once per group on a small tensor, the ranks
   agreeing (eager MIN all-reduces) after each phase so no rank replays a collective the
   others did not capture.  False for gloo (host-side collectives).  The learner loop
   captures its all-reduces only where this holds, else it replays per-step graphs with
-  the collectives issued between them."""
-  key = (id(group), bool(sharded), id(group2) if group2 is not None else None)
+  the collectives issued between them.  comms: a pair of RcclComm -- probe the learner's own
+  communicators (fc bucket on the comm stream, conv bucket on the origin) instead of
+  ``group`` / ``group2``'s torch collectives."""
+  key = (id(group), bool(sharded), id(group2) if group2 is not None else None,
+         None if comms is None else tuple(id(c) for c in comms))
   if key in _CAPTURABLE:
     return _CAPTURABLE[key]
   if dist.get_backend(group) != 'nccl':
@@ -119,11 +187,20 @@ def collectives_capturable(group, device, stream=None, sharded=False, group2=Non
     e.record(origin)
     comm.wait_event(e)
     with torch.cuda.stream(comm):
-      allreduce_mean_(x, group)
-      if sharded:
-        reduce_scatter_mean_(x, group)
-        all_gather_(x, group)
-    if group2 is not None:
+      if comms is not None:
+        comms[0].allreduce_mean_(x)
+        if sharded:
+          comms[0].reduce_scatter_mean_(x)
+          comms[0].all_gather_(x)
+      else:
+        allreduce_mean_(x, group)
+        if sharded:
+          reduce_scatter_mean_(x, group)
+          all_gather_(x, group)
+    if comms is not None:
+      with torch.cuda.stream(origin):
+        comms[1].allreduce_mean_(y)
+    elif group2 is not None:
       with torch.cuda.stream(origin):
         allreduce_mean_(y, group2)
     e = torch.cuda.Event()
@@ -152,7 +229,7 @@ def collectives_capturable(group, device, stream=None, sharded=False, group2=Non
       torch.cuda.synchronize(device)
       want = sum(range(1, world + 1)) / world if (world > 1 or FORCE_COLLECTIVES) else 1.0
       ok = bool(torch.allclose(x, torch.full_like(x, want)))
-      if group2 is not None:
+      if group2 is not None or comms is not None:
         ok = ok and bool(torch.allclose(y, torch.full_like(y, want)))
     except Exception:                             # noqa: BLE001
       ok = False

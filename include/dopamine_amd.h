@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define DQ_ABI_VERSION 2
+#define DQ_ABI_VERSION 3
 
 /* host-side return codes */
 #define DQ_OK 0
@@ -532,6 +532,28 @@ int dq_iqn_tau_cos(int64_t* counter, uint64_t seed, int32_t rows, int32_t embed_
 
 /* _build_sync_op (dqn_agent.py:324-339): online -> target copy of the flat buffer. */
 int dq_sync_copy(void* dst, const void* src, int64_t bytes, void* stream);
+
+/* ---------------- data-parallel gradient exchange (BASELINE config 4) ----------------
+ * The reference trains one replica (dqn_agent.py:432, _train_op); config 4 runs one learner
+ * and one 1M buffer per GPU and averages their gradients each step.  A dq_comm is one RCCL
+ * communicator over the learners; every call is issued on the given stream (graph-capturable),
+ * in place, float32, ReduceOp AVG, so the learner chooses the queue each bucket runs on.
+ * RCCL (librccl.so.1) is opened on first use.  Bootstrap: rank 0's dq_comm_unique_id is
+ * handed to every rank (torch.distributed broadcast), then every rank calls dq_comm_create
+ * (synchronous, collective). */
+#define DQ_COMM_ID_BYTES 128
+typedef struct dq_comm dq_comm;
+int dq_comm_unique_id(uint8_t* id_out /* DQ_COMM_ID_BYTES */);
+int dq_comm_create(const uint8_t* id, int32_t nranks, int32_t rank, int32_t device, dq_comm** out);
+int dq_comm_destroy(dq_comm* c);
+/* buf[0, n) := mean over the ranks of buf[0, n) */
+int dq_comm_allreduce_mean(dq_comm* c, float* buf, int64_t n, void* stream);
+/* slice r = buf[r n, (r + 1) n) := its mean over the ranks, on rank r (ZeRO-1) */
+int dq_comm_reduce_scatter_mean(dq_comm* c, float* buf, int64_t n_per_rank, void* stream);
+/* every slice r of buf := rank r's slice r */
+int dq_comm_all_gather(dq_comm* c, float* buf, int64_t n_per_rank, void* stream);
+/* RCCL's version code, or -1 if it cannot be opened */
+int dq_comm_version(void);
 
 #ifdef __cplusplus
 }

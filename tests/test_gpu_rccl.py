@@ -54,7 +54,8 @@ def test_rccl_one_rank_schedule_equals_single_learner_bitwise(rccl_group, loop):
   assert agent._graph_sets.get(True) is not None   # the split graphs were captured and replayed
   assert parallel.replicas_in_sync(agent.online_convnet.fp.flat, rccl_group)
   if loop:
-    assert agent._pg_conv is not None       # the conv bucket went over the second communicator
+    # the conv bucket went over the second communicator (the agent's own RcclComm pair)
+    assert agent._rccl is not None and agent._pg_conv is None
     # ... and the learner loop replayed chunk graphs with the all-reduces captured in them
     assert any(k[0] == 'chunk' for k in agent._graph_sets if isinstance(k, tuple))
   single = _run(_agent(None, 0), loop).numpy()
@@ -99,3 +100,61 @@ def test_allreduce_mean_over_rccl_is_identity_for_one_rank(rccl_group):
   torch.cuda.current_stream().wait_stream(s)
   torch.cuda.synchronize()
   assert torch.equal(x, ref)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize('loop', [False, True])
+def test_rccl_torch_collectives_schedule_equals_single_learner_bitwise(rccl_group, loop):
+  """The same schedule with torch.distributed's collectives (native_comm=False): the
+  learner's own communicators and the process group's give the same bits."""
+  agent = _agent(rccl_group, 0, native_comm=False)
+  assert agent._rccl is None
+  flat = _run(agent, loop).numpy()
+  single = _run(_agent(None, 0), loop).numpy()
+  assert np.array_equal(flat, single)
+
+
+def test_native_comm_is_used_and_collectives_are_identity_for_one_rank(rccl_group):
+  """parallel.RcclComm (dq_comm_*): the agent owns a pair over RCCL; in-place all-reduce,
+  reduce-scatter and all-gather of one rank leave the values as they are, eagerly and
+  replayed from a captured graph on a side stream."""
+  from dopamine_amd import parallel
+  agent = _agent(rccl_group, 0)
+  assert agent._rccl is not None and len(agent._rccl) == 2
+  c = agent._rccl[0]
+  x = torch.randn(4_278_892, device='cuda')
+  ref = x.clone()
+  s = torch.cuda.Stream()
+  s.wait_stream(torch.cuda.current_stream())
+  with torch.cuda.stream(s):
+    c.allreduce_mean_(x)
+    c.reduce_scatter_mean_(x)
+    c.all_gather_(x)
+  torch.cuda.current_stream().wait_stream(s)
+  torch.cuda.synchronize()
+  assert torch.equal(x, ref)
+  g = torch.cuda.CUDAGraph()
+  with torch.cuda.graph(g, stream=s):
+    c.allreduce_mean_(x)
+    x.mul_(2.0)
+  for _ in range(2):
+    g.replay()
+  torch.cuda.synchronize()
+  assert torch.equal(x, ref * 4.0)
+  parallel._CAPTURABLE.clear()
+  assert parallel.collectives_capturable(rccl_group, torch.device('cuda', 0), sharded=True,
+                                         comms=agent._rccl)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize('native', [True])
+def test_rccl_one_rank_zero1_update_on_second_stream_equals_single_learner(rccl_group, native):
+  """ZeRO-1 with the slice's update on its own stream between the reduce-scatter and the
+  all-gather (comm -> comm_opt -> comm), captured in the learner loop's chunk graphs:
+  the arrangement whose capture_end segfaulted on ROCm 7.2 in round 2."""
+  agent = _agent(rccl_group, 0, shard_optimizer=True, native_comm=native)
+  agent.zero_update_stream = True
+  flat = _run(agent, True).numpy()
+  assert any(k[0] == 'chunk' for k in agent._graph_sets if isinstance(k, tuple))
+  single = _run(_agent(None, 0), True).numpy()
+  assert np.array_equal(flat, single)
