@@ -60,6 +60,9 @@ def parse():
                        'for the fc bucket (1: DQNAgent shard_optimizer -- reduce-scatter, TF1 '
                        'Adam on the rank\'s slice, all-gather); default: both, headline from the '
                        'faster')
+  ap.add_argument('--branch-first', action='store_true',
+                  help='N > 1: capture the fc bucket\'s branch before the backward tail '
+                       '(DQNAgent.branch_first; a schedule experiment)')
   ap.add_argument('--comm', choices=('native', 'torch'), default='native',
                   help='N > 1 over RCCL: the learner\'s own communicators (parallel.RcclComm) '
                        'or torch.distributed\'s collectives')
@@ -70,8 +73,9 @@ def parse():
   return ap.parse_args()
 
 
-def fill_synthetic(mem, A, seed):
-  """SURVEY 8(d) synthetic inputs, generated on the device."""
+def fill_synthetic(mem, A, seed, priority=None):
+  """SURVEY 8(d) synthetic inputs, generated on the device (priority: one priority for
+  every transition, e.g. 1.0 as a 'uniform' scheme inserts; default random in [0.1, 2))."""
   C = mem._replay_capacity
   dev = mem._device
   g = torch.Generator(device=dev).manual_seed(seed)
@@ -80,6 +84,8 @@ def fill_synthetic(mem, A, seed):
   rewards = (torch.randint(0, 3, (C,), device=dev, generator=g) - 1).float()
   terminals = (torch.rand(C, device=dev, generator=g) < 1.0 / 500).to(torch.uint8)
   prios = torch.rand(C, device=dev, generator=g, dtype=torch.float64) * 1.9 + 0.1
+  if priority is not None:
+    prios.fill_(priority)
   mem.load_arrays(frames, actions, rewards, terminals, add_count=C + 12345, priorities=prios)
   del frames
 
@@ -370,6 +376,9 @@ def main():
     os.environ.setdefault('MASTER_PORT', '29533')
     dist.init_process_group('nccl', rank=0, world_size=1, device_id=dev)
     pg = dist.group.WORLD
+  if args.branch_first:
+    from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
+    DQNAgent.branch_first = True
   if args.split_c51 is not None:
     from dopamine_amd.agents.rainbow.rainbow_agent import RainbowAgent
     RainbowAgent.split_c51 = bool(args.split_c51)

@@ -634,6 +634,8 @@ class DQNAgent(object):
   # ZeRO-1: the slice's Adam update on its own stream between the reduce-scatter and the
   # all-gather (comm -> comm_opt -> comm) instead of on the comm stream
   zero_update_stream = False
+  # N > 1: capture the fc bucket's branch before the backward tail instead of after it
+  branch_first = False
 
   def _gather_opt_state(self):
     """ZeRO-1: every rank's Adam moments of the sharded range, slice r from rank r (a
@@ -674,8 +676,28 @@ class DQNAgent(object):
     # the tail is issued (captured) before the comm branch, so in a captured graph it is the
     # first child of the head's last launch and stays on that launch's hardware queue -- the
     # all-reduce branch takes the other one (a fork to another queue costs ~10 us on the
-    # critical path, measured with the branch captured first)
-    tail()
+    # critical path, measured with the branch captured first; branch_first re-measures it)
+    if not self.branch_first:
+      tail()
+    last, conv, o = self._fc_branch(ev, grad, conv, o, k, split_opt)
+    if self.branch_first:
+      tail()
+    if defer:
+      self._ar_conv(conv, True)
+      self._fc_pending = torch.cuda.Event()
+      self._fc_pending.record(last)
+    else:
+      self._ar_conv(conv, False)
+      main.wait_stream(last)
+    if split_opt:
+      self._opt.step_part(grad, 0, o, slot=k, bump=True)
+    else:
+      opt()
+
+  def _fc_branch(self, ev, grad, conv, o, k, split_opt):
+    """The fc bucket's exchange and update on the comm stream (forked at event ev, after
+    the backward launch that leaves fc1 / fc2's gradients final).  Returns (the stream to
+    join, the conv bucket, its end offset)."""
     self._comm.wait_event(ev)
     # The fc bucket as _FC_PIECES all-reduces back to back on the comm stream; each
     # piece's Adam part runs on a second stream behind its own all-reduce, under the
@@ -733,17 +755,7 @@ class DQNAgent(object):
           with torch.cuda.stream(self._comm_opt):
             self._opt.step_part(grad, lo, hi, slot=k, bump=False)
           last = self._comm_opt
-    if defer:
-      self._ar_conv(conv, True)
-      self._fc_pending = torch.cuda.Event()
-      self._fc_pending.record(last)
-    else:
-      self._ar_conv(conv, False)
-      main.wait_stream(last)
-    if split_opt:
-      self._opt.step_part(grad, 0, o, slot=k, bump=True)
-    else:
-      opt()
+    return last, conv, o
 
   def _post_loss(self, t):
     """Work that needs the loss but not the gradient (PER priority write-back)."""

@@ -161,4 +161,7 @@ class ImplicitQuantileAgent(rainbow_agent.RainbowAgent):
       d['taus'] = on.taus
       d['target_q'] = tg.acts['q']
       d['target_taus'] = tg.taus
+      if self.double_dqn:            # the online net's argmax quantiles on s'
+        d['online_next_q'] = self._iqn['online_next'].acts['q']
+        d['online_next_taus'] = self._iqn['online_next'].taus
     return d

@@ -131,16 +131,20 @@ def _prime(agent):
 
 
 def _run_lockstep(agent, kind):
-  """Drive the bench path and the float64 oracle in lockstep; returns the errors."""
+  """Drive the bench path and the float64 oracle in lockstep; returns the errors.
+  kind: 'rainbow' (PER loss weights + priority write-back), 'c51' (RainbowAgent with
+  replay_scheme 'uniform': the same prioritized buffer and stratified sampler, rb:331,
+  no weights and no write-back) or 'dqn' (uniform buffer, numpy's stream, Huber)."""
   mem = agent._replay.memory
-  prioritized = kind == 'rainbow'
+  prioritized = kind in ('rainbow', 'c51')      # the sampler: Python's random on the sum tree
+  per_loss = kind == 'rainbow'
   B = agent._batch_size
   A = agent.num_actions
   offsets = agent.online_convnet.fp.offsets
   k0 = agent._opt_steps % 2
   w = agent.online_convnet.fp.flat.cpu().double().numpy().copy()
   tw = agent.target_convnet.fp.flat.cpu().double().numpy().copy()
-  opt = _Adam64(agent._opt, k0) if kind == 'rainbow' else _RMSProp64(agent._opt, k0)
+  opt = _Adam64(agent._opt, k0) if prioritized else _RMSProp64(agent._opt, k0)
   orc = _oracle_replay(agent, prioritized)
   T64 = ONC.Params64(tw, offsets)
   cg = np.float64(np.float32(agent.cumulative_gamma))
@@ -159,7 +163,7 @@ def _run_lockstep(agent, kind):
     for name, ref in (('action', act), ('reward', rew), ('terminal', term),
                       ('next_action', nact), ('next_reward', nrew)):
       np.testing.assert_array_equal(tr[name], ref, err_msg=name)
-    if prioritized:
+    if per_loss:
       np.testing.assert_array_equal(tr['sampling_probabilities'], b[8])
     x = np.moveaxis(st, -1, 1).astype(np.float32) / np.float32(255)
     nx = np.moveaxis(nst, -1, 1).astype(np.float32) / np.float32(255)
@@ -174,7 +178,8 @@ def _run_lockstep(agent, kind):
     if prioritized:
       N = support.shape[0]
       ref = OL.c51_loss(out.detach().numpy().reshape(B, A, N), tout.numpy().reshape(B, A, N),
-                        act, rew, term, support, cg, b[8], dtype=np.float64)
+                        act, rew, term, support, cg, b[8] if per_loss else None,
+                        dtype=np.float64)
       errs['priorities'] = max(errs['priorities'],
                                float((np.abs(tr['priorities'] - ref['priorities']) /
                                       np.abs(ref['priorities'])).max()))
@@ -194,7 +199,7 @@ def _run_lockstep(agent, kind):
       e = _rel(tr['grad'][o:o + n], g[o:o + n])
       errs['grad'][name] = max(errs['grad'].get(name, 0.0), e)
     opt.step(w, g)
-    if prioritized:   # the next step samples the tree the device wrote
+    if per_loss:      # the next step samples the tree the device wrote
       orc.set_priority(np.asarray(idx, np.int32), tr['priorities'].astype(np.float32))
 
   eager0 = dict(agent._eager_steps)
@@ -245,6 +250,31 @@ def test_rainbow_bench_path_matches_float64_oracle():
 
 
 @pytest.mark.timeout(600)
+def test_c51_uniform_bench_path_matches_float64_oracle():
+  """C51 as c51.gin binds it (RainbowAgent, replay_scheme 'uniform', n = 1, Adam 2.5e-4 /
+  3.125e-4; rb:175-198, 331), 9 actions, 1M buffer, B = 32, on the same graph / chunk path:
+  the prioritized buffer's stratified sampler over equal insert priorities (1.0), the loss
+  unweighted, no priority write-back."""
+  import bench
+  from dopamine_amd.agents.optimizers import AdamOptimizer
+  from dopamine_amd.agents.rainbow.rainbow_agent import RainbowAgent
+  torch.cuda.set_device(0)
+  agent = RainbowAgent(num_actions=9, update_horizon=1, gamma=0.99, replay_scheme='uniform',
+                       min_replay_history=20000, update_period=4, target_update_period=8000,
+                       optimizer=AdamOptimizer(learning_rate=0.00025, epsilon=0.0003125),
+                       replay_capacity=1_000_000, batch_size=32, device=torch.device('cuda', 0))
+  agent.enable_trace()
+  random.seed(0)
+  bench.fill_synthetic(agent._replay.memory, 9, seed=4, priority=1.0)
+  _prime(agent)
+  tree = agent._replay.memory._tree
+  _check(_run_lockstep(agent, 'c51'), 'c51')
+  first = (tree.numel() + 1) // 2 - 1        # the heap's leaf level (sum_tree.py:80-89)
+  leaves = tree[first:first + agent._replay.memory._replay_capacity]
+  assert bool((leaves == 1.0).all())          # no write-back under the uniform scheme
+
+
+@pytest.mark.timeout(600)
 def test_dqn_pong_bench_path_matches_float64_oracle():
   """Config 2: DQN on Pong's 6 actions, uniform replay (numpy's legacy stream), n = 1,
   TF1 centered RMSProp, 1M buffer, B = 32, the same graph / chunk path."""
@@ -260,7 +290,7 @@ def test_dqn_pong_bench_path_matches_float64_oracle():
   _check(_run_lockstep(agent, 'dqn'), 'dqn')
 
 
-def _iqn_agent():
+def _iqn_agent(double_dqn=False):
   """Config 5 as implicit_quantile.gin binds it (N = N' = 64, K = 32, n = 3, Adam 5e-5 /
   3.125e-4, 'uniform' replay scheme on the prioritized buffer) at batch 64, 1M buffer."""
   from dopamine_amd.agents.implicit_quantile.implicit_quantile_agent import ImplicitQuantileAgent
@@ -270,12 +300,19 @@ def _iqn_agent():
                                replay_scheme='uniform', min_replay_history=20000, update_period=4,
                                target_update_period=8000,
                                optimizer=AdamOptimizer(learning_rate=0.00005, epsilon=0.0003125),
-                               replay_capacity=1_000_000, batch_size=64,
+                               replay_capacity=1_000_000, batch_size=64, double_dqn=double_dqn,
                                device=torch.device('cuda', 0))
 
 
+# The gradient without the device's ReLU decisions (float64 decides every mask itself): a
+# pre-activation within fp32 rounding of 0 flips a unit, so this is looser than GRAD_TOL,
+# but a systematic mask bug (a wrong ReLU, a wrong tile) moves it to O(1)
+GRAD_UNPINNED_TOL = 1e-2
+
+
 @pytest.mark.timeout(900)
-def test_iqn_breakout_step_matches_float64_oracle():
+@pytest.mark.parametrize('double_dqn', [False, True])
+def test_iqn_breakout_step_matches_float64_oracle(double_dqn):
   """Config 5: every step of the captured-graph learner loop (per-step graph replays;
   IQN has no chunk graphs) against float64 at the device's parameters of that step
   (each step is one call, so they are read between steps):
@@ -286,10 +323,12 @@ def test_iqn_breakout_step_matches_float64_oracle():
     * every parameter gradient within 1e-5 per tensor of float64 on the device's ReLU
       decisions (mask-pinned: see oracle/nature_cnn._relu; the unpinned error is printed);
     * the Adam update: float64 Adam from the device's state and gradient reproduces the
-      device's new parameters within PARAM_ATOL."""
+      device's new parameters within PARAM_ATOL.
+  double_dqn: the greedy next action from the ONLINE net on s' with K samples
+  (iqn:170-172, 205-214), at the step's parameters, instead of the target net."""
   import bench
   torch.cuda.set_device(0)
-  agent = _iqn_agent()
+  agent = _iqn_agent(double_dqn)
   assert agent._iqn is not None
   agent.enable_trace()
   random.seed(0)
@@ -327,7 +366,15 @@ def test_iqn_breakout_step_matches_float64_oracle():
                                torch.from_numpy(tr['target_taus']).double()).numpy()
     errs['q'] = max(errs['q'], _rel(tr['qv'], q.detach().numpy()))
     errs['target_q'] = max(errs['target_q'], _rel(tr['target_q'], tq_all))
-    ref = OL.iqn_loss(q.detach().numpy(), tq_all[:Np * B], tq_all[Np * B:], tr['taus'], act, rew,
+    if double_dqn:      # the argmax quantiles: the online net (this step's w) on s'
+      assert tq_all.shape[0] == Np * B
+      with torch.no_grad():
+        ta = ONC.iqn_forward(P, ONC.to_input(np.moveaxis(nx, 1, -1)),
+                             torch.from_numpy(tr['online_next_taus']).double()).numpy()
+      errs['argmax_q'] = max(errs.get('argmax_q', 0.0), _rel(tr['online_next_q'], ta))
+    else:
+      ta = tq_all[Np * B:]
+    ref = OL.iqn_loss(q.detach().numpy(), tq_all[:Np * B], ta, tr['taus'], act, rew,
                       term, cg, 1.0, dtype=np.float64)
     errs['loss'] = max(errs['loss'], _rel(tr['loss'], ref['loss']))
     errs['dq'] = max(errs['dq'], _rel(tr['grad_out'], ref['grad']))
@@ -345,8 +392,10 @@ def test_iqn_breakout_step_matches_float64_oracle():
     gw = agent.online_convnet.fp.flat.cpu().double().numpy()
     errs['params'] = max(errs['params'], float(np.abs(gw - w).max()))
   assert agent._eager_steps == eager0, 'a step ran eagerly: not the graph path'
-  print(json.dumps({'northstar_errors': 'iqn', **errs}), flush=True)
+  print(json.dumps({'northstar_errors': 'iqn_double' if double_dqn else 'iqn', **errs}), flush=True)
   assert errs['q'] <= Q_TOL and errs['target_q'] <= Q_TOL and errs['loss'] <= Q_TOL, errs
+  assert errs.get('argmax_q', 0.0) <= Q_TOL, errs
+  assert max(errs['grad_unpinned'].values()) <= GRAD_UNPINNED_TOL, errs
   assert errs['dq'] <= Q_TOL, errs
   assert max(errs['grad'].values()) <= GRAD_TOL, errs
   assert errs['params'] <= PARAM_ATOL, errs
