@@ -8,7 +8,7 @@ import os
 
 from dopamine_amd._build import HEADER, LIB_PATH  # noqa: F401
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 OK = 0
 (ST_OK, ST_EMPTY_TREE, ST_MAX_ATTEMPTS, ST_TAPE_EXHAUSTED, ST_NEG_PRIORITY, ST_TOO_FEW, ST_BAD_INDEX,
  ST_BROADCAST) = range(8)
@@ -133,6 +133,8 @@ SIGNATURES = {
     'dq_replay_egreedy': [_P, _P, _I32, _D, _P, _P],
     'dq_replay_record_sumtree_set': [_P, _P, _P, _I64, ctypes.POINTER(Rider)],
     'dq_replay_record_sample': [_P, _I32, _P, ctypes.POINTER(Rider)],
+    'dq_replay_record_sample_groups': [_P, _I32, _I32, _P, ctypes.POINTER(Rider)],
+    'dq_replay_sample_indices_groups': [_P, _I32, _I32, _P, _P],
     'dq_rider_chain': [ctypes.POINTER(Rider), ctypes.POINTER(Rider), ctypes.POINTER(Rider)],
     'dq_replay_record_gather_nhwc': [_P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                      ctypes.POINTER(Rider)],

@@ -166,7 +166,7 @@ class DQNAgent(object):
       self._build_train_op()
       self._opt = self.optimizer.build(self.online_convnet.fp.flat,
                                        segments=self.online_convnet.fp.segments())
-      self._side = torch.cuda.Stream(self._device)
+      self._side = torch.cuda.Stream(self._device, priority=self.side_priority)
       self._comm = torch.cuda.Stream(self._device)        # N > 1: the fc bucket's all-reduces
       self._comm_opt = torch.cuda.Stream(self._device)    # ... and the Adam parts behind them
       if self._pg is not None:
@@ -240,6 +240,8 @@ class DQNAgent(object):
     if self._hip is not None:
       d['online_out'] = self._hip['online'].acts['out']
       d['target_out'] = self._hip['target'][c].acts['out']
+      for k in ('a1', 'a2', 'a3', 'h'):    # the online forward's ReLU outputs (mask pinning)
+        d['act_' + k] = self._hip['online'].acts[k]
     elif getattr(self, '_last_online_out', None) is not None and 'q' in (self._ptgt[c] or {}):
       d['online_out'] = self._last_online_out       # the PyTorch-network path (e.g. CartPole)
       d['target_out'] = self._ptgt[c]['q']
@@ -634,6 +636,9 @@ class DQNAgent(object):
   # ZeRO-1: the slice's Adam update on its own stream between the reduce-scatter and the
   # all-gather (comm -> comm_opt -> comm) instead of on the comm stream
   zero_update_stream = False
+  # HIP stream priority of the prefetch stream (the pipelined non-rider schedule, e.g. IQN's
+  # target network beside the online backward): 0 normal, -1 high
+  side_priority = 0
   # N > 1: capture the fc bucket's branch before the backward tail instead of after it
   branch_first = False
 

@@ -53,8 +53,8 @@ __global__ __launch_bounds__(kTreeT) void k_per_sample(ReplayView v, int B, int3
   per_sample_par<kTreeT>(v, B, out, lds);
 }
 
-__global__ __launch_bounds__(64) void k_uniform_sample(ReplayView v, int B, int32_t* out) {
-  uniform_sample_body(v, B, out);
+__global__ __launch_bounds__(64) void k_uniform_sample(ReplayView v, int B, int32_t* out, int G) {
+  uniform_sample_body(v, B, out, G);
 }
 
 // SumTree.sample / stratified_sample (sum_tree.py:99-166) on the flat heap, one
@@ -487,8 +487,23 @@ int dq_replay_sample_indices(dq_replay* h, int32_t batch, int32_t* indices_out, 
   if (h->cfg.prioritized)
     hipLaunchKernelGGL(k_per_sample, dim3(1), dim3(kTreeT), 0, s, h->view(), batch, indices_out);
   else
-    hipLaunchKernelGGL(k_uniform_sample, dim3(1), dim3(64), 0, s, h->view(), batch, indices_out);
+    hipLaunchKernelGGL(k_uniform_sample, dim3(1), dim3(64), 0, s, h->view(), batch, indices_out, 1);
   DQ_CHECK_LAUNCH("sample_indices");
+  return DQ_OK;
+}
+
+int dq_replay_sample_indices_groups(dq_replay* h, int32_t batch, int32_t groups,
+                                    int32_t* indices_out, void* stream) {
+  DQ_CHECK_ARG(h && indices_out, "null argument");
+  DQ_CHECK_ARG(!h->tree_only, "a standalone sum tree has no transition store");
+  DQ_CHECK_ARG(!h->cfg.prioritized, "grouped sampling needs a uniform buffer (a prioritized "
+               "draw depends on the previous batch's priorities)");
+  DQ_CHECK_ARG(batch >= 1 && groups >= 1 && (int64_t)batch * groups <= kMaxBatch,
+               "batch * groups must be in [1, 1024]");
+  DQ_CHECK_ARG(h->st.tape, "RNG tape not attached");
+  hipLaunchKernelGGL(k_uniform_sample, dim3(1), dim3(64), 0, (hipStream_t)stream, h->view(), batch,
+                     indices_out, groups);
+  DQ_CHECK_LAUNCH("sample_indices_groups");
   return DQ_OK;
 }
 
@@ -686,6 +701,22 @@ int dq_replay_record_sample(dq_replay* h, int32_t batch, int32_t* indices_out, d
   RiderDesc r{};
   r.kind = h->cfg.prioritized ? kRiderPerSample : kRiderUniformSample;
   r.batch = batch;
+  r.out = indices_out;
+  return record(h, r, out);
+}
+
+int dq_replay_record_sample_groups(dq_replay* h, int32_t batch, int32_t groups,
+                                   int32_t* indices_out, dq_rider* out) {
+  DQ_CHECK_ARG(h && indices_out, "null argument");
+  DQ_CHECK_ARG(!h->tree_only, "a standalone sum tree has no transition store");
+  DQ_CHECK_ARG(!h->cfg.prioritized, "grouped sampling needs a uniform buffer");
+  DQ_CHECK_ARG(batch >= 1 && groups >= 1 && (int64_t)batch * groups <= kMaxBatch,
+               "batch * groups must be in [1, 1024]");
+  DQ_CHECK_ARG(h->st.tape, "RNG tape not attached");
+  RiderDesc r{};
+  r.kind = kRiderUniformSample;
+  r.batch = batch;
+  r.groups = groups;
   r.out = indices_out;
   return record(h, r, out);
 }

@@ -173,14 +173,19 @@ __device__ inline void per_sample_body(const ReplayView& v, int B, int32_t* out,
 // The draw/validate chain is evaluated 64 words at a time speculatively; a
 // ballot/prefix-count finds where the reference's loop would have stopped.
 // ---------------------------------------------------------------------------
-__device__ inline void uniform_sample_body(const ReplayView& v, int B, int32_t* out) {
+// G consecutive batches of B (the draws of G sample_index_batch(B) calls in a row, each with
+// its own max-attempts budget and its own error) into out[g * B + i]: the learner-only loop
+// draws a whole chunk's uniform batches at once (they do not depend on priorities).  The
+// rewind cursor (meta->reserved[0]) is the entry of the LAST batch, so
+// dq_replay_rewind_last_sample gives back exactly the one batch a prefetch holds.
+__device__ inline void uniform_sample_body(const ReplayView& v, int B, int32_t* out, int G = 1) {
   const int lane = threadIdx.x;
   dq_replay_meta* meta = v.meta;
   int64_t pos = meta->tape_pos;
-  const int64_t pos0 = pos;
+  int64_t entry = pos;
   if (meta->status != 0) {
-    if (lane == 0) meta->reserved[0] = pos0;
-    for (int i = lane; i < B; i += kWave) out[i] = 0;
+    if (lane == 0) meta->reserved[0] = entry;
+    for (int i = lane; i < G * B; i += kWave) out[i] = 0;
     return;
   }
   const int64_t add_count = meta->add_count;
@@ -195,9 +200,9 @@ __device__ inline void uniform_sample_body(const ReplayView& v, int B, int32_t* 
     if (max_id <= min_id) {
       if (lane == 0) {
         latch(meta, DQ_ST_TOO_FEW, 0, 0.0);
-        meta->reserved[0] = pos0;
+        meta->reserved[0] = entry;
       }
-      for (int i = lane; i < B; i += kWave) out[i] = 0;
+      for (int i = lane; i < G * B; i += kWave) out[i] = 0;
       return;
     }
   }
@@ -206,54 +211,61 @@ __device__ inline void uniform_sample_body(const ReplayView& v, int B, int32_t* 
   mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4;
   mask |= mask >> 8; mask |= mask >> 16; mask |= mask >> 32;
   const int64_t len = meta->tape_len;
-  int count = 0, fails = 0;
-  bool tape_dry = false;
-  if (rng == 0) {  // randint consumes no word when high - low == 1
-    const int64_t idx = pymod(min_id, v.C);
-    const bool ok = is_valid(v, idx, add_count);
-    if (ok) {
-      for (int i = lane; i < B; i += kWave) out[i] = (int32_t)idx;
-      count = B;
-    } else {
-      fails = v.max_attempts;
-    }
-  } else {
-    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    while (count < B && fails < v.max_attempts) {
-      const int64_t avail = len - pos;
-      if (avail <= 0) { tape_dry = true; break; }
-      const bool live = lane < avail;
-      const uint64_t w = live ? (uint64_t)v.tape[pos + lane] : 0ull;
-      const uint64_t val = w & mask;
-      const bool drawn = live && val <= rng;
-      const int64_t idx = pymod(min_id + (int64_t)val, v.C);
-      const bool ok = drawn && is_valid(v, idx, add_count);
-      const bool bad = drawn && !ok;
-      const uint64_t okm = __ballot(ok), badm = __ballot(bad);
-      const int cok = count + __popcll(okm & below) + (ok ? 1 : 0);
-      const int cbad = fails + __popcll(badm & below) + (bad ? 1 : 0);
-      const bool stop = (ok && cok == B) || (bad && cbad == v.max_attempts);
-      const uint64_t stopm = __ballot(stop);
-      if (stopm) {
-        const int s = __ffsll((unsigned long long)stopm) - 1;
-        if (ok && lane <= s) out[cok - 1] = (int32_t)idx;
-        count = __shfl(cok, s);
-        fails = __shfl(cbad, s);
-        pos += s + 1;
-        break;
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int g = 0; g < G; ++g) {
+    int32_t* o = out + (int64_t)g * B;
+    entry = pos;
+    int count = 0, fails = 0;
+    bool tape_dry = false;
+    if (rng == 0) {  // randint consumes no word when high - low == 1
+      const int64_t idx = pymod(min_id, v.C);
+      const bool ok = is_valid(v, idx, add_count);
+      if (ok) {
+        for (int i = lane; i < B; i += kWave) o[i] = (int32_t)idx;
+        count = B;
+      } else {
+        fails = v.max_attempts;
       }
-      if (ok) out[cok - 1] = (int32_t)idx;
-      count += __popcll(okm);
-      fails += __popcll(badm);
-      const int64_t used = avail < kWave ? avail : kWave;
-      pos += used;
-      if (used < kWave) { tape_dry = true; break; }
+    } else {
+      while (count < B && fails < v.max_attempts) {
+        const int64_t avail = len - pos;
+        if (avail <= 0) { tape_dry = true; break; }
+        const bool live = lane < avail;
+        const uint64_t w = live ? (uint64_t)v.tape[pos + lane] : 0ull;
+        const uint64_t val = w & mask;
+        const bool drawn = live && val <= rng;
+        const int64_t idx = pymod(min_id + (int64_t)val, v.C);
+        const bool ok = drawn && is_valid(v, idx, add_count);
+        const bool bad = drawn && !ok;
+        const uint64_t okm = __ballot(ok), badm = __ballot(bad);
+        const int cok = count + __popcll(okm & below) + (ok ? 1 : 0);
+        const int cbad = fails + __popcll(badm & below) + (bad ? 1 : 0);
+        const bool stop = (ok && cok == B) || (bad && cbad == v.max_attempts);
+        const uint64_t stopm = __ballot(stop);
+        if (stopm) {
+          const int s = __ffsll((unsigned long long)stopm) - 1;
+          if (ok && lane <= s) o[cok - 1] = (int32_t)idx;
+          count = __shfl(cok, s);
+          fails = __shfl(cbad, s);
+          pos += s + 1;
+          break;
+        }
+        if (ok) o[cok - 1] = (int32_t)idx;
+        count += __popcll(okm);
+        fails += __popcll(badm);
+        const int64_t used = avail < kWave ? avail : kWave;
+        pos += used;
+        if (used < kWave) { tape_dry = true; break; }
+      }
+    }
+    if (tape_dry || count != B) {      // this batch's error, as its own call would raise it
+      if (lane == 0) latch(meta, tape_dry ? DQ_ST_TAPE_EXHAUSTED : DQ_ST_MAX_ATTEMPTS, count, 0.0);
+      for (int i = lane + (g + 1) * B; i < G * B; i += kWave) out[i] = 0;
+      break;
     }
   }
   if (lane == 0) {
-    if (tape_dry) latch(meta, DQ_ST_TAPE_EXHAUSTED, count, 0.0);
-    else if (count != B) latch(meta, DQ_ST_MAX_ATTEMPTS, count, 0.0);
-    meta->reserved[0] = pos0;   // entry cursor, for dq_replay_rewind_last_sample
+    meta->reserved[0] = entry;   // the last batch's entry cursor, for dq_replay_rewind_last_sample
     meta->tape_pos = pos;
   }
 }
@@ -788,7 +800,7 @@ struct RiderDesc {
   int32_t kind;
   int32_t batch;
   int32_t gx;        // gather: column blocks of 256 threads per (b, which) stack
-  int32_t pad;
+  int32_t groups;    // uniform sample: consecutive batches of `batch` (0 or 1: one)
   ReplayView v;
   GatherOut g;
   SetArgs s;
@@ -817,7 +829,7 @@ __device__ __forceinline__ void run_rider(const RiderDesc& r, int blk, void* lds
       per_sample_par<T>(r.v, r.batch, r.out, lds);
       return;
     case kRiderUniformSample:
-      if (t < kWave) uniform_sample_body(r.v, r.batch, r.out);
+      if (t < kWave) uniform_sample_body(r.v, r.batch, r.out, r.groups > 1 ? r.groups : 1);
       return;
     case kRiderGatherNhwc: {
       const int sub = blk * (T / 256) + t / 256;

@@ -84,6 +84,13 @@ class RcclComm(object):
 
   def __init__(self, group, device):
     from dopamine_amd import _lib
+    # RCCL's implicit launch order (on by default in this RCCL) chains the kernels of every
+    # communicator of the process in host call order: inside the captured step the fc
+    # bucket's all-reduce, issued first on the comm stream, then started only after the conv
+    # bucket's, ~45 us late (rocprof, profiles/r3_dist).  The two buckets' kernels are small
+    # grids that fit on the GPU together, so no cross-communicator order is needed for progress.
+    # Read by this package's own RCCL instance (dlopened at its first call), not torch's.
+    os.environ.setdefault('NCCL_LAUNCH_ORDER_IMPLICIT', '0')
     self._lib = _lib
     self.world = dist.get_world_size(group)
     self.rank = dist.get_rank(group)

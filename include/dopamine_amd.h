@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define DQ_ABI_VERSION 3
+#define DQ_ABI_VERSION 4
 
 /* host-side return codes */
 #define DQ_OK 0
@@ -125,6 +125,13 @@ int dq_replay_add(dq_replay* h, int64_t n, const uint8_t* frames, const int32_t*
  * SumTree.stratified_sample / sample, sum_tree.py:99-166).  Random numbers come
  * from the device RNG tape; exact draw-for-draw equivalent of the reference. */
 int dq_replay_sample_indices(dq_replay* h, int32_t batch, int32_t* indices_out, void* stream);
+/* `groups` consecutive uniform sample_index_batch(batch) calls (crb:436-477) in one launch,
+ * indices_out[g * batch + i]: the same draws, RNG words and per-call max-attempts budgets and
+ * errors as the calls in a row (the first failing batch latches its error).  The rewind
+ * cursor is the last batch's, so dq_replay_rewind_last_sample gives back that batch only.
+ * Uniform buffers only (a prioritized draw depends on the previous batch's write-back). */
+int dq_replay_sample_indices_groups(dq_replay* h, int32_t batch, int32_t groups,
+                                    int32_t* indices_out, void* stream);
 
 /* sample_transition_batch given indices (circular_replay_buffer.py:479-558 +
  * prioritized_replay_buffer.py:173-201).  Any output pointer may be NULL. */
@@ -219,6 +226,8 @@ typedef struct dq_rider {
 int dq_replay_record_sumtree_set(dq_replay* h, const int32_t* indices, const float* priorities,
                                  int64_t n, dq_rider* out);
 int dq_replay_record_sample(dq_replay* h, int32_t batch, int32_t* indices_out, dq_rider* out);
+int dq_replay_record_sample_groups(dq_replay* h, int32_t batch, int32_t groups,
+                                   int32_t* indices_out, dq_rider* out);
 int dq_replay_record_gather_nhwc(dq_replay* h, const int32_t* indices, int32_t batch,
                                  float* state_out, float* next_state_out, int32_t* action_out,
                                  float* reward_out, int32_t* next_action_out,

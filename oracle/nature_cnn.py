@@ -75,9 +75,10 @@ def torso(P, x_nhwc, masks=None):
   return x.permute(0, 2, 3, 1).reshape(x.shape[0], -1)
 
 
-def forward(P, x_nhwc):
-  """NatureDQN q-values (B, A) or Rainbow logits (B, A*N): fc1 + ReLU, fc2."""
-  h = F.relu(F.linear(torso(P, x_nhwc), P['fc1_w'], P['fc1_b']))
+def forward(P, x_nhwc, masks=None):
+  """NatureDQN q-values (B, A) or Rainbow logits (B, A*N): fc1 + ReLU, fc2.  masks: the
+  device's activations (a1, a2, a3, h) to pin the ReLU decisions (see _relu)."""
+  h = _relu(F.linear(torso(P, x_nhwc, masks), P['fc1_w'], P['fc1_b']), masks, 'h')
   return F.linear(h, P['fc2_w'], P['fc2_b'])
 
 

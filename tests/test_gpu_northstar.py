@@ -38,7 +38,13 @@ from oracle import replay as OR
 pytestmark = pytest.mark.gpu
 
 Q_TOL = 1e-5         # north_star: Q-values / logits and losses
-GRAD_TOL = 1e-5      # flat gradient, per tensor, relative to the tensor's max |g|
+GRAD_TOL = 1e-5      # flat gradient, per tensor, relative to the tensor's max |g|, on the
+                     # device's ReLU decisions (mask-pinned, oracle/nature_cnn._relu)
+# The same gradient with float64 deciding every ReLU itself: a pre-activation within fp32
+# rounding of 0 flips a unit and moves a tensor's gradient by up to ~1e-2 of its scale
+# (measured: 9.3e-3 conv2_w in the C51 test, 5.5e-3 fc1_w in IQN double_dqn); a systematic
+# mask or tile bug moves it by O(1)
+GRAD_UNPINNED_TOL = 5e-2
 PARAM_ATOL = 5e-8    # parameters after fp32 updates vs the float64 trajectory (|w| ~ 0.05)
 CHUNKS = 3
 
@@ -151,7 +157,7 @@ def _run_lockstep(agent, kind):
   if prioritized:
     support = agent._support.cpu().double().numpy()
   errs = dict(logits=0.0, target=0.0, loss=0.0, loss_elementwise=0.0, priorities=0.0, grad={},
-              params=0.0)
+              grad_unpinned={}, params=0.0)
   U = agent._UNROLL
 
   def step(slot):
@@ -193,12 +199,17 @@ def _run_lockstep(agent, kind):
     errs['loss_elementwise'] = max(errs['loss_elementwise'], float(
         (np.abs(tr['loss'] - ref['loss']) / np.maximum(np.abs(ref['loss']), 1e-30)).max()))
     out.backward(torch.from_numpy(gout))
-    g = P.flat_grad()
+    g_free = P.flat_grad()
+    Pm = ONC.Params64(w, offsets)               # the same step on the device's ReLU decisions
+    masks = {k: tr['act_' + k] for k in ('a1', 'a2', 'a3', 'h')}
+    ONC.forward(Pm, ONC.to_input(np.moveaxis(x, 1, -1)), masks).backward(torch.from_numpy(gout))
+    g = Pm.flat_grad()
     for name, (o, shape) in offsets.items():
       n = int(np.prod(shape))
-      e = _rel(tr['grad'][o:o + n], g[o:o + n])
-      errs['grad'][name] = max(errs['grad'].get(name, 0.0), e)
-    opt.step(w, g)
+      errs['grad'][name] = max(errs['grad'].get(name, 0.0), _rel(tr['grad'][o:o + n], g[o:o + n]))
+      errs['grad_unpinned'][name] = max(errs['grad_unpinned'].get(name, 0.0),
+                                        _rel(tr['grad'][o:o + n], g_free[o:o + n]))
+    opt.step(w, tr['grad'].astype(np.float64))  # the device's gradient, float64 optimizer
     if per_loss:      # the next step samples the tree the device wrote
       orc.set_priority(np.asarray(idx, np.int32), tr['priorities'].astype(np.float32))
 
@@ -233,6 +244,7 @@ def _check(errs, kind):
   assert errs['loss'] <= Q_TOL, errs
   assert errs['priorities'] <= Q_TOL, errs
   assert max(errs['grad'].values()) <= GRAD_TOL, errs
+  assert max(errs['grad_unpinned'].values()) <= GRAD_UNPINNED_TOL, errs
   assert errs['params'] <= PARAM_ATOL, errs
 
 
@@ -304,10 +316,7 @@ def _iqn_agent(double_dqn=False):
                                device=torch.device('cuda', 0))
 
 
-# The gradient without the device's ReLU decisions (float64 decides every mask itself): a
-# pre-activation within fp32 rounding of 0 flips a unit, so this is looser than GRAD_TOL,
-# but a systematic mask bug (a wrong ReLU, a wrong tile) moves it to O(1)
-GRAD_UNPINNED_TOL = 1e-2
+
 
 
 @pytest.mark.timeout(900)
