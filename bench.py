@@ -185,6 +185,17 @@ def other_configs(device, steps):
     res[name] = {'value': round(n / elapsed, 2), 'unit': 'gradient-steps/s', 'steps': n,
                  'ms_per_step': round(1e3 * elapsed / n, 4), 'batch': agent._batch_size,
                  'final_mean_loss': round(loss, 5)}
+    if name == 'dqn_pong' and agent._chunk_gathers():
+      # the learner loop's chunk gather: one K * B launch per chunk (K = 4), timed as the
+      # headline's gather is (standalone launches, fresh random indices, HIP events)
+      kb = agent._UNROLL * agent._batch_size
+      us, _, algo, gname = time_gather(agent, 100, batch=kb)
+      gbs = algo / (us * 1e-6) / 1e9
+      res[name]['chunk_gather_roofline'] = {
+          'kernel': gname + ' (chunk gather, batch %d)' % kb, 'bound': 'hbm',
+          'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+          'frac': round(gbs / HBM_PEAK_GBS, 4), 'algo_bytes_per_launch': algo,
+          'avg_launch_us': round(us, 3)}
     del agent
     gc.collect()
     torch.cuda.empty_cache()
@@ -195,13 +206,14 @@ def other_configs(device, steps):
   return res
 
 
-def time_gather(agent, iters):
+def time_gather(agent, iters, batch=None):
   """Average duration of the gather kernel, HIP events on the launch stream,
-  back-to-back launches captured in a HIP graph (no host launch gaps)."""
+  back-to-back launches captured in a HIP graph (no host launch gaps).  batch: the launch's
+  batch (default the agent's; the DQN learner loop's chunk gather launches K * B)."""
   from dopamine_amd import _lib
   mem = agent._replay.memory
-  out = agent._replay._out
-  B = agent._batch_size
+  B = batch or agent._batch_size
+  out = agent._replay._out if B == agent._batch_size else mem._alloc_batch(B, agent._replay._layout)
   layout = agent._replay._layout
   stream = torch.cuda.current_stream()
   # a fresh random index batch per launch: 400 x 1.8 MB of frames (> the 256 MB

@@ -152,6 +152,9 @@ class DQNAgent(object):
     self._ptgt = [None, None]
     self._has_prefetch = False
     self._prefetch_add_count = -1
+    self._cb = None                # chunk gather: 2 sets of _UNROLL batches (see _chunk_gathers)
+    self._cb_ready = None          # set p: the prefetched batch is set p's last one
+    self._gather_plan = None       # (set, step) while a chunk-gather graph is captured
     self._online_ready = None
     self._head = None              # (target net, input) whose forward head rides in the backward
     self._tail_head = None         # ... in the N > 1 tail graph
@@ -419,9 +422,15 @@ class DQNAgent(object):
 
   def _place_riders(self, riders):
     """Rider i rides in backward launch first + i, in the recorded order (PER write-back,
-    sample, gather).  Other placements were measured and not kept; a timing
-    experiment may override this method, never the product path."""
+    sample, gather).  Other placements were measured and not kept.  A chunk
+    gather's K * B gather (a chunk's first step) rides in backward launch
+    chunk_gather_launch (it must precede the next batch's target head, launch 5)."""
+    if self._gather_plan is not None and len(riders) == 2 and self.chunk_gather_launch > 2:
+      empty = [_lib.Rider() for _ in range(self.chunk_gather_launch - 2)]
+      return riders[:1] + empty + riders[1:]
     return riders
+
+  chunk_gather_launch = 2
 
   def _forward_fused_c51(self, c, part=None):
     raise NotImplementedError
@@ -459,6 +468,15 @@ class DQNAgent(object):
 
   def _prefetch(self, i):
     mem = self._replay.memory
+    if self._gather_plan is not None:   # capturing a chunk-gather graph (_run_gather_chunk)
+      p, j = self._gather_plan
+      if j == 0:                        # the chunk's K next batches: one sample + one gather
+        mem.sample_device(self._batch_size, layout=self._replay._layout, out=self._cb_sets()[p],
+                          reserve=False, groups=self._UNROLL)
+      t = self._cbv[p][j]               # the batch of the chunk's step j + 1
+      self._pbuf[i] = t
+      self._head = (self._hip['target'][i], t['next_state'])
+      return
     t = mem.sample_device(self._batch_size, layout=self._replay._layout, out=self._pbuf[i],
                           reserve=False)
     self._pbuf[i] = t
@@ -781,8 +799,95 @@ class DQNAgent(object):
 
   def _discard_prefetch(self):
     if self._has_prefetch:
+      # (after a chunk-gather chunk the rewind cursor is its last batch's: exactly the
+      # prefetched one is given back)
       self._replay.memory.rewind_last_sample()
       self._has_prefetch = False
+      self._cb_ready = None
+
+  # ----------------------------------------------------- chunk gather (uniform)
+  # In the learner-only loop a uniform replay's batches do not depend on priorities, so
+  # the K batches of a chunk (steps 1..K-1 and the next chunk's step 0) are drawn by ONE
+  # grouped sample and gathered by ONE K*B launch, riding in the chunk's first backward
+  # (crb:436-558: the same draws, RNG words and batches as K per-step samples).  Two sets
+  # of K batches alternate between consecutive chunks: a chunk's first step still reads
+  # the previous set's last batch while its riders fill the other set.
+  chunk_gather = True
+
+  def _chunk_gathers(self):
+    return (self.chunk_gather and self._fused() and self._pg is None and
+            not self._replay.memory._prioritized)
+
+  def _cb_sets(self):
+    if self._cb is None:
+      mem, K, B = self._replay.memory, self._UNROLL, self._batch_size
+      self._cb = []
+      for _ in range(2):
+        d = mem._alloc_batch(K * B, self._replay._layout)
+        d['sample_indices'] = torch.empty((K * B,), dtype=torch.int32, device=self._device)
+        self._cb.append(d)
+      self._cbv = [[{k: v[i * B:(i + 1) * B] for k, v in d.items()} for i in range(K)]
+                   for d in self._cb]
+    return self._cb
+
+  def _prefetched(self):
+    """The batch the next gradient step trains on (prefetched)."""
+    if self._cb_ready is not None:
+      return self._cbv[self._cb_ready][self._UNROLL - 1]
+    return self._pbuf[self._slot]
+
+  def _materialize_cb(self):
+    """A chunk's prefetched batch into the per-call pipeline slot (the per-call graphs read
+    _pbuf); its target head already ran into the slot's target executor."""
+    src, dst = self._prefetched(), self._pbuf[self._slot]
+    for k, v in dst.items():
+      if k in src:
+        v.copy_(src[k])
+    self._cb_ready = None
+
+  def _run_gather_chunk(self, K):
+    """K gradient steps as one chunk-gather graph replay (captured per starting parity,
+    three variants: entering from the per-call pipeline, and the two alternating sets)."""
+    mem = self._replay.memory
+    k0 = self._opt_steps % 2
+    steady = self._cb_ready is not None
+    p = 1 - self._cb_ready if steady else 0
+    key = ('gchunk', K, k0, p, steady)
+    if key not in self._graph_sets:
+      torch.cuda.synchronize(self._device)
+      self._cb_sets()
+      saved = list(self._pbuf)
+      try:
+        for st, q in ((False, 0), (True, 0), (True, 1)):
+          g = torch.cuda.CUDAGraph()
+          with torch.cuda.graph(g, pool=self._graph_pool):
+            for j in range(K):
+              k = (k0 + j) % 2
+              if j == 0:                # the prefetched batch
+                self._pbuf[k] = self._cbv[1 - q][K - 1] if st else saved[k0]
+              self._gather_plan = (q, j)
+              self._grad_step(k, k, True)
+              self._device_opt_step(k)
+              self._trace_step(j, k)
+            self._gather_plan = None
+          self._graph_pool = g.pool()
+          self._graph_sets[('gchunk', K, k0, q, st)] = g
+      finally:
+        self._gather_plan = None
+        self._pbuf[:] = saved
+    for _ in range(K):
+      mem.reserve_rng(self._batch_size)
+    self._graph_sets[key].replay()
+    self._opt_steps += K
+    last = self._cbv[p][K - 2]          # the batch the chunk's last step trained on
+    self._replay._out = last
+    self._replay.unpack_transition(last)
+    self._slot = (k0 + K) % 2
+    self._cb_ready = p
+    self._has_prefetch = True
+    self._prefetch_add_count = int(mem.add_count)
+    self._last_train_add_count = int(mem.add_count)
+    self._selects_since_train = 0
 
   # The prefetch of step t+1 (drawn right after step t's priority write-back) is
   # only usable if nothing touches the replay RNG stream or the buffer before
@@ -804,6 +909,8 @@ class DQNAgent(object):
     pipe = self.pipeline and not self._interleaved()
     if self._has_prefetch and (not pipe or self._prefetch_add_count != int(mem.add_count)):
       self._discard_prefetch()            # transitions were added after the prefetch
+    if self._cb_ready is not None:        # a chunk's prefetch, for the per-call graphs
+      self._materialize_cb()
     if pipe and not self._has_prefetch:
       mem.reserve_rng(self._batch_size)
       self._prefetch(c)
@@ -904,7 +1011,7 @@ class DQNAgent(object):
     self._join_fc()
     ops.sync_copy(self.target_convnet.fp.flat, self.online_convnet.fp.flat)
     if self.pipeline and self._has_prefetch and self._rides():   # the prefetched head is stale
-      self._hip['target'][self._slot].forward_head(self._pbuf[self._slot]['next_state'])
+      self._hip['target'][self._slot].forward_head(self._prefetched()['next_state'])
     elif self.pipeline and self._has_prefetch and not self._pairs():   # prefetched target outputs are stale
       tg = self._target_forward(self._pbuf[self._slot], self._slot)
       for k, v in tg.items():
@@ -1068,6 +1175,8 @@ class DQNAgent(object):
       return False
     if not self._chunks_apply():
       return True
+    if self._chunk_gathers():
+      return all(('gchunk', self._UNROLL, k, 0, False) in self._graph_sets for k in (0, 1))
     return all(('chunk', self._UNROLL, k) in self._graph_sets for k in (0, 1))
 
   def _captures_collectives(self):
@@ -1105,6 +1214,8 @@ class DQNAgent(object):
   def _run_train_ops_chunk(self, K):
     """K pipelined gradient steps as one replay of a K-step graph (captured per
     starting parity on first use)."""
+    if self._chunk_gathers():
+      return self._run_gather_chunk(K)
     mem = self._replay.memory
     k0 = self._opt_steps % 2
     key = ('chunk', K, k0)

@@ -648,32 +648,40 @@ class OutOfGraphReplayBuffer(object):
     return self._rng.reserve(self._words_worst_case(B), self._stream)
 
   def sample_device(self, batch_size=None, layout=_lib.LAYOUT_F32_NORM, out=None, indices=None,
-                    reserve=True):
+                    reserve=True, groups=1):
     """Sample + gather without leaving the device or synchronising.
 
     Returns a dict of device tensors (``state``/``next_state`` as float32 NCHW
     normalised by 1/255 for the CNN).  The host RNG stream is brought in step
     lazily (``sync_rng``); device-latched errors surface at the next sync.
     ``reserve=False`` skips the host tape bookkeeping (the caller did it with
-    ``reserve_rng``, e.g. around a HIP-graph replay)."""
+    ``reserve_rng``, e.g. around a HIP-graph replay).  ``groups`` > 1 (uniform buffers):
+    that many consecutive batches of ``batch_size`` -- the draws of as many calls in a row
+    (dq_replay_sample_indices_groups) -- gathered as one groups * batch_size batch."""
     B = self._batch_size if batch_size is None else batch_size
+    n = B * groups
     if out is None:
-      out = self._alloc_batch(B, layout)
+      out = self._alloc_batch(n, layout)
     if indices is None:
       if reserve:
-        self.reserve_rng(B)
+        for _ in range(groups):
+          self.reserve_rng(B)
       if 'sample_indices' not in out:
-        out['sample_indices'] = torch.empty((B,), dtype=torch.int32, device=self._device)
+        out['sample_indices'] = torch.empty((n,), dtype=torch.int32, device=self._device)
+      p = _lib.ptr(out['sample_indices'])
       if self._riders is not None:
         r = _lib.Rider()
-        _lib.call('dq_replay_record_sample', self._h, B, _lib.ptr(out['sample_indices']),
-                  ctypes.byref(r))
+        if groups > 1:
+          _lib.call('dq_replay_record_sample_groups', self._h, B, groups, p, ctypes.byref(r))
+        else:
+          _lib.call('dq_replay_record_sample', self._h, B, p, ctypes.byref(r))
         self._riders.append(r)
+      elif groups > 1:
+        _lib.call('dq_replay_sample_indices_groups', self._h, B, groups, p, self._stream)
       else:
-        _lib.call('dq_replay_sample_indices', self._h, B, _lib.ptr(out['sample_indices']),
-                  self._stream)
+        _lib.call('dq_replay_sample_indices', self._h, B, p, self._stream)
       indices = out['sample_indices']
-    return self._gather(indices, B, layout, out)
+    return self._gather(indices, n, layout, out)
 
   @contextlib.contextmanager
   def recording(self):

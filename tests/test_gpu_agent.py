@@ -246,11 +246,51 @@ def test_learner_loop_chunks_equal_per_call_loop(kind):
     a._discard_prefetch()
     a._replay.memory.sync_rng()
     leaves = a._replay.memory.sum_tree.nodes[-1].copy() if kind == 'rainbow' else None
+    ns = np.random.get_state()
     res.append((np.stack(idx), a.online_convnet.fp.flat.cpu().numpy(),
                 a.target_convnet.fp.flat.cpu().numpy(), leaves, a.training_steps,
-                a._opt_steps, random.getstate()))
+                a._opt_steps, random.getstate(), ns[1].copy(), ns[2]))
     if chunked:
-      assert any(k[0] == 'chunk' for k in a._graph_sets if isinstance(k, tuple)), 'no chunk ran'
+      # a uniform replay's chunks draw and gather their batches at once (chunk gather)
+      want = 'gchunk' if kind == 'dqn' else 'chunk'
+      assert any(k[0] == want for k in a._graph_sets if isinstance(k, tuple)), 'no chunk ran'
+  for x, y in zip(res[0], res[1]):
+    if isinstance(x, np.ndarray):
+      np.testing.assert_array_equal(x, y)
+    else:
+      assert x == y
+
+
+def test_chunk_gather_equals_per_step_gather_chunks():
+  """DQN (uniform replay) learner loop: chunks whose K batches are drawn by one grouped
+  sample and gathered by one K*B launch (chunk_gather) == chunks that sample and gather per
+  step, bit for bit (batches, parameters, numpy RNG state), through chunk-to-chunk,
+  chunk-to-per-call and target-sync transitions and a prefetch discarded by an add()."""
+  from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
+  res = []
+  for cg in (False, True):
+    random.seed(7); np.random.seed(7); torch.manual_seed(7)
+    a = DQNAgent(num_actions=6, replay_capacity=3000, batch_size=32, min_replay_history=100,
+                 target_update_period=36)
+    a.chunk_gather = cg
+    _fill(a._replay.memory, 6, 3)
+    idx = []
+    for n in (9, 12, 2, 8, 4):
+      a.train_gradient_steps(n)
+      idx.append(a._replay.transition['indices'].cpu().numpy().copy())
+    a._replay.add(np.zeros((84, 84), np.uint8), 1, 0.5, False)   # invalidates the prefetch
+    for _ in range(8):
+      a._train_step()
+    idx.append(a._replay.transition['indices'].cpu().numpy().copy())
+    a.train_gradient_steps(8)
+    idx.append(a._replay.transition['indices'].cpu().numpy().copy())
+    a._discard_prefetch()
+    a._replay.memory.sync_rng()
+    ns = np.random.get_state()
+    res.append((np.stack(idx), a.online_convnet.fp.flat.cpu().numpy(),
+                a.target_convnet.fp.flat.cpu().numpy(), a.training_steps, ns[1].copy(), ns[2]))
+    keys = [k[0] for k in a._graph_sets if isinstance(k, tuple)]
+    assert ('gchunk' in keys) == cg and ('chunk' in keys) != cg
   for x, y in zip(res[0], res[1]):
     if isinstance(x, np.ndarray):
       np.testing.assert_array_equal(x, y)
