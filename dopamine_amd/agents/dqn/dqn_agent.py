@@ -430,7 +430,7 @@ class DQNAgent(object):
       return riders[:1] + empty + riders[1:]
     return riders
 
-  chunk_gather_launch = 2
+  chunk_gather_launch = 3
 
   def _forward_fused_c51(self, c, part=None):
     raise NotImplementedError

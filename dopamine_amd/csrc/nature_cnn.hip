@@ -299,13 +299,17 @@ struct OptPart<2> {
 // A recorded replay operation (replay_dev.h) riding in a grouped launch: its
 // blocks come first in the launch so the single-wave sum-tree update / sampler
 // chains start before the GEMM blocks fill the machine.
-struct RiderOp {
+template <bool kGroups = false>
+struct RiderOpT {
   static constexpr int kT = kGroupT;
   static constexpr int kLds = (kRiderLds + 3) / 4;
   RiderDesc r;
-  __device__ __forceinline__ void run(int blk, float* smem) const { run_rider<kT>(r, blk, smem); }
+  __device__ __forceinline__ void run(int blk, float* smem) const {
+    run_rider<kT, kGroups>(r, blk, smem);
+  }
   int blocks() const { return rider_blocks<kT>(r); }
 };
+using RiderOp = RiderOpT<false>;
 
 template <class... Ops>
 constexpr int max_lds() {
@@ -400,7 +404,10 @@ void group(Ctx& c, Op0 op0, Ops... ops) {
 template <class... Ops>
 void group_r(Ctx& c, const RiderDesc* r, Ops... ops) {
   if (r && r->kind != kRiderNone)
-    group(c, RiderOp{*r}, ops...);
+    if (r->kind == kRiderUniformSample && r->groups > 1)   // a chunk's grouped draw
+      group(c, RiderOpT<true>{*r}, ops...);
+    else
+      group(c, RiderOp{*r}, ops...);
   else
     group(c, ops...);
 }

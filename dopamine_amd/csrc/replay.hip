@@ -54,7 +54,10 @@ __global__ __launch_bounds__(kTreeT) void k_per_sample(ReplayView v, int B, int3
 }
 
 __global__ __launch_bounds__(64) void k_uniform_sample(ReplayView v, int B, int32_t* out, int G) {
-  uniform_sample_body(v, B, out, G);
+  if (G > 1)
+    uniform_sample_groups(v, B, out, G);
+  else
+    uniform_sample_body(v, B, out);
 }
 
 // SumTree.sample / stratified_sample (sum_tree.py:99-166) on the flat heap, one

@@ -173,12 +173,99 @@ __device__ inline void per_sample_body(const ReplayView& v, int B, int32_t* out,
 // The draw/validate chain is evaluated 64 words at a time speculatively; a
 // ballot/prefix-count finds where the reference's loop would have stopped.
 // ---------------------------------------------------------------------------
-// G consecutive batches of B (the draws of G sample_index_batch(B) calls in a row, each with
+__device__ inline void uniform_sample_body(const ReplayView& v, int B, int32_t* out) {
+  const int lane = threadIdx.x;
+  dq_replay_meta* meta = v.meta;
+  int64_t pos = meta->tape_pos;
+  const int64_t pos0 = pos;
+  if (meta->status != 0) {
+    if (lane == 0) meta->reserved[0] = pos0;
+    for (int i = lane; i < B; i += kWave) out[i] = 0;
+    return;
+  }
+  const int64_t add_count = meta->add_count;
+  const int64_t cursor = add_count % v.C;
+  int64_t min_id, max_id;
+  if (add_count >= v.C) {
+    min_id = cursor - v.C + v.S - 1;
+    max_id = cursor - v.n;
+  } else {
+    min_id = v.S - 1;
+    max_id = cursor - v.n;
+    if (max_id <= min_id) {
+      if (lane == 0) {
+        latch(meta, DQ_ST_TOO_FEW, 0, 0.0);
+        meta->reserved[0] = pos0;
+      }
+      for (int i = lane; i < B; i += kWave) out[i] = 0;
+      return;
+    }
+  }
+  const uint64_t rng = (uint64_t)(max_id - min_id - 1);
+  uint64_t mask = rng;
+  mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4;
+  mask |= mask >> 8; mask |= mask >> 16; mask |= mask >> 32;
+  const int64_t len = meta->tape_len;
+  int count = 0, fails = 0;
+  bool tape_dry = false;
+  if (rng == 0) {  // randint consumes no word when high - low == 1
+    const int64_t idx = pymod(min_id, v.C);
+    const bool ok = is_valid(v, idx, add_count);
+    if (ok) {
+      for (int i = lane; i < B; i += kWave) out[i] = (int32_t)idx;
+      count = B;
+    } else {
+      fails = v.max_attempts;
+    }
+  } else {
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    while (count < B && fails < v.max_attempts) {
+      const int64_t avail = len - pos;
+      if (avail <= 0) { tape_dry = true; break; }
+      const bool live = lane < avail;
+      const uint64_t w = live ? (uint64_t)v.tape[pos + lane] : 0ull;
+      const uint64_t val = w & mask;
+      const bool drawn = live && val <= rng;
+      const int64_t idx = pymod(min_id + (int64_t)val, v.C);
+      const bool ok = drawn && is_valid(v, idx, add_count);
+      const bool bad = drawn && !ok;
+      const uint64_t okm = __ballot(ok), badm = __ballot(bad);
+      const int cok = count + __popcll(okm & below) + (ok ? 1 : 0);
+      const int cbad = fails + __popcll(badm & below) + (bad ? 1 : 0);
+      const bool stop = (ok && cok == B) || (bad && cbad == v.max_attempts);
+      const uint64_t stopm = __ballot(stop);
+      if (stopm) {
+        const int s = __ffsll((unsigned long long)stopm) - 1;
+        if (ok && lane <= s) out[cok - 1] = (int32_t)idx;
+        count = __shfl(cok, s);
+        fails = __shfl(cbad, s);
+        pos += s + 1;
+        break;
+      }
+      if (ok) out[cok - 1] = (int32_t)idx;
+      count += __popcll(okm);
+      fails += __popcll(badm);
+      const int64_t used = avail < kWave ? avail : kWave;
+      pos += used;
+      if (used < kWave) { tape_dry = true; break; }
+    }
+  }
+  if (lane == 0) {
+    if (tape_dry) latch(meta, DQ_ST_TAPE_EXHAUSTED, count, 0.0);
+    else if (count != B) latch(meta, DQ_ST_MAX_ATTEMPTS, count, 0.0);
+    meta->reserved[0] = pos0;   // entry cursor, for dq_replay_rewind_last_sample
+    meta->tape_pos = pos;
+  }
+}
+
+// G > 1 consecutive batches of B (the draws of G sample_index_batch(B) calls in a row, each with
 // its own max-attempts budget and its own error) into out[g * B + i]: the learner-only loop
 // draws a whole chunk's uniform batches at once (they do not depend on priorities).  The
 // rewind cursor (meta->reserved[0]) is the entry of the LAST batch, so
-// dq_replay_rewind_last_sample gives back exactly the one batch a prefetch holds.
-__device__ inline void uniform_sample_body(const ReplayView& v, int B, int32_t* out, int G = 1) {
+// dq_replay_rewind_last_sample gives back exactly the one batch a prefetch holds.  Riders run
+// inside the CNN's grouped launches, whose GEMM tiles are held to 64 VGPRs: only the launches
+// that carry a grouped sample instantiate this loop (run_rider<T, true>).
+__device__ inline void uniform_sample_groups(const ReplayView& v, int B, int32_t* out, int G) {
   const int lane = threadIdx.x;
   dq_replay_meta* meta = v.meta;
   int64_t pos = meta->tape_pos;
@@ -810,8 +897,9 @@ static_assert(sizeof(RiderDesc) <= sizeof(dq_rider), "dq_rider too small");
 
 constexpr int kRiderLds = kSumtreeParLds > kPerSampleParLds ? kSumtreeParLds : kPerSampleParLds;
 
-// Runs rider r as block blk of a launch with T >= 256 threads per block.
-template <int T>
+// Runs rider r as block blk of a launch with T >= 256 threads per block.  kGroups: the
+// launch carries a grouped uniform sample (the DQN learner loop's chunk gather).
+template <int T, bool kGroups = false>
 __device__ __forceinline__ void run_rider(const RiderDesc& r, int blk, void* lds) {
   static_assert(T % 256 == 0, "rider blocks are whole 256-thread gather sub-blocks");
   const int t = threadIdx.x;
@@ -829,7 +917,12 @@ __device__ __forceinline__ void run_rider(const RiderDesc& r, int blk, void* lds
       per_sample_par<T>(r.v, r.batch, r.out, lds);
       return;
     case kRiderUniformSample:
-      if (t < kWave) uniform_sample_body(r.v, r.batch, r.out, r.groups > 1 ? r.groups : 1);
+      if (t < kWave) {
+        if constexpr (kGroups)
+          uniform_sample_groups(r.v, r.batch, r.out, r.groups > 1 ? r.groups : 1);
+        else
+          uniform_sample_body(r.v, r.batch, r.out);
+      }
       return;
     case kRiderGatherNhwc: {
       const int sub = blk * (T / 256) + t / 256;

@@ -144,17 +144,3 @@ def test_native_comm_is_used_and_collectives_are_identity_for_one_rank(rccl_grou
   parallel._CAPTURABLE.clear()
   assert parallel.collectives_capturable(rccl_group, torch.device('cuda', 0), sharded=True,
                                          comms=agent._rccl)
-
-
-@pytest.mark.timeout(600)
-@pytest.mark.parametrize('native', [True])
-def test_rccl_one_rank_zero1_update_on_second_stream_equals_single_learner(rccl_group, native):
-  """ZeRO-1 with the slice's update on its own stream between the reduce-scatter and the
-  all-gather (comm -> comm_opt -> comm), captured in the learner loop's chunk graphs:
-  the arrangement whose capture_end segfaulted on ROCm 7.2 in round 2."""
-  agent = _agent(rccl_group, 0, shard_optimizer=True, native_comm=native)
-  agent.zero_update_stream = True
-  flat = _run(agent, True).numpy()
-  assert any(k[0] == 'chunk' for k in agent._graph_sets if isinstance(k, tuple))
-  single = _run(_agent(None, 0), True).numpy()
-  assert np.array_equal(flat, single)
