@@ -192,6 +192,8 @@ class DQNAgent(object):
     import torch.distributed as dist
     if not (self.native_comm and self._split_allreduce() and dist.get_backend(self._pg) == 'nccl'):
       return None
+    if not parallel.native_comm_available(self._pg, self._device):
+      return None        # every rank agreed: torch.distributed's collectives instead
     return (parallel.RcclComm(self._pg, self._device), parallel.RcclComm(self._pg, self._device))
 
   def _ar_fc(self, t):

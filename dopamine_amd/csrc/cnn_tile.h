@@ -378,6 +378,60 @@ struct EpiGradAdam {
   }
 };
 
+// gradient + TF1 Adam in the vector (kVec) epilogue form, 4 consecutive columns per call
+// (16-B loads and stores of the gradient, parameter and moments): fc1's weight gradient
+// (512 x 7744 + the bias column) updates fc1 where each tile's gradient is made, instead of
+// storing it for Adam riders in the following launches to read back.  Same arithmetic as
+// EpiGradAdam / k_adam (adam1), element by element.
+struct EpiGradAdamVec {
+  float* gw;
+  float* gb;
+  int nw;                  // nw % 4 == 0 (the column groups never straddle the bias column)
+  float *w, *mw, *vw;
+  float *b, *mb, *vb;
+  AdamDev o;
+  static constexpr bool kVec = true;
+  __device__ __forceinline__ void scalar(int m, int n, float g) const {
+    const float alpha = adam_alpha_of(o.state, o.slot, o.lr);
+    const float omb1 = __fsub_rn(1.0f, o.b1), omb2 = __fsub_rn(1.0f, o.b2);
+    if (n < nw) {
+      const int64_t i = (int64_t)m * nw + n;
+      float pw = w[i], pm = mw[i], pv = vw[i];
+      adam1(pw, g, pm, pv, alpha, omb1, omb2, o.eps);
+      gw[i] = g;
+      w[i] = pw;
+      mw[i] = pm;
+      vw[i] = pv;
+    } else if (n == nw) {
+      float pw = b[m], pm = mb[m], pv = vb[m];
+      adam1(pw, g, pm, pv, alpha, omb1, omb2, o.eps);
+      gb[m] = g;
+      b[m] = pw;
+      mb[m] = pm;
+      vb[m] = pv;
+    }
+  }
+  __device__ __forceinline__ void operator()(int m, int n, float g, int) const { scalar(m, n, g); }
+  __device__ __forceinline__ void vec4(int m, int n, float4 g) const {
+    if (n >= nw) {                 // the bias column (and the tile's padding past it)
+      scalar(m, n, g.x);
+      return;
+    }
+    const int64_t i = (int64_t)m * nw + n;
+    float4 pw = ld4(w + i), pm = ld4(mw + i), pv = ld4(vw + i);
+    const float alpha = adam_alpha_of(o.state, o.slot, o.lr);
+    const float omb1 = __fsub_rn(1.0f, o.b1), omb2 = __fsub_rn(1.0f, o.b2);
+    adam1(pw.x, g.x, pm.x, pv.x, alpha, omb1, omb2, o.eps);
+    adam1(pw.y, g.y, pm.y, pv.y, alpha, omb1, omb2, o.eps);
+    adam1(pw.z, g.z, pm.z, pv.z, alpha, omb1, omb2, o.eps);
+    adam1(pw.w, g.w, pm.w, pv.w, alpha, omb1, omb2, o.eps);
+    *reinterpret_cast<float4*>(gw + i) = g;
+    *reinterpret_cast<float4*>(w + i) = pw;
+    *reinterpret_cast<float4*>(mw + i) = pm;
+    *reinterpret_cast<float4*>(vw + i) = pv;
+  }
+};
+
 // gradient + TF1 RMSProp in one pass (dq_rmsprop_tf1's arithmetic, rms1): m = ms,
 // v = mom, g2 = mg (centered only)
 struct RmsDev {

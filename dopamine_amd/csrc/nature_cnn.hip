@@ -296,6 +296,21 @@ struct OptPart<2> {
   }
 };
 
+// fc1's weight gradient + its optimizer in the vector epilogue (DQ_FC1_EPI_OPT): TF1 Adam
+// over fc1_w and fc1_b, the riders' arithmetic.  Adam only: centered RMSProp's four state
+// arrays made the epilogue the longer path (config 2: 8,060 vs 8,143 steps/s with riders)
+template <int kOpt>
+struct Fc1EpiOpt;
+template <>
+struct Fc1EpiOpt<1> {
+  static EpiGradAdamVec make(const dq_cnn_params* p, const dq_cnn_params* g, const dq_adam_args* o) {
+    const ptrdiff_t ow = p->fc1_w - o->var, ob = p->fc1_b - o->var;
+    return EpiGradAdamVec{g->fc1_w, g->fc1_b, kFlat, p->fc1_w, o->m + ow, o->v + ow, p->fc1_b,
+                          o->m + ob, o->v + ob,
+                          AdamDev{o->state, o->slot, o->lr, o->beta1, o->beta2, o->epsilon}};
+  }
+};
+
 // A recorded replay operation (replay_dev.h) riding in a grouped launch: its
 // blocks come first in the launch so the single-wave sum-tree update / sampler
 // chains start before the GEMM blocks fill the machine.
@@ -760,6 +775,44 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
 #endif
       float* f1 = f0 + (((f3 - f0) * DQ_FC1_A / 24) & ~(int64_t)3);
       float* f2 = f0 + (((f3 - f0) * DQ_FC1_B / 24) & ~(int64_t)3);
+#ifndef DQ_FC1_EPI_OPT
+#define DQ_FC1_EPI_OPT 1
+#endif
+      // TF1 Adam on fc1 in its weight-gradient GEMM's (vector) epilogue, launch 2, instead of
+      // Adam riders over fc1 in launches 3-5 reading the stored gradient back (+0.6-1.2%
+      // config 1: 7,600-7,644 vs 7,555-7,559 steps/s)
+      if constexpr (kHeadFrom >= 5 && kOpt == 1 && DQ_FC1_EPI_OPT) {
+        auto dW_fc1a = gemm_op<4, 4, 1>(ColK{d->h, kHidden}, ColKOnes{a->a3, kFlat},
+                                        Fc1EpiOpt<kOpt>::make(p, g, opt.a), kHidden, kFlat + 1,
+                                        B, B);
+        auto sum_c2a = ReduceOp<decltype(GE::make(0, 0, 0, 0, 0, opt, 0))>{
+            ws + o2, nz3, 64, Conv2::K + 1,
+            GE::make(g->conv2_w, g->conv2_b, Conv2::K, p->conv2_w, p->conv2_b, opt, 0)};
+        if (in(0)) group_r(c, rd(0), dX_fc2);
+        if (in(1)) group_r(c, rd(1), dW_fc2, dX_fc1);
+        if (in(2)) group_r(c, rd(2), dW_fc1a, dX_c3, part(p->fc2_w, p->fc2_b + NO));
+        if (kHeadFrom == 6) {
+          if (in(3)) group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11, dW_c2);
+          if (in(4)) group_r(c, rd(4), sum_c3, dW_c1);
+          if (in(5)) {
+            if (head)
+              group_r(c, rd(5), sum_c2a, sum_c1, part(p->conv3_w, p->fc1_w), head->conv1());
+            else
+              group_r(c, rd(5), sum_c2a, sum_c1, part(p->conv3_w, p->fc1_w));
+          }
+          return;
+        }
+        if (in(3)) group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11);
+        if (head) {
+          if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, dW_c1, head->conv1());
+          if (in(5))
+            group_r(c, rd(5), sum_c2a, sum_c1, part(p->conv3_w, p->fc1_w), head->conv2());
+        } else {
+          if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, dW_c1);
+          if (in(5)) group_r(c, rd(5), sum_c2a, sum_c1, part(p->conv3_w, p->fc1_w));
+        }
+        return;
+      }
       if constexpr (kHeadFrom >= 5) {
         // five launches: conv2's input gradient by sub-pixel class needs only da2, so
         // conv1's weight-gradient slabs join launch 4 and the three split-K sums end

@@ -144,6 +144,17 @@ class RcclComm(object):
       self._h = None
 
 
+def native_comm_available(group, device):
+  """Whether EVERY rank of ``group`` can open RCCL for RcclComm (dq_comm_version): the ranks
+  agree (MIN all-reduce) before any of them enters the collective communicator init, so a
+  rank that cannot does not leave the others blocked in it."""
+  from dopamine_amd import _lib
+  ok = 1.0 if int(_lib.lib.dq_comm_version()) > 0 else 0.0
+  t = torch.tensor([ok], device=device if dist.get_backend(group) == 'nccl' else 'cpu')
+  dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+  return bool(t.item() == 1.0)
+
+
 def replicas_in_sync(flat_params, group=None):
   """Checksum-broadcast check that every rank holds identical parameters."""
   s = torch.stack([flat_params.double().sum(), (flat_params.double() ** 2).sum()])
