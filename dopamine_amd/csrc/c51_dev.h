@@ -10,8 +10,19 @@ namespace dq {
 // Logit sources: stored logits, or (the fused Rainbow path) fc2's 16 k-band
 // partial products summed in band order plus the bias -- exactly the reduction
 // order of the CNN's fc2 tile, so the logits are bitwise dq_cnn_forward's.
+// load() issues an element's loads, sum() forms it from them (get = sum(load)): a kernel
+// can put independent work between the two while the loads are in flight.
 struct LogitsDirect {
   const float* p;
+  int NO;
+  struct Pend {
+    float v;
+  };
+  __device__ __forceinline__ Pend load(int64_t i) const { return Pend{p[i]}; }
+  __device__ __forceinline__ Pend load_bc(int b, int col) const {
+    return Pend{p[(int64_t)b * NO + col]};
+  }
+  __device__ __forceinline__ float sum(const Pend& q) const { return q.v; }
   __device__ __forceinline__ float get(int64_t i) const { return p[i]; }
 };
 struct LogitsParts {
@@ -19,6 +30,35 @@ struct LogitsParts {
   const float* bias;   // [NO]
   int64_t stride;      // B * NO
   int np, NO;          // np <= 16: straight-line loads, all in flight before the first add
+  struct Pend {
+    float v[16];
+    float bias;
+  };
+  // element (b, col) of the (B, NO) logits: one buffer load per slab -- the slab's byte
+  // offset in a scalar register, the element's in a 32-bit vector one (the slabs span
+  // < 2 GB) -- so the loss kernel's prologue has no 64-bit address or index arithmetic
+  __device__ __forceinline__ Pend load_bc(int b, int col) const {
+    Pend q;
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(part), 0, 0x7fffffff,
+                                                        0x00020000);
+    const int off = (b * NO + col) * 4;
+#pragma unroll
+    for (int z = 0; z < 16; ++z)
+      q.v[z] = __builtin_bit_cast(
+          float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, off, (int)(min(z, np - 1) * stride * 4), 0));
+    q.bias = bias[col];
+    return q;
+  }
+  __device__ __forceinline__ Pend load(int64_t i) const {
+    return load_bc((int)(i / NO), (int)(i % NO));
+  }
+  __device__ __forceinline__ float sum(const Pend& q) const {   // get()'s order
+    float x = q.v[0];
+#pragma unroll
+    for (int z = 1; z < 16; ++z)
+      if (z < np) x = __fadd_rn(x, q.v[z]);
+    return __fadd_rn(x, q.bias);
+  }
   __device__ __forceinline__ float get(int64_t i) const {
     float v[16];
 #pragma unroll
@@ -61,6 +101,24 @@ __device__ __forceinline__ float fast_min(float v) {
   v = fminf(v, dpp_ror<0x122>(v));
   v = fminf(v, dpp_ror<0x121>(v));
   return fminf(fminf(rl(v, 0), rl(v, 16)), fminf(rl(v, 32), rl(v, 48)));
+}
+
+// The fused d h's dot product for column `col` of LDS-resident W2 rows (row stride `ld`):
+// sum_i g_i W2[i][col] as four interleaved partial sums (i mod 4, each in i order) added
+// pairwise -- a 13-deep dependent add chain instead of N = 51, the loss kernels' tail.
+// k_c51 and k_c51_online share it, so their d h stay bitwise equal.
+__device__ __forceinline__ float dh_dot(const float* s_g, const float* s_w, int ld, int col, int N) {
+  float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  int i = 0;
+  for (; i + 8 <= N; i += 8) {
+    float t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] = __fmul_rn(s_g[i + u], s_w[(i + u) * ld + col]);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc[u & 3] = __fadd_rn(acc[u & 3], t[u]);
+  }
+  for (; i < N; ++i) acc[i & 3] = __fadd_rn(acc[i & 3], __fmul_rn(s_g[i], s_w[i * ld + col]));
+  return __fadd_rn(__fadd_rn(acc[0], acc[1]), __fadd_rn(acc[2], acc[3]));
 }
 
 // The target half of the C51 loss for sample b, split off k_c51 so it can ride in the

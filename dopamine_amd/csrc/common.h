@@ -40,9 +40,44 @@ void set_error(const std::string& msg);
 
 constexpr int kWave = 64;
 
-// Python / numpy floor modulo for a positive modulus.
+// Warm the scalar cache with a kernel's argument block: one s_load per 64-byte line, all in
+// flight together and waited for once.  The compiler loads argument fields lazily, each
+// behind the branch that needs it (an op of a grouped launch, a compile-time-absent
+// pointer), so without this a launch pays one dependent scalar miss round per branch
+// level before its first global load.  kBytes: the explicit arguments' size (reading a
+// line past them stays inside the argument block, whose hidden arguments follow).
+template <int kBytes>
+__device__ __forceinline__ void warm_kernargs() {
+  typedef const uint32_t __attribute__((address_space(4)))* KPtr;
+  const KPtr p = (KPtr)__builtin_amdgcn_kernarg_segment_ptr();
+  constexpr int n = (kBytes + 63) / 64;
+  static_assert(n <= 32, "argument block larger than the warm-up covers");
+#ifndef DQ_NO_WARM
+  uint32_t v[32];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) v[i] = p[(i < n ? i : n - 1) * 16];   // all issued, then
+#pragma unroll
+  for (int i = 0; i < 32; i += 8)                                   // one wait for all
+    if (i < n)
+      asm volatile("" ::"s"(v[i]), "s"(v[i + 1]), "s"(v[i + 2]), "s"(v[i + 3]), "s"(v[i + 4]),
+                   "s"(v[i + 5]), "s"(v[i + 6]), "s"(v[i + 7]));
+#endif
+}
+
+// IEEE square root, correctly rounded, as TF1's CPU kernels (std::sqrt) and numpy compute
+// it.  hipcc's __fsqrt_rn is __ocml_native_sqrt_f32 -- v_sqrt_f32 with denormal scaling,
+// not correctly rounded -- unless OCML_BASIC_ROUNDED_OPERATIONS is defined; the builtin
+// lowers to the exact expansion (v_sqrt_f32, then the +-1 ulp residual test).
+__device__ __forceinline__ float sqrt_rn(float x) { return __builtin_sqrtf(x); }
+
+// Python / numpy floor modulo for a positive modulus.  The replay's operands are almost
+// always within one period of [0, m) (a sampled index, index + k for a short trajectory or
+// frame stack): those take a compare and an add; only the rest run the 64-bit division,
+// whose ~130-instruction software sequence sat in the gather's index -> frame-address
+// chain four times per wave.
 __device__ __forceinline__ int64_t pymod(int64_t a, int64_t m) {
-  int64_t r = a % m;
+  if (a >= -m && a < 2 * m) return a < 0 ? a + m : (a >= m ? a - m : a);
+  const int64_t r = a % m;
   return r < 0 ? r + m : r;
 }
 
@@ -70,7 +105,7 @@ __device__ __forceinline__ float wave_min(float v) {
 __device__ __forceinline__ float adam_alpha_of(const float* state, int slot, float lr) {
   const float b1p = state[2 * slot], b2p = state[2 * slot + 1];
   // alpha = lr * sqrt(1 - beta2^t) / (1 - beta1^t)
-  return __fdiv_rn(__fmul_rn(lr, __fsqrt_rn(__fsub_rn(1.0f, b2p))), __fsub_rn(1.0f, b1p));
+  return __fdiv_rn(__fmul_rn(lr, sqrt_rn(__fsub_rn(1.0f, b2p))), __fsub_rn(1.0f, b1p));
 }
 
 __device__ __forceinline__ void adam_bump(float* state, int slot, float b1, float b2) {
@@ -83,7 +118,7 @@ __device__ __forceinline__ void adam1(float& var, float g, float& m, float& v, f
                                       float omb1, float omb2, float eps) {
   m = __fadd_rn(m, __fmul_rn(__fsub_rn(g, m), omb1));
   v = __fadd_rn(v, __fmul_rn(__fsub_rn(__fmul_rn(g, g), v), omb2));
-  var = __fsub_rn(var, __fdiv_rn(__fmul_rn(m, alpha), __fadd_rn(__fsqrt_rn(v), eps)));
+  var = __fsub_rn(var, __fdiv_rn(__fmul_rn(m, alpha), __fadd_rn(sqrt_rn(v), eps)));
 }
 
 // ---- TF1 ApplyRMSProp / ApplyCenteredRMSProp (omr = 1 - rho), shared by k_rmsprop and
@@ -99,7 +134,7 @@ __device__ __forceinline__ void rms1(float& var, float g, float& ms, float& mg, 
   } else {
     denom = __fadd_rn(ms, eps);
   }
-  mom = __fadd_rn(__fmul_rn(mom, mu), __fdiv_rn(__fmul_rn(g, lr), __fsqrt_rn(denom)));
+  mom = __fadd_rn(__fmul_rn(mom, mu), __fdiv_rn(__fmul_rn(g, lr), sqrt_rn(denom)));
   var = __fsub_rn(var, mom);
 }
 

@@ -4,6 +4,8 @@
 // Restates the TF1 graph code of rainbow_agent.py:200-305 + 340-494,
 // dqn_agent.py:283-322, implicit_quantile_agent.py:190-321 and the TF1
 // ApplyAdam / ApplyCenteredRMSProp op semantics.
+#include <algorithm>
+
 #include "c51_dev.h"
 
 namespace dq {
@@ -52,6 +54,8 @@ struct C51Extra {
 __device__ long long g_c51_t[256][8];
 __device__ long long g_c51_w[256][16];
 __device__ long long g_c51_w2[256][16];
+__device__ long long g_c51_w0[256][16];
+#define C51_W0() if ((threadIdx.x & 63) == 0) g_c51_w0[blockIdx.x][threadIdx.x >> 6] = wall_clock64()
 #define C51_T(k) if (threadIdx.x == 0) g_c51_t[blockIdx.x][k] = wall_clock64()
 #define C51_W2() if ((threadIdx.x & 63) == 0) g_c51_w2[blockIdx.x][threadIdx.x >> 6] = wall_clock64()
 #define C51_W() if ((threadIdx.x & 63) == 0) g_c51_w[blockIdx.x][threadIdx.x >> 6] = wall_clock64()
@@ -59,19 +63,40 @@ __device__ long long g_c51_w2[256][16];
 #define C51_T(k)
 #define C51_W()
 #define C51_W2()
+#define C51_W0()
 #endif
-template <class LS>
+// Compile-time switches of k_c51 (the runtime pointers they stand for are non-NULL exactly
+// when the bit is set): no kernel-argument test is left in the chain, so the compiler loads
+// the arguments in one batch instead of one dependent scalar round per branch.
+constexpr int kC51Probs = 1, kC51W2 = 2, kC51LogitsOut = 4;
+#ifndef DQ_C51_SPLIT
+#define DQ_C51_SPLIT 4
+#endif
+
+// LDS floats of k_c51's head (before the fused path's W2 rows), 4-float aligned
+__host__ __device__ constexpr int c51_head_floats(int A, int N, int nw) {
+  return (A * N + A + N + N * kWave + 2 * nw * kWave + 3) / 4 * 4;
+}
+
+template <class LS, int kF>
 __global__ __launch_bounds__(1024) void k_c51(C51Args a, LS ol, LS tl, C51Extra x) {
+  constexpr bool kProbs = kF & kC51Probs, kW2 = kF & kC51W2, kOut = kF & kC51LogitsOut;
+  warm_kernargs<sizeof(C51Args) + 2 * sizeof(LS) + sizeof(C51Extra)>();
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int N = a.N, A = a.A, b = blockIdx.x, T = blockDim.x;
+  // S blocks per sample (gridDim.x = B * S): each runs the whole loss chain (latency-bound,
+  // so the copies cost nothing) and forms d h for its 1/S of the H columns -- the W2 rows'
+  // LDS traffic, what bounds that product, split over S CUs.  Part 0 writes the outputs.
+  const int N = a.N, A = a.A, T = blockDim.x, S = gridDim.x / a.B;
+  const int b = blockIdx.x / S, part = blockIdx.x - b * S, HS = kW2 ? x.H / S : 0;
+  const bool writer = part == 0;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = T >> 6;
   float* s_p = smem;                 // [A][N] target probabilities
   float* s_q = s_p + A * N;          // [A]    target Q
-  float* s_tz = s_q + A;             // [N]    clipped Bellman support
-  float* s_g = s_tz + N;             // [N]    the chosen action's logit gradient
-  float* s_c = s_g + N;              // [N][64] projection terms c(i, j) p_j
-  float* s_w = smem + (A * N + A + 2 * N + N * kWave + 3) / 4 * 4;   // [N][H] fc2 rows, 16-B aligned
-  __shared__ float s_red[16];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = T >> 6;
+  float* s_g = s_q + A;              // [N]    the chosen action's logit gradient
+  float* s_c = s_g + N;              // [N][64] projection terms c(i, j)
+  int* s_lo = reinterpret_cast<int*>(s_c + N * kWave);   // [nw][64] first / last source atom
+  int* s_hi = s_lo + nw * kWave;                          // with c(i, j) > 0, per wave
+  float* s_w = smem + c51_head_floats(A, N, nw);          // [N][HS] fc2 row slices, 16-B aligned
   const bool on = lane < N;
   const float ninf = -__builtin_inff();
   C51_T(0);
@@ -81,48 +106,62 @@ __global__ __launch_bounds__(1024) void k_c51(C51Args a, LS ol, LS tl, C51Extra 
   const int ab = a.act[b];
   const float rew_b = a.rew[b], term_b = (float)a.term[b];
   const float vmin = a.support[0], vmax = a.support[N - 1], z1 = a.support[1];
-  const float pr_t = a.probs ? a.probs[min((int)threadIdx.x, a.B - 1)] : 0.0f;
-  const float pr_b = a.probs ? a.probs[b] : 0.0f;
-  const float hv = x.w2 ? x.h[(int64_t)b * x.H + min((int)threadIdx.x, x.H - 1)] : 0.0f;
+  // PER: every wave loads all B probabilities (B <= 64: one per lane) and takes their min
+  // itself, so the importance weight needs no cross-wave step
+  const float pr_t = kProbs ? a.probs[min(lane, a.B - 1)] : 0.0f;
+  const float pr_b = kProbs ? a.probs[b] : 0.0f;
+  const float hv = kW2 ? x.h[(int64_t)b * x.H + part * HS + min((int)threadIdx.x, HS - 1)] : 0.0f;
   // the chosen online logit row (wave 0 uses it last) and the first target row of each
   // wave (nw <= A): loaded by every lane at clamped indices, so both rows' loads sit in one
   // basic block and are all in flight before the first wait
+  // (their sums are formed after the c(i, j) loop below, which runs under the loads)
   const int lc = min(lane, N - 1);
-  const float x0 = tl.get(((int64_t)b * A + wave) * N + lc);   // (not behind act[b])
-  float y = ninf;
-  if (wave == 0) {            // (the vector-memory issue of 16-band rows is what costs)
-    const float y0 = ol.get(((int64_t)b * A + ab) * N + lc);
-    y = on ? y0 : ninf;
-  }
-  float xv[4];
-  xv[0] = on ? x0 : ninf;
-#pragma unroll
-  for (int r = 1; r < 4; ++r) {
-    const int act = wave + r * nw;
-    xv[r] = (act < A && on) ? tl.get(((int64_t)b * A + act) * N + lane) : ninf;
-  }
+  const typename LS::Pend x0 = tl.load_bc(b, min(wave, A - 1) * N + lc);   // (not behind act[b])
+  typename LS::Pend y0;
+  if (wave == 0)              // (the vector-memory issue of 16-band rows is what costs)
+    y0 = ol.load_bc(b, ab * N + lc);
   // The Eq.-7 clipped quotients c(i, j) = clip(1 - |clip(Tz_j) - z_i| / dz, 0, 1) need only
   // the reward, the terminal flag and the support: formed now, while the logits load
-  // (wave w takes source atoms j = w, w + nw, ...; lane = target atom i)
+  // (wave w takes source atoms j = w, w + nw, ...; lane = target atom i).  clip(Tz_j) is
+  // non-decreasing in j, so the j with c(i, j) > 0 are one run [lo_i, hi_i]: each wave
+  // records its own first and last such j per lane.
   {
     const float dz = __fsub_rn(z1, vmin);
     const float gt = __fmul_rn(a.cg, __fsub_rn(1.0f, term_b));
+    C51_W0();
+    int lo = kWave, hi = -1;
     for (int j = __builtin_amdgcn_readfirstlane(wave); j < N; j += nw) {
       const float zj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(z), j));
       const float tzj = fminf(fmaxf(__fadd_rn(rew_b, __fmul_rn(gt, zj)), vmin), vmax);
       if (on) {
         float c = __fsub_rn(1.0f, __fdiv_rn(fabsf(__fsub_rn(tzj, z)), dz));
-        s_c[j * kWave + lane] = fminf(fmaxf(c, 0.0f), 1.0f);
+        c = fminf(fmaxf(c, 0.0f), 1.0f);
+        s_c[j * kWave + lane] = c;
+        if (c > 0.0f) {
+          lo = min(lo, j);
+          hi = j;
+        }
       }
     }
+    s_lo[wave * kWave + lane] = lo;
+    s_hi[wave * kWave + lane] = hi;
   }
   C51_W2();
+  float y = ninf;
+  if (wave == 0) y = on ? ol.sum(y0) : ninf;
+  float xv[4];
+  xv[0] = (wave < A && on) ? tl.sum(x0) : ninf;
+#pragma unroll
+  for (int r = 1; r < 4; ++r) {
+    const int act = wave + r * nw;
+    xv[r] = (act < A && on) ? tl.sum(tl.load_bc(b, act * N + lane)) : ninf;
+  }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int act = wave + r * nw;
     if (act >= A) break;
     const float v = xv[r];
-    if (x.tl_out && on) x.tl_out[((int64_t)b * A + act) * N + lane] = v;
+    if (kOut && x.tl_out && on && writer) x.tl_out[((int64_t)b * A + act) * N + lane] = v;
     const float mx = fast_max(v);
     const float e = on ? expf(__fsub_rn(v, mx)) : 0.0f;
     const float p = __fdiv_rn(e, fast_sum(e));
@@ -132,19 +171,18 @@ __global__ __launch_bounds__(1024) void k_c51(C51Args a, LS ol, LS tl, C51Extra 
   }
   C51_T(1);
   C51_W();
-  // PER importance weights (rb:277-280): w_b = r(p_b) / max_i r(p_i), r(p) = 1 / sqrt(p + eps).
-  // r rounds monotonically (non-increasing), so max_i r(p_i) = r(min_i p_i) exactly: each
-  // wave's min joins the barrier that completes s_p and s_q.  Formed here, before the
-  // LDS-DMA below, so no wait on a plain load can drain it.
-  if (a.probs) {
-    float pm = pr_t;
-    for (int i = threadIdx.x + T; i < a.B; i += T) pm = fminf(pm, a.probs[i]);
-    pm = fast_min(pm);
-    if (lane == 0) s_red[wave] = pm;
-  }
-  // the chosen online row's softmax terms (wave 0), likewise before the LDS-DMA
-  float sh = 0.0f, ey = 0.0f, lse = 0.0f, py = 0.0f;
+  // the chosen online row's softmax terms and the PER importance weight (wave 0), before
+  // the barrier.  rb:277-280: w_b = r(p_b) / max_i r(p_i), r(p) = 1 / sqrt(p + eps); r
+  // rounds monotonically (non-increasing), so max_i r(p_i) = r(min_i p_i) exactly.
+  float sh = 0.0f, ey = 0.0f, lse = 0.0f, py = 0.0f, w = 1.0f;
   if (wave == 0) {
+    if (kProbs) {
+      float pm = pr_t;
+      for (int i = lane + kWave; i < a.B; i += kWave) pm = fminf(pm, a.probs[i]);
+      pm = fast_min(pm);
+      const float m = __fdiv_rn(1.0f, sqrt_rn(__fadd_rn(pm, 1e-10f)));
+      w = __fdiv_rn(__fdiv_rn(1.0f, sqrt_rn(__fadd_rn(pr_b, 1e-10f))), m);
+    }
     const float my = fast_max(y);
     sh = on ? __fsub_rn(y, my) : 0.0f;
     ey = on ? expf(sh) : 0.0f;
@@ -152,99 +190,116 @@ __global__ __launch_bounds__(1024) void k_c51(C51Args a, LS ol, LS tl, C51Extra 
     lse = logf(sy);
     py = __fdiv_rn(ey, sy);
   }
-  if (x.ol_out)
+  if (kOut && x.ol_out && writer)
     for (int act = wave; act < A; act += nw) {
       const int64_t i = ((int64_t)b * A + act) * N + lane;
       if (on) x.ol_out[i] = act == ab && wave == 0 ? y : ol.get(i);
     }
-  // s_p, s_q, s_c, s_red complete.  A bare barrier: __syncthreads' release fence would
-  // also wait for vmcnt(0), i.e. for the whole LDS-DMA just issued
+  // s_p, s_q, s_c, s_lo/hi complete.  A bare barrier: __syncthreads' release fence would
+  // also wait for vmcnt(0), i.e. for the whole LDS-DMA issued next
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   C51_T(2);
-  // fused d h: this sample's N contiguous W2 rows (N x H floats) stream into LDS by
-  // LDS-DMA (global_load_lds, 1 KB per wave instruction, no registers), landing under
-  // the rest of the loss chain.  Issued by waves 1.. (wave 0 runs the chain) after the
-  // barrier, so neither the chain nor the barrier waits behind the issue.
-  if (x.w2 && (wave > 0 || nw == 1)) {
-    const int bytes = N * x.H * 4, nq = (bytes + 1023) >> 10;
+  // fused d h: this block's column slice of the chosen action's N W2 rows (N x HS floats)
+  // streams into LDS by LDS-DMA (global_load_lds: 16 B per lane from its own address, 1 KB
+  // contiguous in LDS per wave instruction, no registers), landing under the rest of the
+  // loss chain.  Issued by waves 1.. (wave 0 runs the chain) after the
+  // barrier, so neither the chain nor the barrier waits behind the issue.  (Measured: the
+  // rows as plain loads into registers, issued with the logits or after the softmax,
+  // queue the logits' loads behind them: 7,585 / 7,610 vs 7,700 steps/s.)
+  if (kW2 && (wave > 0 || nw == 1)) {
+    const int rc = HS >> 2, chunks = N * rc, nq = (chunks + 63) >> 6;   // 16-B chunks
     const int w0 = nw > 1 ? wave - 1 : 0, nwd = nw > 1 ? nw - 1 : 1;
-    const char* src = reinterpret_cast<const char*>(x.w2 + (int64_t)ab * N * x.H);
+    const float* src = x.w2 + (int64_t)ab * N * x.H + part * HS;
     for (int q = w0; q < nq; q += nwd) {
-      const int off = min(q * 1024 + lane * 16, bytes - 16);   // the tail re-reads in-bounds bytes
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + off),
+      const int c = min(q * 64 + lane, chunks - 1);   // the tail re-reads in-bounds chunks
+      const int row = c / rc;
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + (int64_t)row * x.H +
+                                                                     4 * (c - row * rc)),
                                        (__attribute__((address_space(3))) void*)(
                                            reinterpret_cast<char*>(s_w) + q * 1024),
                                        16, 0, 0);
     }
   }
-  float w = 1.0f;
-  if (a.probs) {
-    float pm = s_red[0];
-    for (int i = 1; i < nw; ++i) pm = fminf(pm, s_red[i]);
-    const float m = __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(pm, 1e-10f)));
-    w = __fdiv_rn(__fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(pr_b, 1e-10f))), m);
-  }
   C51_T(3);
   const float gscale = __fmul_rn(w, __fdiv_rn(1.0f, (float)a.B));
-  for (int act = wave; act < A; act += nw) {
+  for (int act = wave; act < A && writer; act += nw) {
     if (act == ab) continue;
     if (on) a.grad[((int64_t)b * A + act) * N + lane] = 0.0f;
   }
-  // greedy target action (first max) and Tz, redundantly per wave (no barrier)
-  int astar = 0;
-  const float qv = lane < A ? s_q[lane] : 0.0f;   // one LDS read, then lane reads (A <= 64)
-  float best = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qv), 0));
-  for (int act = 1; act < A; ++act) {
-    const float qa = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qv), act));
-    if (qa > best) {
-      best = qa;
-      astar = act;
-    }
-  }
-  const float* pst = s_p + astar * N;
   if (wave == 0) {
-    float proj = 0.0f;        // sum_j c(i, j) p_j in j order (rb:340-494)
-    if (on) {
+    // greedy target action (first max)
+    int astar = 0;
+    const float qv = lane < A ? s_q[lane] : 0.0f;   // one LDS read, then lane reads (A <= 64)
+    float best = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qv), 0));
+    for (int act = 1; act < A; ++act) {
+      const float qa = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qv), act));
+      if (qa > best) {
+        best = qa;
+        astar = act;
+      }
+    }
+    const float* pst = s_p + astar * N;
+    // sum_j c(i, j) p_j in j order (rb:340-494) over the run [lo, hi] only: every other
+    // term is c = 0 times a finite p >= 0, i.e. +0, and adding +0 to the non-negative
+    // partial sum changes no bit -- the same sum as all N terms, in 8-term batches
+    int lo = kWave, hi = -1;
+    for (int v = 0; v < nw; ++v) {
+      lo = min(lo, s_lo[v * kWave + lane]);
+      hi = max(hi, s_hi[v * kWave + lane]);
+    }
+    float proj = 0.0f;       // (lanes >= N: lo > hi, no term)
+    if (term_b != 0.0f || a.cg == 0.0f) {
+      // gamma_t = 0: every source atom lands on clip(r), c(i, j) = c(i, 0) for all j and the
+      // run is all N atoms -- the same j-ordered sum with c in a register and p_j read
+      // across lanes (no per-term LDS round trip)
+      const float ci = on ? s_c[lane] : 0.0f;
+      const float pl = pst[lc];
       int j = 0;
-      for (; j + 8 <= N; j += 8) {      // 8 terms' LDS reads in flight, then summed in j order
+      for (; j + 8 <= N; j += 8) {   // the lane reads of a batch ahead of its add chain
         float t[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) t[u] = __fmul_rn(s_c[(j + u) * kWave + lane], pst[j + u]);
+        for (int u = 0; u < 8; ++u)
+          t[u] = __fmul_rn(ci, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pl), j + u)));
 #pragma unroll
         for (int u = 0; u < 8; ++u) proj = __fadd_rn(proj, t[u]);
       }
-      for (; j < N; ++j) proj = __fadd_rn(proj, __fmul_rn(s_c[j * kWave + lane], pst[j]));
+      for (; j < N; ++j)
+        proj = __fadd_rn(proj, __fmul_rn(ci, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pl), j))));
+      lo = 0;
+      hi = -1;
+    }
+    for (int j = lo; j <= hi; j += 8) {   // 8 terms' LDS reads in flight, then summed in order
+      float t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {       // unconditional (clamped) reads, then a select:
+        const int jj = min(j + u, N - 1); // a guarded read became a branch per term
+        const float tt = __fmul_rn(s_c[jj * kWave + lane], pst[jj]);
+        t[u] = j + u <= hi ? tt : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) proj = __fadd_rn(proj, t[u]);
     }
     const float loss = fast_sum(on ? __fmul_rn(proj, __fsub_rn(lse, sh)) : 0.0f);
     const float gr = on ? __fmul_rn(gscale, __fsub_rn(py, proj)) : 0.0f;
     if (on) {
-      a.grad[((int64_t)b * A + ab) * N + lane] = gr;
+      if (writer) a.grad[((int64_t)b * A + ab) * N + lane] = gr;
       s_g[lane] = gr;
     }
-    if (lane == 0) {
+    if (lane == 0 && writer) {
       if (a.loss_out) a.loss_out[b] = loss;
-      if (a.prio_out) a.prio_out[b] = __fsqrt_rn(__fadd_rn(loss, 1e-10f));
+      if (a.prio_out) a.prio_out[b] = sqrt_rn(__fadd_rn(loss, 1e-10f));
     }
   }
   C51_T(4);
-  if (!x.w2) return;
+  if (!kW2) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's LDS-DMA has landed
   __syncthreads();
   C51_T(5);
-  // d h[b][j] = (h[b][j] > 0) * sum_i g_i W2[ab*N + i][j], i in order
-  for (int j = threadIdx.x; j < x.H; j += T) {
-    const float m = j == (int)threadIdx.x ? hv : x.h[(int64_t)b * x.H + j];
-    float acc = 0.0f;
-    int i = 0;
-    for (; i + 8 <= N; i += 8) {
-      float t[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) t[u] = __fmul_rn(s_g[i + u], s_w[(i + u) * x.H + j]);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) acc = __fadd_rn(acc, t[u]);
-    }
-    for (; i < N; ++i) acc = __fadd_rn(acc, __fmul_rn(s_g[i], s_w[i * x.H + j]));
-    x.dh[(int64_t)b * x.H + j] = m > 0.0f ? acc : 0.0f;
+  // d h[b][j] = (h[b][j] > 0) * sum_i g_i W2[ab*N + i][j] (dh_dot's order), j in this block's slice
+  for (int jl = threadIdx.x; jl < HS; jl += T) {
+    const float m = jl == (int)threadIdx.x ? hv : x.h[(int64_t)b * x.H + part * HS + jl];
+    const float acc = dh_dot(s_g, s_w, HS, jl, N);
+    x.dh[(int64_t)b * x.H + part * HS + jl] = m > 0.0f ? acc : 0.0f;
   }
   C51_T(6);
 }
@@ -254,6 +309,8 @@ extern "C" int dq_debug_c51_times(long long* out) {
 }
 extern "C" int dq_debug_c51_wave_times(long long* out) {
   if (hipMemcpyFromSymbol(out + 256 * 16, HIP_SYMBOL(g_c51_w2), sizeof(g_c51_w2)) != hipSuccess)
+    return -1;
+  if (hipMemcpyFromSymbol(out + 2 * 256 * 16, HIP_SYMBOL(g_c51_w0), sizeof(g_c51_w0)) != hipSuccess)
     return -1;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_c51_w), sizeof(g_c51_w)) == hipSuccess ? 0 : -1;
 }
@@ -268,6 +325,7 @@ extern "C" int dq_debug_c51_wave_times(long long* out) {
 template <class LS>
 __global__ __launch_bounds__(1024) void k_c51_online(C51Args a, LS ol, const float* __restrict__ m,
                                                      C51Extra x) {
+  warm_kernargs<sizeof(C51Args) + sizeof(LS) + 8 + sizeof(C51Extra)>();
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int N = a.N, A = a.A, b = blockIdx.x, T = blockDim.x;
   float* s_g = smem;                                   // [N] the chosen row's logit gradient
@@ -325,8 +383,8 @@ __global__ __launch_bounds__(1024) void k_c51_online(C51Args a, LS ol, const flo
   if (a.probs) {
     float pm = s_red[0];
     for (int i = 1; i < nw; ++i) pm = fminf(pm, s_red[i]);
-    const float mm = __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(pm, 1e-10f)));
-    w = __fdiv_rn(__fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(pr_b, 1e-10f))), mm);
+    const float mm = __fdiv_rn(1.0f, sqrt_rn(__fadd_rn(pm, 1e-10f)));
+    w = __fdiv_rn(__fdiv_rn(1.0f, sqrt_rn(__fadd_rn(pr_b, 1e-10f))), mm);
   }
   const float gscale = __fmul_rn(w, __fdiv_rn(1.0f, (float)a.B));
   for (int act = wave; act < A; act += nw) {
@@ -342,7 +400,7 @@ __global__ __launch_bounds__(1024) void k_c51_online(C51Args a, LS ol, const flo
     }
     if (lane == 0) {
       if (a.loss_out) a.loss_out[b] = loss;
-      if (a.prio_out) a.prio_out[b] = __fsqrt_rn(__fadd_rn(loss, 1e-10f));
+      if (a.prio_out) a.prio_out[b] = sqrt_rn(__fadd_rn(loss, 1e-10f));
     }
   }
   if (!x.w2) return;
@@ -350,25 +408,14 @@ __global__ __launch_bounds__(1024) void k_c51_online(C51Args a, LS ol, const flo
   __syncthreads();
   for (int j = threadIdx.x; j < x.H; j += T) {
     const float mk = j == (int)threadIdx.x ? hv : x.h[(int64_t)b * x.H + j];
-    float acc = 0.0f;
-    int i = 0;
-    for (; i + 8 <= N; i += 8) {
-      float tt[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) tt[u] = __fmul_rn(s_g[i + u], s_w[(i + u) * x.H + j]);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) acc = __fadd_rn(acc, tt[u]);
-    }
-    for (; i < N; ++i) acc = __fadd_rn(acc, __fmul_rn(s_g[i], s_w[i * x.H + j]));
+    const float acc = dh_dot(s_g, s_w, x.H, j, N);
     x.dh[(int64_t)b * x.H + j] = mk > 0.0f ? acc : 0.0f;
   }
 }
 
-// dynamic LDS of k_c51 (bytes), with the fused path's W2 rows when they fit the prefetch
-static size_t c51_lds(int A, int N, int H) {
-  // s_w must be 16-byte aligned for the LDS-DMA: round the head up to 4 floats
-  const size_t head = ((size_t)A * N + A + 2 * N + (size_t)N * kWave + 3) / 4 * 4;
-  return (head + (size_t)N * H) * sizeof(float);
+// dynamic LDS of k_c51 (bytes): the head, plus the W2 rows in the LDS-DMA form
+static size_t c51_lds(int A, int N, int H, int nw) {
+  return ((size_t)c51_head_floats(A, N, nw) + (size_t)N * H) * sizeof(float);
 }
 
 // mean(w * loss) for summaries (rb:298-301); launched only when requested.
@@ -378,12 +425,12 @@ __global__ __launch_bounds__(64) void k_wmean(const float* loss, const float* pr
   if (probs) {
     float m = 0.0f;
     for (int i = threadIdx.x; i < B; i += 64)
-      m = fmaxf(m, __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(probs[i], 1e-10f))));
+      m = fmaxf(m, __fdiv_rn(1.0f, sqrt_rn(__fadd_rn(probs[i], 1e-10f))));
     wmax = wave_max(m);
   }
   float acc = 0.0f;
   for (int b = threadIdx.x; b < B; b += 64) {
-    const float w = probs ? __fdiv_rn(__fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(probs[b], 1e-10f))), wmax) : 1.0f;
+    const float w = probs ? __fdiv_rn(__fdiv_rn(1.0f, sqrt_rn(__fadd_rn(probs[b], 1e-10f))), wmax) : 1.0f;
     acc = __fadd_rn(acc, __fmul_rn(w, loss[b]));
   }
   acc = wave_sum(acc);
@@ -451,6 +498,7 @@ struct DqnFusedArgs {
 };
 
 __global__ __launch_bounds__(128) void k_dqn_fused(DqnFusedArgs a) {
+  warm_kernargs<sizeof(DqnFusedArgs)>();
   const int b = blockIdx.x, t = threadIdx.x, A = a.A, H = a.H;
   const int ab = a.act[b];
   // the d h operands first: they depend on the action only, not on the loss chain
@@ -682,9 +730,11 @@ int dq_c51_loss(const float* online_logits, const float* target_logits, const in
   DQ_CHECK_ARG(!mean_loss_out || loss_out, "mean_loss_out needs loss_out");
   DQ_CHECK_ARG(num_actions <= 64, "num_actions must be <= 64");
   const int waves = num_actions < 16 ? num_actions : 16;
-  const size_t shm = c51_lds(num_actions, num_atoms, 0);
-  hipLaunchKernelGGL(k_c51<LogitsDirect>, dim3(batch), dim3(64 * waves), shm, (hipStream_t)stream,
-                     a, LogitsDirect{online_logits}, LogitsDirect{target_logits}, C51Extra{});
+  const size_t shm = c51_lds(num_actions, num_atoms, 0, waves);
+  auto kern = probs ? k_c51<LogitsDirect, kC51Probs> : k_c51<LogitsDirect, 0>;
+  hipLaunchKernelGGL(kern, dim3(batch), dim3(64 * waves), shm, (hipStream_t)stream,
+                     a, LogitsDirect{online_logits, num_actions * num_atoms},
+                     LogitsDirect{target_logits, num_actions * num_atoms}, C51Extra{});
   DQ_CHECK_LAUNCH("k_c51");
   if (mean_loss_out) {
     hipLaunchKernelGGL(k_wmean, dim3(1), dim3(64), 0, (hipStream_t)stream, loss_out, probs, batch,
@@ -715,8 +765,15 @@ int dq_c51_loss_fused(const float* online_parts, const float* online_bias,
   const int64_t stride = (int64_t)batch * NO;
   DQ_CHECK_ARG(num_actions <= 64, "num_actions must be <= 64");
   const int waves = num_actions < 16 ? num_actions : 16;
-  const size_t shm = c51_lds(num_actions, num_atoms, fc2_w ? hidden : 0);
-  hipLaunchKernelGGL(k_c51<LogitsParts>, dim3(batch), dim3(64 * waves), shm, (hipStream_t)stream,
+  // d h split over S blocks per sample when the column slices stay whole 16-B chunks
+  const int S = fc2_w && hidden % (4 * DQ_C51_SPLIT) == 0 ? DQ_C51_SPLIT : 1;
+  const size_t shm = c51_lds(num_actions, num_atoms, fc2_w ? hidden / S : 0, waves);
+  static void (*const kerns[8])(C51Args, LogitsParts, LogitsParts, C51Extra) = {
+      k_c51<LogitsParts, 0>, k_c51<LogitsParts, 1>, k_c51<LogitsParts, 2>, k_c51<LogitsParts, 3>,
+      k_c51<LogitsParts, 4>, k_c51<LogitsParts, 5>, k_c51<LogitsParts, 6>, k_c51<LogitsParts, 7>};
+  const int f = (probs ? kC51Probs : 0) | (fc2_w ? kC51W2 : 0) |
+                (online_logits_out || target_logits_out ? kC51LogitsOut : 0);
+  hipLaunchKernelGGL(kerns[f], dim3(batch * S), dim3(64 * waves), shm, (hipStream_t)stream,
                      a, LogitsParts{online_parts, online_bias, stride, n_parts, NO},
                      LogitsParts{target_parts, target_bias, stride, n_parts, NO},
                      C51Extra{online_logits_out, target_logits_out, fc2_w, h, dh, hidden});

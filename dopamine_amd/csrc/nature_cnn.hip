@@ -387,6 +387,7 @@ constexpr int group_wpe() {
 template <int T, class... Ops>
 __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(group_wpe<Ops...>())))
 void k_grouped(GroupArgs<Ops...> g, Ops... ops) {
+  warm_kernargs<sizeof(GroupArgs<Ops...>) + (sizeof(Ops) + ...) + 8 * sizeof...(Ops)>();
   __shared__ __attribute__((aligned(16))) float smem[max_lds<Ops...>()];
   int blk = blockIdx.x, i = 0;
   ((dispatch(ops, g.nblocks[i++], blk, smem)) || ...);

@@ -49,11 +49,13 @@ namespace dq {
 constexpr int kTreeT = 1024;   // block of the block-parallel sum-tree kernels
 
 __global__ __launch_bounds__(kTreeT) void k_per_sample(ReplayView v, int B, int32_t* out) {
+  warm_kernargs<sizeof(ReplayView) + 16>();
   __shared__ __attribute__((aligned(16))) uint8_t lds[kPerSampleParLds];
   per_sample_par<kTreeT>(v, B, out, lds);
 }
 
 __global__ __launch_bounds__(64) void k_uniform_sample(ReplayView v, int B, int32_t* out, int G) {
+  warm_kernargs<sizeof(ReplayView) + 24>();
   if (G > 1)
     uniform_sample_groups(v, B, out, G);
   else
@@ -158,6 +160,7 @@ __global__ void k_egreedy(dq_replay_meta* meta, const uint32_t* tape, const floa
 constexpr int kGatherR = 4;
 
 __global__ __launch_bounds__(256) void k_gather_f32(ReplayView v, GatherOut g) {
+  warm_kernargs<sizeof(ReplayView) + sizeof(GatherOut)>();
   const int S = v.S;
   const int slot = blockIdx.y;
   const int b = slot / (2 * S);
@@ -191,6 +194,7 @@ __global__ __launch_bounds__(256) void k_gather_f32(ReplayView v, GatherOut g) {
 // the scalar chain.
 template <int R>
 __global__ __launch_bounds__(256) void k_gather_nhwc4(ReplayView v, GatherOut g) {
+  warm_kernargs<sizeof(ReplayView) + sizeof(GatherOut)>();
   const int slot = blockIdx.y;
   if (blockIdx.x == gridDim.x - 1) {
     if ((slot & 1) == 0 && threadIdx.x < kWave)
@@ -330,6 +334,7 @@ __global__ __launch_bounds__(256) void k_gather_raw(ReplayView v, GatherOut g) {
 }
 
 __global__ __launch_bounds__(kTreeT) void k_sumtree_set(ReplayView v, SetArgs a) {
+  warm_kernargs<sizeof(ReplayView) + sizeof(SetArgs)>();
   __shared__ __attribute__((aligned(16))) uint8_t lds[kSumtreeParLds];
   sumtree_set_par<kTreeT>(v, a, lds);
 }

@@ -13,7 +13,9 @@ from dopamine_amd import _build  # noqa: E402
 
 
 def main():
-  name, tus, extra = sys.argv[1], sys.argv[2].split(','), sys.argv[3:]
+  name, extra = sys.argv[1], sys.argv[3:]
+  # "tu" recompiles the in-tree source, "tu=path" another file in its place (e.g. a git show)
+  tus = dict((t.split('=') + [None])[:2] for t in sys.argv[2].split(','))
   out_dir = os.path.join(ROOT, 'ab', name)
   os.makedirs(out_dir, exist_ok=True)
   bdir = os.path.join(ROOT, 'dopamine_amd', 'build')
@@ -24,7 +26,7 @@ def main():
     tu = os.path.splitext(os.path.basename(src))[0]
     if tu in tus:
       obj = os.path.join(out_dir, tu + '.o')
-      cmd = ['hipcc'] + flags + ['-c', '-o', obj, src]
+      cmd = ['hipcc'] + flags + ['-c', '-o', obj, tus[tu] or src]
       procs.append(subprocess.Popen(cmd))
     else:
       obj = os.path.join(bdir, 'libdopamine_amd.so.%s.o' % tu)

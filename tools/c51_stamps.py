@@ -15,6 +15,9 @@ from dopamine_amd.agents.networks import RainbowNetwork  # noqa: E402
 from dopamine_amd.cnn import HipNatureCNN, forward_fused  # noqa: E402
 
 
+SPLIT = int(os.environ.get('DQ_C51_SPLIT', '4'))   # blocks per sample of the build
+
+
 def main():
   B, A, N = 32, 9, 51
   on, tg = RainbowNetwork(A, device='cuda', seed=1), RainbowNetwork(A, device='cuda', seed=2)
@@ -31,7 +34,7 @@ def main():
   buf = np.zeros((256, 8), np.int64)
   wfn = _lib.lib.dq_debug_c51_wave_times
   wfn.argtypes = [ctypes.c_void_p]
-  wbuf = np.zeros((2, 256, 16), np.int64)
+  wbuf = np.zeros((3, 256, 16), np.int64)
   rows, wrows = [], []
   for it in range(30):
     forward_fused(ho, x, ht)
@@ -39,16 +42,23 @@ def main():
     torch.cuda.synchronize()
     assert fn(buf.ctypes.data) == 0
     if it >= 10:
-      t = buf[:B, :7].astype(np.float64)
+      t = buf[:B * SPLIT, :7].astype(np.float64)
       t = (t - t[:, 0].min()) / 100.0
       rows.append(t)
       assert wfn(wbuf.ctypes.data) == 0
-      wrows.append((wbuf[:, :B, :A].astype(np.float64) - buf[:B, 0].min()) / 100.0)
+      wrows.append((wbuf[:, :B * SPLIT, :A].astype(np.float64) - buf[:B * SPLIT, 0].min()) / 100.0)
   r = np.median(np.stack(rows), axis=0)       # (B, 7) median over iterations
   print('stage   median-over-blocks   max-over-blocks (us from first block start)')
   for k in range(7):
     print('%d  %8.2f  %8.2f' % (k, np.median(r[:, k]), r[:, k].max()))
+  d = r[:, 4] - r[:, 3]
+  tm = np.repeat(term.cpu().numpy(), SPLIT)
+  order = np.argsort(d)
+  print('stage 3->4 per block (us, terminal):', ' '.join('%.2f%s' % (d[i], '*' if tm[i] else '') for i in order))
+  d = r[:, 6] - r[:, 5]
+  print('stage 5->6 per block (us, terminal):', ' '.join('%.2f%s' % (d[i], '*' if tm[i] else '') for i in np.argsort(d)))
   w = np.median(np.stack(wrows), axis=0)
+  print('inputs in per wave  :', ' '.join('%.2f' % v for v in np.median(w[2], axis=0)))
   print('c(i,j) done per wave:', ' '.join('%.2f' % v for v in np.median(w[1], axis=0)))
   print('stage 1 per wave    :', ' '.join('%.2f' % v for v in np.median(w[0], axis=0)))
 
