@@ -1,9 +1,12 @@
-// The exact-fp32 matrix-core tile engine shared by the Nature-CNN (nature_cnn.hip)
-// and the IQN quantile heads (iqn.hip): loaders producing 16-byte operand groups,
-// epilogues, the templated tile kernel igemm_block (v_mfma_f32_32x32x2_f32), the
-// ordered split-K sum and the host-side launch context.  See nature_cnn.hip's header
-// for the design.
+// The fp32 matrix-core tile engine shared by the Nature-CNN (nature_cnn.hip) and the
+// IQN quantile heads (iqn.hip): loaders producing 16-byte operand groups, epilogues,
+// the templated tile kernel igemm_block in two forms -- exact f32
+// (v_mfma_f32_32x32x2_f32) and split-bf16 "x6" (fp32 to rounding on
+// v_mfma_f32_32x32x16_bf16, X6Img below) -- the ordered split-K sum and the host-side
+// launch context.  See nature_cnn.hip's header for the design.
 #pragma once
+#include <type_traits>
+
 #include "common.h"
 #include "replay_dev.h"
 
@@ -611,10 +614,170 @@ struct Tile {
   }
 };
 
+// ---------------------------------------------- split-bf16 ("x6") matrix-core form
+// fp32 operands as exact sums of three bf16 pieces, a = hi + mid + lo (round to
+// nearest at each stage: a - hi and (a - hi) - mid are exact in fp32, and the last
+// remainder has <= 8 significant bits, so lo holds it exactly), multiplied by
+// v_mfma_f32_32x32x16_bf16 (bf16 x bf16 products are exact in fp32, fp32
+// accumulate) over the six piece pairs whose weight reaches 2^-16:
+//   hi.hi + hi.mid + mid.hi + hi.lo + mid.mid + lo.hi.
+// The three dropped pairs are below 2^-25 |a b| (each piece is at most 2^-9 of the
+// one above), under fp32's own rounding of the product, so the result is an fp32
+// GEMM to rounding -- not a bf16 one -- at 6 x 32 cycles per 32x32x16 step instead
+// of 8 x 64 for v_mfma_f32_32x32x2_f32 (2.7x the f32 matrix rate).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+// two fp32 -> their hi / mid / lo bf16 pieces, each pair packed (element 0 low)
+__device__ __forceinline__ void split_x3(float a, float b, unsigned& h, unsigned& m, unsigned& l) {
+  const unsigned hu = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2v){a, b}, bf16x2v));
+  const float ra = a - __uint_as_float(hu << 16), rb = b - __uint_as_float(hu & 0xffff0000u);
+  const unsigned mu = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2v){ra, rb}, bf16x2v));
+  const float sa = ra - __uint_as_float(mu << 16), sb = rb - __uint_as_float(mu & 0xffff0000u);
+  h = hu;
+  m = mu;
+  l = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2v){sa, sb}, bf16x2v));
+}
+
+// eight fp32 operands of one lane (k = 8h + j of its row) -> the three bf16x8 pieces
+__device__ __forceinline__ void split_x3_8(const float* v, bf16x8& h, bf16x8& m, bf16x8& l) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 hu, mu, lu;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    unsigned a, b, c;
+    split_x3(v[2 * i], v[2 * i + 1], a, b, c);
+    hu[i] = a;
+    mu[i] = b;
+    lu[i] = c;
+  }
+  h = __builtin_bit_cast(bf16x8, hu);
+  m = __builtin_bit_cast(bf16x8, mu);
+  l = __builtin_bit_cast(bf16x8, lu);
+}
+// acc += A B over one 16-k step from the pieces, smallest pairs first
+__device__ __forceinline__ f32x16 mfma_x6(const bf16x8& ah, const bf16x8& am, const bf16x8& al,
+                                          const bf16x8& bh, const bf16x8& bm, const bf16x8& bl,
+                                          f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+}
+// the same with the five correction pairs in their own accumulator (its magnitude
+// ~2^-8 of the main one), the two added once at the end of the K loop
+__device__ __forceinline__ void mfma_x6_2(const bf16x8& ah, const bf16x8& am, const bf16x8& al,
+                                          const bf16x8& bh, const bf16x8& bm, const bf16x8& bl,
+                                          f32x16& acc, f32x16& cor) {
+  cor = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, cor, 0, 0, 0);
+  cor = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, cor, 0, 0, 0);
+  cor = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, cor, 0, 0, 0);
+  cor = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, cor, 0, 0, 0);
+  cor = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, cor, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+}
+#ifndef DQ_X6_COR
+#define DQ_X6_COR 0
+#endif
+
+// The x6 staging image of one operand slice: 3 planes (hi, mid, lo) of [rows][BKT]
+// bf16, 16-byte k chunks XOR-swizzled by row so a 32x32x16 operand read (row r, 8
+// consecutive k) is one ds_read_b128 and 8 consecutive rows hit distinct banks.
+template <int ROWS, int BKT>
+struct X6Img {
+  static constexpr int RB = 2 * BKT;               // bytes per row per plane
+  static constexpr int PLANE = ROWS * RB;          // bytes per plane
+  static constexpr int BYTES = 3 * PLANE;
+  __device__ static __forceinline__ int off(int row, int k) {   // byte offset of element (row, k)
+    return row * RB + 16 * ((k >> 3) ^ ((row >> 2) & 3)) + 2 * (k & 7);
+  }
+  // the 16-byte group of a loader (4 consecutive k of row rr when kFast, else 4
+  // consecutive rows at k) split and written into the three planes
+  __device__ static __forceinline__ void put(char* img, bool kfast, int rr, int kk, float4 v) {
+    unsigned h0, m0, l0, h1, m1, l1;
+    split_x3(v.x, v.y, h0, m0, l0);
+    split_x3(v.z, v.w, h1, m1, l1);
+    if (kfast) {                                   // kk % 4 == 0: one 8-byte write per plane
+      char* p = img + off(rr, kk);
+      *reinterpret_cast<uint2*>(p) = make_uint2(h0, h1);
+      *reinterpret_cast<uint2*>(p + PLANE) = make_uint2(m0, m1);
+      *reinterpret_cast<uint2*>(p + 2 * PLANE) = make_uint2(l0, l1);
+    } else {                                       // rr % 4 == 0: one swizzle for the 4 rows
+      const unsigned hs[4] = {h0 & 0xffffu, h0 >> 16, h1 & 0xffffu, h1 >> 16};
+      const unsigned ms[4] = {m0 & 0xffffu, m0 >> 16, m1 & 0xffffu, m1 >> 16};
+      const unsigned ls[4] = {l0 & 0xffffu, l0 >> 16, l1 & 0xffffu, l1 >> 16};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        char* p = img + off(rr + i, kk);
+        *reinterpret_cast<unsigned short*>(p) = (unsigned short)hs[i];
+        *reinterpret_cast<unsigned short*>(p + PLANE) = (unsigned short)ms[i];
+        *reinterpret_cast<unsigned short*>(p + 2 * PLANE) = (unsigned short)ls[i];
+      }
+    }
+  }
+  // the 32x32x16 operand of rows base.. base+31, k = kb .. kb+15: lane (r, h) gets row
+  // base + r, k = kb + 8h + j in element j -- one ds_read_b128 per plane
+  __device__ static __forceinline__ void get(const char* img, int base, int kb, int lane, bf16x8& h,
+                                             bf16x8& m, bf16x8& l) {
+    const char* p = img + off(base + (lane & 31), kb + 8 * (lane >> 5));
+    h = *reinterpret_cast<const bf16x8*>(p);
+    m = *reinterpret_cast<const bf16x8*>(p + PLANE);
+    l = *reinterpret_cast<const bf16x8*>(p + 2 * PLANE);
+  }
+};
+
+// The x6 image of a row-contiguous operand (loader groups = 4 consecutive rows at one
+// k): planes [k][rows] bf16, so each group lands as one 8-byte write per plane, and
+// the k-contiguous MFMA operand comes back through gfx950's transposing LDS read
+// (ds_read_b64_tr_b16: per 16-lane group, lane 4q + p addresses image row q, columns
+// 4p .. 4p+3 of a 4 x 16 block and lane i receives column i, row q in element q).
+// Row stride 2*ROWS (+ 64 B when that is a multiple of 128) puts the four image rows
+// of a read in distinct 64-B bank windows: the 32 lanes of a half read 256 distinct
+// bytes, conflict-free.
+typedef short s16x4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4v lds_s16x4v;
+template <int ROWS, int BKT>
+struct X6ImgT {
+  static constexpr int RS = 2 * ROWS + ((2 * ROWS) % 128 == 0 ? 64 : 0);   // bytes per k row
+  static constexpr int PLANE = BKT * RS;
+  static constexpr int BYTES = 3 * PLANE;
+  __device__ static __forceinline__ int off(int row, int k) { return k * RS + 2 * row; }
+  __device__ static __forceinline__ void put(char* img, bool, int rr, int kk, float4 v) {
+    unsigned h0, m0, l0, h1, m1, l1;
+    split_x3(v.x, v.y, h0, m0, l0);
+    split_x3(v.z, v.w, h1, m1, l1);
+    char* p = img + off(rr, kk);                   // rr % 4 == 0: 8-byte aligned
+    *reinterpret_cast<uint2*>(p) = make_uint2(h0, h1);
+    *reinterpret_cast<uint2*>(p + PLANE) = make_uint2(m0, m1);
+    *reinterpret_cast<uint2*>(p + 2 * PLANE) = make_uint2(l0, l1);
+  }
+  __device__ static __forceinline__ bf16x8 tr8(const char* p) {   // k = q and 4 + q
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const s16x4v a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4v*)(p));
+    const s16x4v b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4v*)(p + 4 * RS));
+    const s16x8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+  // same operand map as X6Img::get (EXEC must be all ones: the read gathers across lanes)
+  __device__ static __forceinline__ void get(const char* img, int base, int kb, int lane, bf16x8& h,
+                                             bf16x8& m, bf16x8& l) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3;
+    const char* p = img + off(base + 16 * (g & 1) + 4 * p4, kb + 8 * (g >> 1) + q);
+    h = tr8(p);
+    m = tr8(p + PLANE);
+    l = tr8(p + 2 * PLANE);
+  }
+};
+template <bool kFast, int ROWS, int BKT>
+using X6Of = typename std::conditional<kFast, X6Img<ROWS, BKT>, X6ImgT<ROWS, BKT>>::type;
+
 // kLate: issue each half-band fetch after the previous half's MFMAs (<= 64 VGPRs,
 // for launches with several rounds of blocks, two 16-wave blocks per CU); else
 // while they run (one more fetch in flight, for single-round launches).
-template <int WM, int WN, int WK, class AL, class BL, class EP, bool kLate = true>
+// kX6: the split-bf16 matrix-core form (block-shared staging only).
+template <int WM, int WN, int WK, class AL, class BL, class EP, bool kLate = true, bool kX6 = false>
 __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& E, int M, int N,
                                             int K, int kchunk, int bx, int by, int bz,
                                             float* smem) {
@@ -698,7 +861,55 @@ __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& 
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-  if constexpr (TL::kPrivate) {
+  if constexpr (kX6 && !TL::kPrivate) {
+    // Block-shared staging as below, the slice split into bf16 pieces as it is
+    // written to LDS (each element once, whichever waves read it), then per 16-k
+    // step six 32x32x16 bf16 MFMAs, smallest pairs first.
+    using IA = X6Of<AL::kFast, BM, BKT>;
+    using IB = X6Of<BL::kFast, BN, BKT>;
+    char* ia = reinterpret_cast<char*>(smem);
+    char* ib = ia + IA::BYTES;
+#if DQ_X6_COR
+    f32x16 cor;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) cor[i] = 0.0f;
+#endif
+    load(kbeg);
+    for (int k0 = kbeg; k0 < kend; k0 += BKT) {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        int rr, kk;
+        group_coord<AL::kFast, BM, BKT>(i * T + tid, rr, kk);
+        IA::put(ia, AL::kFast, rr, kk, ra[i]);
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        int rr, kk;
+        group_coord<BL::kFast, BN, BKT>(i * T + tid, rr, kk);
+        IB::put(ib, BL::kFast, rr, kk, rb[i]);
+      }
+      __syncthreads();
+      if (k0 + BKT < kend) load(k0 + BKT);
+      if (k0 + wk * 32 < kend) {              // wave-uniform: bands past the end are all zero
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          bf16x8 ah, am, al, bh, bm, bl;
+          IA::get(ia, wm * 32, wk * 32 + 16 * s, lane, ah, am, al);
+          IB::get(ib, wn * 32, wk * 32 + 16 * s, lane, bh, bm, bl);
+#if DQ_X6_COR
+          mfma_x6_2(ah, am, al, bh, bm, bl, acc, cor);
+#else
+          acc = mfma_x6(ah, am, al, bh, bm, bl, acc);
+#endif
+        }
+      }
+      __syncthreads();
+    }
+#if DQ_X6_COR
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = __fadd_rn(acc[i], cor[i]);
+#endif
+  } else if constexpr (TL::kPrivate) {
     // Wave-private staging: wave wk fetches its own 32-wide k band (the same
     // coalesced 128-byte row segments as the shared layout) and transposes it
     // through its own LDS window, 16 k at a time -- no block barrier until the
@@ -783,9 +994,18 @@ __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& 
 #ifdef DQ_ABLATE_MFMA    // timing experiments only: no matrix-core chain
           for (int s = 0; s < 8; ++s) acc[s] += av[s] * bv[s];
 #else
+          if constexpr (kX6) {
+            // each staged element is this lane's alone (one 32 x 32 tile per wave):
+            // split as read, one 16-k step of six bf16 MFMAs for the half
+            bf16x8 ah, am, al, bh, bm, bl;
+            split_x3_8(av, ah, am, al);
+            split_x3_8(bv, bh, bm, bl);
+            acc = mfma_x6(ah, am, al, bh, bm, bl, acc);
+          } else {
 #pragma unroll
-          for (int s = 0; s < 8; ++s)
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc, 0, 0, 0);
+            for (int s = 0; s < 8; ++s)
+              acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc, 0, 0, 0);
+          }
 #endif
         }
         if constexpr (kLate) {
@@ -909,10 +1129,16 @@ __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& 
   }
 }
 
-template <int WM, int WN, int WK, class AL, class BL, class EP>
+template <int WM, int WN, int WK, class AL, class BL, class EP, bool kX6 = false>
 __global__ __launch_bounds__(64 * WM * WN * WK) void k_igemm(AL A, BL B, EP E, int M, int N, int K,
                                                              int kchunk) {
-  constexpr int kTile = Tile<WM, WN, WK>::template lds<AL, BL>();
+  constexpr int kTile0 = Tile<WM, WN, WK>::template lds<AL, BL>();
+  // the block-shared x6 planes, floats (the wave-private form splits as it reads)
+  constexpr int kX6Img = kX6 && !Tile<WM, WN, WK>::kPrivate
+                             ? (X6Of<AL::kFast, 32 * WM, 32 * WK>::BYTES +
+                                X6Of<BL::kFast, 32 * WN, 32 * WK>::BYTES) / 4
+                             : 0;
+  constexpr int kTile = kTile0 > kX6Img ? kTile0 : kX6Img;
   constexpr int kVecW = HasVec<EP>::value ? WM * WN * WK * 32 * 33 : 0;   // vector epilogue windows
   // block epilogue tile (+ EP::kBlockExtra floats of scratch after it)
   constexpr int kBlkW = HasBlock<EP>::value ? 32 * WM * (32 * WN + 1) + BlockExtra<EP>::value : 0;
@@ -938,9 +1164,10 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_igemm(AL A, BL B, EP E, i
   const unsigned w = (g < r ? g * (q + 1) : r * (q + 1) + (g - r) * q) + orig / 8;
   const unsigned z = w / (nx * ny), xy = w - z * nx * ny;
   const unsigned bx = nx <= ny ? xy % nx : xy / ny, by = nx <= ny ? xy / nx : xy % ny;
-  igemm_block<WM, WN, WK>(A, B, E, M, N, K, kchunk, bx, by, z, smem);
+  igemm_block<WM, WN, WK, AL, BL, EP, true, kX6>(A, B, E, M, N, K, kchunk, bx, by, z, smem);
 #else
-  igemm_block<WM, WN, WK>(A, B, E, M, N, K, kchunk, blockIdx.x, blockIdx.y, blockIdx.z, smem);
+  igemm_block<WM, WN, WK, AL, BL, EP, true, kX6>(A, B, E, M, N, K, kchunk, blockIdx.x, blockIdx.y,
+                                                blockIdx.z, smem);
 #endif
 }
 
@@ -1017,8 +1244,8 @@ inline int split_chunk(int K, int splits, int bkt) {
   return ((K + splits - 1) / splits + bkt - 1) / bkt * bkt;
 }
 
-template <int WM, int WN, int WK, class AL, class BL, class EP>
-void gemm(Ctx& c, AL a, BL b, EP e, int M, int N, int K, int splits = 1) {
+template <int WM, int WN, int WK, bool kX6, class AL, class BL, class EP>
+void gemm_form(Ctx& c, AL a, BL b, EP e, int M, int N, int K, int splits) {
   constexpr int BKT = 32 * WK, T = 64 * WM * WN * WK;
   const unsigned gx = (M + 32 * WM - 1) / (32 * WM), gy = (N + 32 * WN - 1) / (32 * WN);
   const int kchunk = splits > 1 ? split_chunk(K, splits, BKT) : K;
@@ -1029,12 +1256,12 @@ void gemm(Ctx& c, AL a, BL b, EP e, int M, int N, int K, int splits = 1) {
   }
   if (c.dry) return;
   if (nz == 1) {
-    hipLaunchKernelGGL((k_igemm<WM, WN, WK, AL, BL, EP>), dim3(gx, gy, 1), dim3(T), 0, c.s, a, b, e,
-                       M, N, K, K);
+    hipLaunchKernelGGL((k_igemm<WM, WN, WK, AL, BL, EP, kX6>), dim3(gx, gy, 1), dim3(T), 0, c.s, a, b,
+                       e, M, N, K, K);
     return;
   }
-  hipLaunchKernelGGL((k_igemm<WM, WN, WK, AL, BL, EpiPartial>), dim3(gx, gy, nz), dim3(T), 0, c.s, a,
-                     b, EpiPartial{c.ws, M, N}, M, N, K, kchunk);
+  hipLaunchKernelGGL((k_igemm<WM, WN, WK, AL, BL, EpiPartial, kX6>), dim3(gx, gy, nz), dim3(T), 0, c.s,
+                     a, b, EpiPartial{c.ws, M, N}, M, N, K, kchunk);
   const int64_t total = (int64_t)M * N;
   if (total % 4 == 0)
     hipLaunchKernelGGL((k_splitk_reduce4<EP>), dim3((unsigned)((total / 4 + 255) / 256)), dim3(256),
@@ -1042,6 +1269,25 @@ void gemm(Ctx& c, AL a, BL b, EP e, int M, int N, int K, int splits = 1) {
   else
     hipLaunchKernelGGL((k_splitk_reduce<EP>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
                        c.s, c.ws, nz, M, N, e);
+}
+
+// The Nature-CNN's form: exact-fp32 MFMA (v_mfma_f32_32x32x2_f32); -DDQ_CNN_X6=1 builds
+// the wave-private tiles (one 32 x 32 tile per wave, split as read) on the split-bf16
+// form for A/B runs.  One rule for gemm() and the grouped launches' GemmOp, so the
+// per-layer and grouped schedules stay bitwise equal.
+#ifndef DQ_CNN_X6
+#define DQ_CNN_X6 0
+#endif
+template <int WM, int WN, int WK>
+constexpr bool cnn_x6() { return DQ_CNN_X6 && Tile<WM, WN, WK>::kPrivate; }
+template <int WM, int WN, int WK, class AL, class BL, class EP>
+void gemm(Ctx& c, AL a, BL b, EP e, int M, int N, int K, int splits = 1) {
+  gemm_form<WM, WN, WK, cnn_x6<WM, WN, WK>()>(c, a, b, e, M, N, K, splits);
+}
+// split-bf16 MFMA (X6Img): fp32 to rounding at 2.7x the f32 matrix rate
+template <int WM, int WN, int WK, class AL, class BL, class EP>
+void gemm_x6(Ctx& c, AL a, BL b, EP e, int M, int N, int K, int splits = 1) {
+  gemm_form<WM, WN, WK, true>(c, a, b, e, M, N, K, splits);
 }
 
 

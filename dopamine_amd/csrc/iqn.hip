@@ -1,6 +1,6 @@
 // The implicit-quantile head of ImplicitQuantileNetwork (atari_lib.py:147-199) and its
-// backward, on the exact-fp32 matrix cores (v_mfma_f32_32x32x2_f32) through the tile
-// engine of cnn_tile.h.  The Nature-CNN torso runs on nature_cnn.hip
+// backward, on the matrix cores through the tile engine of cnn_tile.h (the big GEMMs on
+// its split-bf16 form, fp32 to rounding; the rest on v_mfma_f32_32x32x2_f32).  The Nature-CNN torso runs on nature_cnn.hip
 // (dq_cnn_forward_torso / dq_cnn_backward_torso); this file owns everything after
 // the 7744-wide state vector.
 //
@@ -37,6 +37,28 @@ constexpr int kSplitFc1 = 4;
 constexpr int kSplitW1 = 2;       // dW1: K = R (1 / 4 measured equal, profiles/r2_s5_iqn_dw1_split_ab.log)
 constexpr int kSplitWe = 8;       // dWe: K = R, 61 row tiles
 constexpr int kSplitW2 = 32;      // dW2: M = A, K = R
+
+// The 7744-wide GEMMs on the split-bf16 matrix-core form (cnn_tile.h X6Img / X6ImgT:
+// fp32 operands as exact hi + mid + lo bf16 sums, the six pairs above fp32 rounding,
+// v_mfma_f32_32x32x16_bf16): the embedding, both FC1 forwards, dW1 and dWe.  dX stays
+// on the exact-f32 form: its d state feeds the torso's weight gradients, sums over every
+// pixel that cancel to ~1/100 of their terms, and the single-accumulator split form
+// moved them from 5e-7 to 1.3e-5 of scale against float64 at B = 64, N = 64 (a bias
+// from the small correction products rounding into the large accumulator; with the
+// corrections in their own accumulator, DQ_X6_COR, they fall to 5e-7 but the 16 extra
+// registers cost the second 16-wave block per CU, config 5 727 vs 751 steps/s), and x6
+// bought dX no time in the two-stream step (734 with vs 751 without).
+// Measured (config 5, same box): exact f32 616, this 751 steps/s (profiles/r3_s3_x6/).
+//   -DDQ_IQN_X6=0: every GEMM exact f32; 2: dX on the split form too (A/B runs).
+#ifndef DQ_IQN_X6
+#define DQ_IQN_X6 1
+#endif
+constexpr bool kIqnX6 = DQ_IQN_X6 != 0;
+constexpr bool kDxX6 = DQ_IQN_X6 == 2;
+template <int WM, int WN, int WK, class AL, class BL, class EP>
+void gemm_iqn(Ctx& c, AL a, BL b, EP e, int M, int N, int K, int splits = 1) {
+  gemm_form<WM, WN, WK, kIqnX6>(c, a, b, e, M, N, K, splits);
+}
 
 __device__ __forceinline__ float uniform_of(uint64_t seed, int64_t call, int64_t i) {
   // a splitmix64 hash of (seed, call, i), 24 random bits -> k * 2^-24
@@ -273,13 +295,13 @@ void forward(Ctx& c, const dq_iqn_head* hp, int B, int nq, const float* state, c
     hipLaunchKernelGGL(k_cos_embedding, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c.s, tau,
                        n, E, a->cos);
   }
-  gemm<4, 4, 1>(c, RowK{a->cos, E}, RowK{hp->emb_w, E}, EpiEmb{a->emb, a->x, hp->emb_b, state, B},
+  gemm_iqn<4, 4, 1>(c, RowK{a->cos, E}, RowK{hp->emb_w, E}, EpiEmb{a->emb, a->x, hp->emb_b, state, B},
                 R, F, E);
   if (a->x)
-    gemm<4, 4, 1>(c, RowK{a->x, F}, RowK{hp->fc1_w, F}, EpiBiasAct{a->h, hp->fc1_b, H, true}, R, H,
+    gemm_iqn<4, 4, 1>(c, RowK{a->x, F}, RowK{hp->fc1_w, F}, EpiBiasAct{a->h, hp->fc1_b, H, true}, R, H,
                   F, kSplitFc1);
   else                               // x formed from emb and state by the loader
-    gemm<4, 4, 1>(c, RowKHad{a->emb, state, B}, RowK{hp->fc1_w, F},
+    gemm_iqn<4, 4, 1>(c, RowKHad{a->emb, state, B}, RowK{hp->fc1_w, F},
                   EpiBiasAct{a->h, hp->fc1_b, H, true}, R, H, F, kSplitFc1);
   gemm<1, 1, 16>(c, RowK{a->h, H}, RowK{hp->fc2_w, H}, EpiBiasAct{a->q, hp->fc2_b, A, false}, R,
                  A, H);
@@ -298,28 +320,28 @@ void backward(Ctx& c, const dq_iqn_head* hp, const dq_iqn_head* hg, int B, int n
   const bool we_narrow = fuse_tile;
   if (fuse_tile) {
     if (!c.dry)
-      hipLaunchKernelGGL((k_igemm<4, 4, 1, RowKQ, ColK, EpiDxQ>), dim3((R + 127) / 128, (F + 127) / 128),
+      hipLaunchKernelGGL((k_igemm<4, 4, 1, RowKQ, ColK, EpiDxQ, kDxX6>), dim3((R + 127) / 128, (F + 127) / 128),
                          dim3(1024), 0, c.s, RowKQ{d->dh, H, B, nq}, ColK{hp->fc1_w, F},
                          EpiDxQ{d->dpre, dstate, we_narrow ? d->dtl : nullptr, a->emb, state, B, nq},
                          R, F, H, H);
   } else {
-    gemm<4, 4, 1>(c, RowK{d->dh, H}, ColK{hp->fc1_w, F}, EpiDx{d->dtl, d->dpre, a->emb, state, B},
-                  R, F, H);
+    gemm_form<4, 4, 1, kDxX6>(c, RowK{d->dh, H}, ColK{hp->fc1_w, F},
+                              EpiDx{d->dtl, d->dpre, a->emb, state, B}, R, F, H, 1);
   }
   if (a->x)
-    gemm<4, 4, 1>(c, ColK{d->dh, H}, ColKOnes{a->x, F}, EpiGrad{hg->fc1_w, hg->fc1_b, F}, H,
+    gemm_iqn<4, 4, 1>(c, ColK{d->dh, H}, ColKOnes{a->x, F}, EpiGrad{hg->fc1_w, hg->fc1_b, F}, H,
                   F + 1, R, kSplitW1);
   else
-    gemm<4, 4, 1>(c, ColK{d->dh, H}, ColKOnesHad{a->emb, state, B},
+    gemm_iqn<4, 4, 1>(c, ColK{d->dh, H}, ColKOnesHad{a->emb, state, B},
                   EpiGrad{hg->fc1_w, hg->fc1_b, F}, H, F + 1, R, kSplitW1);
   if (we_narrow) {           // dWe over the E cosine columns, dbe from the row-tile partials
-    gemm<4, 2, 2>(c, ColK{d->dpre, F}, ColK{a->cos, E}, EpiGrad{hg->emb_w, hg->emb_b, E}, F, E, R,
+    gemm_iqn<4, 2, 2>(c, ColK{d->dpre, F}, ColK{a->cos, E}, EpiGrad{hg->emb_w, hg->emb_b, E}, F, E, R,
                   kSplitWe);
     if (!c.dry)
       hipLaunchKernelGGL(k_colsum, dim3((F + 255) / 256), dim3(256), 0, c.s, d->dtl, (R + 127) / 128, F,
                          hg->emb_b);
   } else                     // 128 x 128 tiles over [cos | 1]
-    gemm<4, 4, 1>(c, ColK{d->dpre, F}, ColKOnes{a->cos, E}, EpiGrad{hg->emb_w, hg->emb_b, E}, F,
+    gemm_iqn<4, 4, 1>(c, ColK{d->dpre, F}, ColKOnes{a->cos, E}, EpiGrad{hg->emb_w, hg->emb_b, E}, F,
                   E + 1, R, kSplitWe);
   if (!c.dry && !fuse_tile) {
     const int64_t n = (int64_t)B * F;
