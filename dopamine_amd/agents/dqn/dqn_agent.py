@@ -965,6 +965,8 @@ class DQNAgent(object):
     same graph, with N GPUs it is a second graph after the RCCL all-reduce."""
     pipe = self.pipeline if pipe is None else pipe
     torch.cuda.synchronize(self._device)
+    if self._pg is not None and self._rccl is None:
+      parallel.settle_watchdog()
     graphs, graphs_opt, pool = [], [], self._graph_pool
     if self._split_allreduce():
       for k in (0, 1):
@@ -1225,6 +1227,8 @@ class DQNAgent(object):
     if g is None:
       self._join_fc()                 # nothing outside the capture may be pending
       torch.cuda.synchronize(self._device)
+      if self._pg is not None and self._rccl is None:
+        parallel.settle_watchdog()
       g = torch.cuda.CUDAGraph()
       if self._pg is None:
         with torch.cuda.graph(g, pool=self._graph_pool):

@@ -11,6 +11,7 @@ ranks' single-GPU gradients, not a single B*N batch.
 """
 import ctypes
 import os
+import time
 
 import torch
 import torch.distributed as dist
@@ -168,6 +169,17 @@ def replicas_in_sync(flat_params, group=None):
 _CAPTURABLE = {}
 
 
+def settle_watchdog():
+  """Before capturing torch.distributed collectives: torch's process-group watchdog polls
+  the events of the works it still holds (~every 100 ms) from its own thread; one held
+  when a capture started was seen queried as "recorded in a capturing stream", and the
+  watchdog aborted the process (ROCm 7.2, torch 2.10; one run in many, tests/test_gpu_rccl
+  capture probe).  The caller has synchronized the device; this lets the watchdog retire
+  the completed eager works first.  (The learner's own RCCL communicators, RcclComm, have
+  no watchdog.)"""
+  time.sleep(0.5)
+
+
 def collectives_capturable(group, device, stream=None, sharded=False, group2=None, comms=None):
   """Whether every rank of ``group`` can capture this backend's all-reduce into a HIP
   graph and replay it correctly -- probed once per group on a small tensor, the ranks
@@ -231,6 +243,8 @@ def collectives_capturable(group, device, stream=None, sharded=False, group2=Non
   # failure there is fatal on every rank instead of one rank leaving the others blocked
   collectives(torch.cuda.current_stream(device))
   torch.cuda.synchronize(device)
+  if comms is None:
+    settle_watchdog()
   try:
     cap.wait_stream(torch.cuda.current_stream(device))
     with torch.cuda.stream(cap):
