@@ -630,6 +630,10 @@ typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
 typedef float f32x2v __attribute__((ext_vector_type(2)));
 // two fp32 -> their hi / mid / lo bf16 pieces, each pair packed (element 0 low)
 __device__ __forceinline__ void split_x3(float a, float b, unsigned& h, unsigned& m, unsigned& l) {
+#ifdef DQ_ABLATE_X6_SPLIT   // timing experiments only: the pieces without the split's VALU work
+  h = m = l = __builtin_amdgcn_perm(__float_as_uint(b), __float_as_uint(a), 0x07060302u);
+  return;
+#endif
   const unsigned hu = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2v){a, b}, bf16x2v));
   const float ra = a - __uint_as_float(hu << 16), rb = b - __uint_as_float(hu & 0xffff0000u);
   const unsigned mu = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2v){ra, rb}, bf16x2v));
@@ -655,10 +659,15 @@ __device__ __forceinline__ void split_x3_8(const float* v, bf16x8& h, bf16x8& m,
   m = __builtin_bit_cast(bf16x8, mu);
   l = __builtin_bit_cast(bf16x8, lu);
 }
-// acc += A B over one 16-k step from the pieces, smallest pairs first
+// acc += A B over one 16-k step from the pieces, smallest pairs first.
+// -DDQ_X6_PAIRS=1 (throughput experiments, NOT fp32): hi.hi only -- a plain bf16 GEMM.
+#ifndef DQ_X6_PAIRS
+#define DQ_X6_PAIRS 6
+#endif
 __device__ __forceinline__ f32x16 mfma_x6(const bf16x8& ah, const bf16x8& am, const bf16x8& al,
                                           const bf16x8& bh, const bf16x8& bm, const bf16x8& bl,
                                           f32x16 acc) {
+  if (DQ_X6_PAIRS == 1) return __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
