@@ -33,8 +33,14 @@ constexpr int H = 512;
 // h = relu(x W1^T + b1): K = 7744, 4 slabs (R/128 x 4 tiles x 4) -- two 16-wave blocks per
 // CU; 4 fills the 512 slots once at R = 4096 and 1.5 times at R = 6144, measured best
 // (config 5: 4 -> 614-616, 6 -> 609-610, 8 -> 607-608 steps/s, profiles/r2_s5_iqn_fc1_split_ab.log)
-constexpr int kSplitFc1 = 4;
-constexpr int kSplitW1 = 2;       // dW1: K = R (1 / 4 measured equal, profiles/r2_s5_iqn_dw1_split_ab.log)
+#ifndef DQ_IQN_SPLIT_FC1            // compile-time overrides for A/B builds only
+#define DQ_IQN_SPLIT_FC1 4
+#endif
+#ifndef DQ_IQN_SPLIT_W1
+#define DQ_IQN_SPLIT_W1 2
+#endif
+constexpr int kSplitFc1 = DQ_IQN_SPLIT_FC1;
+constexpr int kSplitW1 = DQ_IQN_SPLIT_W1;  // dW1: K = R (1 / 4 measured equal, profiles/r2_s5_iqn_dw1_split_ab.log)
 constexpr int kSplitWe = 8;       // dWe: K = R, 61 row tiles
 constexpr int kSplitW2 = 32;      // dW2: M = A, K = R
 
