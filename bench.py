@@ -203,6 +203,10 @@ def other_configs(device, steps):
                                  'centered RMSProp, 1M-transition buffer')
   res['iqn_breakout']['workload'] = ('config 5: IQN Breakout (4 actions), N=N\'=64, K=32, n=3, '
                                      'uniform replay, Adam, 1M-transition buffer')
+  # the quantile heads' big GEMMs run the split-bf16 matrix-core form (fp32 operands as
+  # exact hi + mid + lo bf16 sums, six products: fp32 to rounding, not a bf16 GEMM)
+  res['iqn_breakout']['gemm_form'] = ('split-bf16 x6 (fp32 to rounding) for the embedding, FC1 '
+                                      'and dW1/dWe; exact f32 MFMA for dX and the torso')
   return res
 
 

@@ -71,6 +71,7 @@ __device__ __forceinline__ float bload1(const float* base, int off, bool ok) {
 template <class G>
 struct Im2col {
   static constexpr bool kFast = true;
+  static constexpr bool kConvFwd = true;   // the forward convolutions (cnn_x6)
   const float* x;
   __device__ __forceinline__ int offset(int m, int k) const {   // -1 in the padding
     const int b = m / (G::OH * G::OW), p = m - b * (G::OH * G::OW);
@@ -675,6 +676,35 @@ __device__ __forceinline__ f32x16 mfma_x6(const bf16x8& ah, const bf16x8& am, co
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc, 0, 0, 0);
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
 }
+// one bf16x8 piece of eight fp32 values (round to nearest), the remainders left in v
+__device__ __forceinline__ bf16x8 peel8(float* v) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 p;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const unsigned u = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2v){v[2 * i], v[2 * i + 1]}, bf16x2v));
+    v[2 * i] -= __uint_as_float(u << 16);
+    v[2 * i + 1] -= __uint_as_float(u & 0xffff0000u);
+    p[i] = u;
+  }
+  return __builtin_bit_cast(bf16x8, p);
+}
+// mfma_x6 with B split as it goes (fewer live registers: B's pieces one at a time), the
+// same six pairs, the large one last: al.bh, am.bh, am.bm, ah.bm, ah.bl, ah.bh
+__device__ __forceinline__ f32x16 mfma_x6_lazy(const bf16x8& ah, const bf16x8& am, const bf16x8& al,
+                                               float* bv, f32x16 acc) {
+  const bf16x8 bh = peel8(bv);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc, 0, 0, 0);
+  {
+    const bf16x8 bm = peel8(bv);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc, 0, 0, 0);
+  }
+  const bf16x8 bl = peel8(bv);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+}
 // the same with the five correction pairs in their own accumulator (its magnitude
 // ~2^-8 of the main one), the two added once at the end of the K loop
 __device__ __forceinline__ void mfma_x6_2(const bf16x8& ah, const bf16x8& am, const bf16x8& al,
@@ -1006,10 +1036,9 @@ __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& 
           if constexpr (kX6) {
             // each staged element is this lane's alone (one 32 x 32 tile per wave):
             // split as read, one 16-k step of six bf16 MFMAs for the half
-            bf16x8 ah, am, al, bh, bm, bl;
+            bf16x8 ah, am, al;
             split_x3_8(av, ah, am, al);
-            split_x3_8(bv, bh, bm, bl);
-            acc = mfma_x6(ah, am, al, bh, bm, bl, acc);
+            acc = mfma_x6_lazy(ah, am, al, bv, acc);
           } else {
 #pragma unroll
             for (int s = 0; s < 8; ++s)
@@ -1287,11 +1316,18 @@ void gemm_form(Ctx& c, AL a, BL b, EP e, int M, int N, int K, int splits) {
 #ifndef DQ_CNN_X6
 #define DQ_CNN_X6 0
 #endif
-template <int WM, int WN, int WK>
-constexpr bool cnn_x6() { return DQ_CNN_X6 && Tile<WM, WN, WK>::kPrivate; }
+template <class L, class = void>
+struct IsConvFwd : std::false_type {};
+template <class L>
+struct IsConvFwd<L, std::void_t<decltype(L::kConvFwd)>> : std::integral_constant<bool, L::kConvFwd> {};
+// DQ_CNN_X6: 1 = every wave-private tile, 2 = only the forward convolutions' (Im2col A)
+template <int WM, int WN, int WK, class AL>
+constexpr bool cnn_x6() {
+  return Tile<WM, WN, WK>::kPrivate && (DQ_CNN_X6 == 1 || (DQ_CNN_X6 == 2 && IsConvFwd<AL>::value));
+}
 template <int WM, int WN, int WK, class AL, class BL, class EP>
 void gemm(Ctx& c, AL a, BL b, EP e, int M, int N, int K, int splits = 1) {
-  gemm_form<WM, WN, WK, cnn_x6<WM, WN, WK>()>(c, a, b, e, M, N, K, splits);
+  gemm_form<WM, WN, WK, cnn_x6<WM, WN, WK, AL>()>(c, a, b, e, M, N, K, splits);
 }
 // split-bf16 MFMA (X6Img): fp32 to rounding at 2.7x the f32 matrix rate
 template <int WM, int WN, int WK, class AL, class BL, class EP>

@@ -56,8 +56,8 @@ struct GemmOp {
   int M, N, K, kchunk, gx, gy, gz;
   __device__ __forceinline__ void run(int blk, float* smem) const {
     const int bx = blk % gx, by = (blk / gx) % gy, bz = blk / (gx * gy);
-    igemm_block<WM, WN, WK, AL, BL, EP, kLate, cnn_x6<WM, WN, WK>()>(a, b, e, M, N, K, kchunk, bx, by,
-                                                                  bz, smem);
+    igemm_block<WM, WN, WK, AL, BL, EP, kLate, cnn_x6<WM, WN, WK, AL>()>(a, b, e, M, N, K, kchunk,
+                                                                      bx, by, bz, smem);
   }
   int blocks() const { return gx * gy * gz; }
 };
