@@ -8,7 +8,7 @@ import os
 
 from dopamine_amd._build import HEADER, LIB_PATH  # noqa: F401
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 OK = 0
 (ST_OK, ST_EMPTY_TREE, ST_MAX_ATTEMPTS, ST_TAPE_EXHAUSTED, ST_NEG_PRIORITY, ST_TOO_FEW, ST_BAD_INDEX,
  ST_BROADCAST) = range(8)
@@ -48,7 +48,8 @@ class AdamArgs(ctypes.Structure):
               ('state', ctypes.c_void_p), ('slot', ctypes.c_int32), ('lr', ctypes.c_float),
               ('beta1', ctypes.c_float), ('beta2', ctypes.c_float), ('epsilon', ctypes.c_float),
               ('kind', ctypes.c_int32), ('centered', ctypes.c_int32), ('mg', ctypes.c_void_p),
-              ('decay', ctypes.c_float), ('momentum', ctypes.c_float)]
+              ('decay', ctypes.c_float), ('momentum', ctypes.c_float),
+              ('no_grad_store', ctypes.c_int32)]
 
 
 OPT_ADAM, OPT_RMSPROP = 0, 1

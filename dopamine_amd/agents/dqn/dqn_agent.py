@@ -340,10 +340,18 @@ class DQNAgent(object):
     return (self.fuse_optimizer and self._hip is not None and self._pg is None and
             isinstance(self._opt, (ops.TF1Adam, ops.TF1RMSProp)))
 
+  def _store_grads(self):
+    """Whether the fused-optimizer backward also writes the gradients it consumes to the
+    flat gradient buffer: for ``keep_gradients`` (the agent's attribute; TF keeps no
+    such buffer, so the bench drives the agent with it off) and while tracing.  The
+    parameters and optimizer state are bitwise the same either way."""
+    return bool(self.keep_gradients or self._trace is not None)
+
   def _backward(self, y, g, k=0):
     if self._hip is not None:       # all gradients stored into the flat buffer
       groups = (1, 7) if self._fused() else None    # fused: d h came with the loss
       if self._fused_opt():
+        self._hip['online'].store_grads = self._store_grads()
         self._hip['online'].backward(g, adam=self._opt, slot=k, groups=groups)
       else:
         self._hip['online'].backward(g, groups=groups)
@@ -516,6 +524,7 @@ class DQNAgent(object):
       riders = self._place_riders(riders)
       adam = self._opt if self._fused_opt() else None
       f = self._bwd_first()
+      self._hip['online'].store_grads = self._store_grads()
       self._hip['online'].backward(g, riders=riders, adam=adam, slot=k, head=self._head,
                                    groups=(f, 7), head_from=self._bwd_head_from())
       self._head = None
@@ -653,6 +662,9 @@ class DQNAgent(object):
     o = n - self._grad_buckets()[0].numel()
     return o + (n - o) % (4 * self._world()), n
 
+  # with the optimizer fused into the backward (single replica), also write the gradients
+  # it consumes to the flat gradient buffer (``_store_grads``); bench.py turns it off
+  keep_gradients = True
   # ZeRO-1: the slice's Adam update on its own stream between the reduce-scatter and the
   # all-gather (comm -> comm_opt -> comm) instead of on the comm stream
   zero_update_stream = False

@@ -95,17 +95,22 @@ class HipNatureCNN(object):
     return _lib.CnnNet(p=ctypes.cast(ctypes.pointer(self._p), ctypes.c_void_p), x=x.data_ptr(),
                        a=ctypes.cast(ctypes.pointer(self._a), ctypes.c_void_p), ws=self.ws.data_ptr())
 
+  # with the optimizer fused into a gradient epilogue, also write that gradient to
+  # net.fp.grad (False: it is consumed in registers -- dq_adam_args.no_grad_store)
+  store_grads = True
+
   def _adam_args(self, adam, slot):
     """dq_adam_args of an ops.TF1Adam or ops.TF1RMSProp over net.fp.flat."""
     assert adam.params.data_ptr() == self.net.fp.flat.data_ptr(), 'adam must own net.fp.flat'
+    ngs = 0 if self.store_grads else 1
     if hasattr(adam, 'ms'):          # TF1RMSProp: ms / mom / mg slots (kind DQ_OPT_RMSPROP)
       return _lib.AdamArgs(var=adam.params.data_ptr(), m=adam.ms.data_ptr(), v=adam.mom.data_ptr(),
                            lr=adam.lr, epsilon=adam.eps, kind=_lib.OPT_RMSPROP,
                            centered=int(adam.centered), mg=adam.mg.data_ptr(), decay=adam.decay,
-                           momentum=adam.mu)
+                           momentum=adam.mu, no_grad_store=ngs)
     return _lib.AdamArgs(var=adam.params.data_ptr(), m=adam.m.data_ptr(), v=adam.v.data_ptr(),
                          state=adam.state.data_ptr(), slot=int(slot), lr=adam.lr,
-                         beta1=adam.b1, beta2=adam.b2, epsilon=adam.eps)
+                         beta1=adam.b1, beta2=adam.b2, epsilon=adam.eps, no_grad_store=ngs)
 
   def backward(self, dout, parallel=False, adam=None, slot=0, groups=None, riders=None, head=None,
                head_from=3):

@@ -336,6 +336,7 @@ struct AdamDev {
   float* state;
   int slot;
   float lr, b1, b2, eps;
+  int store_grad;          // fused epilogues: also write the gradient (dq_adam_args.no_grad_store)
 };
 struct EpiGradAdam {
   float* gw;
@@ -365,12 +366,12 @@ struct EpiGradAdam {
     adam1(q.w, g, q.m, q.v, alpha, omb1, omb2, o.eps);
     if (n < nw) {
       const int64_t i = (int64_t)m * nw + n;
-      gw[i] = g;
+      if (o.store_grad) gw[i] = g;
       w[i] = q.w;
       mw[i] = q.m;
       vw[i] = q.v;
     } else {
-      gb[m] = g;
+      if (o.store_grad) gb[m] = g;
       b[m] = q.w;
       mb[m] = q.m;
       vb[m] = q.v;
@@ -402,14 +403,14 @@ struct EpiGradAdamVec {
       const int64_t i = (int64_t)m * nw + n;
       float pw = w[i], pm = mw[i], pv = vw[i];
       adam1(pw, g, pm, pv, alpha, omb1, omb2, o.eps);
-      gw[i] = g;
+      if (o.store_grad) gw[i] = g;
       w[i] = pw;
       mw[i] = pm;
       vw[i] = pv;
     } else if (n == nw) {
       float pw = b[m], pm = mb[m], pv = vb[m];
       adam1(pw, g, pm, pv, alpha, omb1, omb2, o.eps);
-      gb[m] = g;
+      if (o.store_grad) gb[m] = g;
       b[m] = pw;
       mb[m] = pm;
       vb[m] = pv;
@@ -429,7 +430,7 @@ struct EpiGradAdamVec {
     adam1(pw.y, g.y, pm.y, pv.y, alpha, omb1, omb2, o.eps);
     adam1(pw.z, g.z, pm.z, pv.z, alpha, omb1, omb2, o.eps);
     adam1(pw.w, g.w, pm.w, pv.w, alpha, omb1, omb2, o.eps);
-    *reinterpret_cast<float4*>(gw + i) = g;
+    if (o.store_grad) *reinterpret_cast<float4*>(gw + i) = g;
     *reinterpret_cast<float4*>(w + i) = pw;
     *reinterpret_cast<float4*>(mw + i) = pm;
     *reinterpret_cast<float4*>(vw + i) = pv;
@@ -441,10 +442,12 @@ struct EpiGradAdamVec {
 struct RmsDev {
   float lr, omr, mu, eps;
   int centered;
+  int store_grad;          // as AdamDev::store_grad
 };
 __host__ inline RmsDev rms_dev(const dq_adam_args* a) {
   // 1 - rho in host float32 arithmetic: the value k_rmsprop's __fsub_rn forms
-  return RmsDev{a->lr, 1.0f - a->decay, a->momentum, a->epsilon, a->centered != 0};
+  return RmsDev{a->lr, 1.0f - a->decay, a->momentum, a->epsilon, a->centered != 0,
+                a->no_grad_store == 0};
 }
 struct EpiGradRms {
   float* gw;
@@ -468,13 +471,13 @@ struct EpiGradRms {
     rms1(q.w, g, q.m, q.g2, q.v, o.lr, o.omr, o.mu, o.eps, o.centered != 0);
     if (n < nw) {
       const int64_t i = (int64_t)m * nw + n;
-      gw[i] = g;
+      if (o.store_grad) gw[i] = g;
       w[i] = q.w;
       mw[i] = q.m;
       vw[i] = q.v;
       if (o.centered) gw2[i] = q.g2;
     } else {
-      gb[m] = g;
+      if (o.store_grad) gb[m] = g;
       b[m] = q.w;
       mb[m] = q.m;
       vb[m] = q.v;
@@ -556,7 +559,9 @@ struct GradEpi<1> {
     const dq_adam_args* a = h.a;
     const ptrdiff_t ow = w - a->var, ob = b - a->var;
     return EpiGradAdam{gw, gb, nw, w, a->m + ow, a->v + ow, b, a->m + ob, a->v + ob,
-                       AdamDev{a->state, a->slot, a->lr, a->beta1, a->beta2, a->epsilon}, bump};
+                       AdamDev{a->state, a->slot, a->lr, a->beta1, a->beta2, a->epsilon,
+                               a->no_grad_store == 0},
+                       bump};
   }
 };
 template <>

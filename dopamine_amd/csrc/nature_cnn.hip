@@ -279,7 +279,7 @@ struct OptPart<1> {
     const int64_t n = (int64_t)(w1 - w0);
     const int64_t per = (int64_t)kGroupT * AdamOp::kU;
     const int nb = (int)std::max<int64_t>(1, ((n >> 2) + per - 1) / per);
-    const AdamDev od{o->state, o->slot, o->lr, o->beta1, o->beta2, o->epsilon};
+    const AdamDev od{o->state, o->slot, o->lr, o->beta1, o->beta2, o->epsilon, 1};   // reads g
     return AdamOp{w0, g->conv1_w + (w0 - p->conv1_w), o->m + off, o->v + off, n, od, nb};
   }
 };
@@ -308,7 +308,8 @@ struct Fc1EpiOpt<1> {
     const ptrdiff_t ow = p->fc1_w - o->var, ob = p->fc1_b - o->var;
     return EpiGradAdamVec{g->fc1_w, g->fc1_b, kFlat, p->fc1_w, o->m + ow, o->v + ow, p->fc1_b,
                           o->m + ob, o->v + ob,
-                          AdamDev{o->state, o->slot, o->lr, o->beta1, o->beta2, o->epsilon}};
+                          AdamDev{o->state, o->slot, o->lr, o->beta1, o->beta2, o->epsilon,
+                                  o->no_grad_store == 0}};
   }
 };
 

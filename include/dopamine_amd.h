@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define DQ_ABI_VERSION 4
+#define DQ_ABI_VERSION 5
 
 /* host-side return codes */
 #define DQ_OK 0
@@ -387,6 +387,9 @@ typedef struct dq_adam_args {
   int32_t centered;  /* RMSProp: ApplyCenteredRMSProp (reads / writes mg) */
   float* mg;         /* RMSProp, centered: the mean-gradient slot, same layout as var */
   float decay, momentum;   /* RMSProp: rho, mu */
+  int32_t no_grad_store;   /* 1: where the update is fused into a gradient epilogue, the
+                              gradient is consumed in registers and not written to g (the
+                              parameters and moments come out bitwise the same); 0: write it */
 } dq_adam_args;
 /* backward + optimizer step in one pass (single-replica training: no gradient
    all-reduce between them).  Gradients are still written to g. */

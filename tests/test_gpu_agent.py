@@ -334,3 +334,36 @@ def test_device_epsilon_greedy_consumes_random_as_the_host_path(kind):
   np.testing.assert_array_equal(res[0][1], res[1][1])
   assert res[0][2] == res[1][2]
   np.testing.assert_array_equal(res[0][3], res[1][3])
+
+
+@pytest.mark.parametrize('kind', ['rainbow', 'dqn'])
+def test_fused_optimizer_without_gradient_stores_is_bitwise_the_same(kind):
+  """keep_gradients=False (the bench's drive: the fused TF1 Adam / RMSProp consumes the
+  gradient in registers, dq_adam_args.no_grad_store) leaves parameters, optimizer state
+  and sum tree bitwise those of the gradient-storing backward, over graph-replayed chunks."""
+  from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
+  res = []
+  for keep in (True, False):
+    random.seed(7); np.random.seed(7); torch.manual_seed(7)
+    if kind == 'rainbow':
+      a = _rainbow(target_update_period=40)
+    else:
+      a = DQNAgent(num_actions=6, replay_capacity=3000, batch_size=32, min_replay_history=100,
+                   target_update_period=40)
+      _fill(a._replay.memory, 6, 3)
+    a.keep_gradients = keep
+    assert a._fused_opt()
+    a.train_gradient_steps(3)
+    a.train_gradient_steps(12)
+    a._discard_prefetch()
+    torch.cuda.synchronize()
+    slots = (a._opt.m, a._opt.v) if kind == 'rainbow' else (a._opt.ms, a._opt.mom, a._opt.mg)
+    st = [t.cpu().clone() for t in slots]
+    leaves = a._replay.memory.sum_tree.nodes[-1].copy() if kind == 'rainbow' else None
+    res.append((a.online_convnet.fp.flat.cpu().clone(), st, leaves, a._opt_steps))
+  assert torch.equal(res[0][0], res[1][0])
+  for x, y in zip(res[0][1], res[1][1]):
+    assert torch.equal(x, y)
+  if kind == 'rainbow':
+    np.testing.assert_array_equal(res[0][2], res[1][2])
+  assert res[0][3] == res[1][3]
