@@ -417,6 +417,39 @@ struct EpiGradAdamVec {
     }
   }
   __device__ __forceinline__ void operator()(int m, int n, float g, int) const { scalar(m, n, g); }
+#ifndef DQ_VEC_PRE
+#define DQ_VEC_PRE 1
+#endif
+  // two-phase vector form (kVecPre): the next row group's parameter / moment loads are
+  // issued before this group's stores (the compiler cannot tell the rows apart and would
+  // otherwise serialise each group's loads behind the previous group's stores)
+  static constexpr bool kVecPre = DQ_VEC_PRE != 0;
+  struct VPre {
+    float4 w, m, v;
+  };
+  __device__ __forceinline__ VPre vpre(int m, int n) const {
+    if (n >= nw) return VPre{zero4(), zero4(), zero4()};
+    const int64_t i = (int64_t)m * nw + n;
+    return VPre{ld4(w + i), ld4(mw + i), ld4(vw + i)};
+  }
+  __device__ __forceinline__ void vcommit(int m, int n, float4 g, const VPre& p) const {
+    if (n >= nw) {                 // the bias column (and the tile's padding past it)
+      scalar(m, n, g.x);
+      return;
+    }
+    const int64_t i = (int64_t)m * nw + n;
+    float4 pw = p.w, pm = p.m, pv = p.v;
+    const float alpha = adam_alpha_of(o.state, o.slot, o.lr);
+    const float omb1 = __fsub_rn(1.0f, o.b1), omb2 = __fsub_rn(1.0f, o.b2);
+    adam1(pw.x, g.x, pm.x, pv.x, alpha, omb1, omb2, o.eps);
+    adam1(pw.y, g.y, pm.y, pv.y, alpha, omb1, omb2, o.eps);
+    adam1(pw.z, g.z, pm.z, pv.z, alpha, omb1, omb2, o.eps);
+    adam1(pw.w, g.w, pm.w, pv.w, alpha, omb1, omb2, o.eps);
+    if (o.store_grad) *reinterpret_cast<float4*>(gw + i) = g;
+    *reinterpret_cast<float4*>(w + i) = pw;
+    *reinterpret_cast<float4*>(mw + i) = pm;
+    *reinterpret_cast<float4*>(vw + i) = pv;
+  }
   __device__ __forceinline__ void vec4(int m, int n, float4 g) const {
     if (n >= nw) {                 // the bias column (and the tile's padding past it)
       scalar(m, n, g.x);
@@ -510,6 +543,15 @@ struct HasPre<EP, decltype((void)EP::kPre)> {
 // EP::kVec: the epilogue takes 4 consecutive columns at a time (E.vec4(m, n, float4)),
 // so its loads and stores are 16 B per lane: igemm_block passes each wave's 32 x 32
 // accumulator tile through LDS (WK == 1 only; N % 4 == 0).
+template <class EP, class = void>
+struct HasVecPre {
+  static constexpr bool value = false;
+};
+template <class EP>
+struct HasVecPre<EP, decltype((void)EP::kVecPre)> {
+  static constexpr bool value = EP::kVecPre;
+};
+
 template <class EP, class = void>
 struct HasVec {
   static constexpr bool value = false;
@@ -1097,6 +1139,21 @@ __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if constexpr (HasVecPre<EP>::value) {
+      const int c = 4 * (lane & 7), n = n0 + wn * 32 + c;
+      auto mrow = [&](int it) { return m0 + wm * 32 + 8 * it + (lane >> 3); };
+      typename EP::VPre p = E.vpre(min(mrow(0), M - 1), n);
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        typename EP::VPre nx = p;
+        if (it < 3) nx = E.vpre(min(mrow(it + 1), M - 1), n);   // clamped: loads never branch
+        const float* q = W + (8 * it + (lane >> 3)) * 33 + c;
+        const int m = mrow(it);
+        if (m < M && n < N) E.vcommit(m, n, make_float4(q[0], q[1], q[2], q[3]), p);
+        p = nx;
+      }
+      return;
+    }
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int row = 8 * it + (lane >> 3), c = 4 * (lane & 7);
