@@ -522,6 +522,42 @@ struct EpiGradRms {
   }
 };
 
+// EpiGradRms as a vector (kVec) epilogue with the two-phase loads of EpiGradAdamVec:
+// fc1's centered RMSProp (ms, mom, mg) applied in its weight-gradient GEMM
+struct EpiGradRmsVec {
+  EpiGradRms s;            // the scalar form: pointers, constants, the bias column
+  static constexpr bool kVec = true;
+  static constexpr bool kVecPre = true;
+  struct VPre {
+    float4 w, m, v, g2;
+  };
+  __device__ __forceinline__ void operator()(int m, int n, float g, int) const { s(m, n, g, 0); }
+  __device__ __forceinline__ VPre vpre(int m, int n) const {
+    if (n >= s.nw) return VPre{zero4(), zero4(), zero4(), zero4()};
+    const int64_t i = (int64_t)m * s.nw + n;
+    return VPre{ld4(s.w + i), ld4(s.mw + i), ld4(s.vw + i), s.o.centered ? ld4(s.gw2 + i) : zero4()};
+  }
+  __device__ __forceinline__ void vcommit(int m, int n, float4 g, const VPre& p) const {
+    if (n >= s.nw) {               // the bias column (and the tile's padding past it)
+      s(m, n, g.x, 0);
+      return;
+    }
+    const int64_t i = (int64_t)m * s.nw + n;
+    float4 pw = p.w, pm = p.m, pv = p.v, p2 = p.g2;
+    const bool ce = s.o.centered != 0;
+    rms1(pw.x, g.x, pm.x, p2.x, pv.x, s.o.lr, s.o.omr, s.o.mu, s.o.eps, ce);
+    rms1(pw.y, g.y, pm.y, p2.y, pv.y, s.o.lr, s.o.omr, s.o.mu, s.o.eps, ce);
+    rms1(pw.z, g.z, pm.z, p2.z, pv.z, s.o.lr, s.o.omr, s.o.mu, s.o.eps, ce);
+    rms1(pw.w, g.w, pm.w, p2.w, pv.w, s.o.lr, s.o.omr, s.o.mu, s.o.eps, ce);
+    if (s.o.store_grad) *reinterpret_cast<float4*>(s.gw + i) = g;
+    *reinterpret_cast<float4*>(s.w + i) = pw;
+    *reinterpret_cast<float4*>(s.mw + i) = pm;
+    *reinterpret_cast<float4*>(s.vw + i) = pv;
+    if (ce) *reinterpret_cast<float4*>(s.gw2 + i) = p2;
+  }
+  __device__ __forceinline__ void vec4(int m, int n, float4 g) const { vcommit(m, n, g, vpre(m, n)); }
+};
+
 template <class EP, class = void>
 struct HasPf {
   static constexpr bool value = false;

@@ -298,8 +298,10 @@ struct OptPart<2> {
 };
 
 // fc1's weight gradient + its optimizer in the vector epilogue (DQ_FC1_EPI_OPT): TF1 Adam
-// over fc1_w and fc1_b, the riders' arithmetic.  Adam only: centered RMSProp's four state
-// arrays made the epilogue the longer path (config 2: 8,060 vs 8,143 steps/s with riders)
+// or centered RMSProp over fc1_w and fc1_b, the riders' arithmetic.  RMSProp's four state
+// arrays made the epilogue the longer path at first (config 2: 8,060 vs 8,143 steps/s with
+// riders); with the next row group's loads issued before this group's stores (kVecPre) it
+// is the shorter one: 8,295-8,348 vs 8,235-8,250 (profiles/r3_s3_rmsepi_ab.log)
 template <int kOpt>
 struct Fc1EpiOpt;
 template <>
@@ -312,6 +314,17 @@ struct Fc1EpiOpt<1> {
                                   o->no_grad_store == 0}};
   }
 };
+
+template <>
+struct Fc1EpiOpt<2> {       // centered RMSProp (DQN, config 2): DQ_FC1_EPI_RMS
+  static EpiGradRmsVec make(const dq_cnn_params* p, const dq_cnn_params* g, const dq_adam_args* o) {
+    return EpiGradRmsVec{GradEpi<2>::make(g->fc1_w, g->fc1_b, kFlat, p->fc1_w, p->fc1_b,
+                                          AdamHost{o}, 0)};
+  }
+};
+#ifndef DQ_FC1_EPI_RMS
+#define DQ_FC1_EPI_RMS 1
+#endif
 
 // A recorded replay operation (replay_dev.h) riding in a grouped launch: its
 // blocks come first in the launch so the single-wave sum-tree update / sampler
@@ -784,7 +797,8 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
       // TF1 Adam on fc1 in its weight-gradient GEMM's (vector) epilogue, launch 2, instead of
       // Adam riders over fc1 in launches 3-5 reading the stored gradient back (+0.6-1.2%
       // config 1: 7,600-7,644 vs 7,555-7,559 steps/s)
-      if constexpr (kHeadFrom >= 5 && kOpt == 1 && DQ_FC1_EPI_OPT) {
+      if constexpr (kHeadFrom >= 5 && (kOpt == 1 || (kOpt == 2 && DQ_FC1_EPI_RMS)) &&
+                    DQ_FC1_EPI_OPT) {
         auto dW_fc1a = gemm_op<4, 4, 1>(ColK{d->h, kHidden}, ColKOnes{a->a3, kFlat},
                                         Fc1EpiOpt<kOpt>::make(p, g, opt.a), kHidden, kFlat + 1,
                                         B, B);
