@@ -195,7 +195,7 @@ def other_configs(device, steps):
       # the learner loop's chunk gather: one K * B launch per chunk (K = 4), timed as the
       # headline's gather is (standalone launches, fresh random indices, HIP events)
       kb = agent._UNROLL * agent._batch_size
-      us, _, algo, gname = time_gather(agent, 100, batch=kb)
+      us, algo, gname = time_gather(agent, 100, batch=kb)
       gbs = algo / (us * 1e-6) / 1e9
       res[name]['chunk_gather_roofline'] = {
           'kernel': gname + ' (chunk gather, batch %d)' % kb, 'bound': 'hbm',
@@ -247,17 +247,12 @@ def time_gather(agent, iters, batch=None):
   e1.record(stream)
   e1.synchronize()
   graph_us = e0.elapsed_time(e1) * 1e3 / iters
-  # eager back-to-back launches on the same stream, for comparison
-  e0.record(stream)
-  for i in range(iters):
-    mem._gather(sets[i], B, layout, out)
-  e1.record(stream)
-  e1.synchronize()
-  eager_us = e0.elapsed_time(e1) * 1e3 / iters
+  # (no eager comparison loop: under rocprofv3 --stats this kernel's rows are then exactly
+  # the 10 warm-up launches and the 2 x iters graph launches timed here)
   S, obs = mem._stack_size, mem._obs_bytes
   algo_bytes = B * (2 * S * obs + 2 * S * obs * 4)   # u8 frames read + fp32 NCHW written
   name = {_lib.LAYOUT_F32_NHWC: 'k_gather_nhwc4', _lib.LAYOUT_F32_NORM: 'k_gather_f32'}[layout]
-  return graph_us, eager_us, algo_bytes, name
+  return graph_us, algo_bytes, name
 
 
 def time_gather_large(agent, batch=1024, iters=50):
@@ -304,19 +299,6 @@ def gather_traffic(batch):
     return round(float(d['traffic_bytes_per_launch'][str(batch)])), os.path.relpath(path, ROOT)
   except (OSError, KeyError, ValueError):
     return None, None
-
-
-def gather_in_step():
-  """The gather's marginal cost where the step runs it (a rider of backward launch B3):
-  B3's mean duration with and without the gather's blocks, from the committed rocprof A/B
-  (profiles/r2_gather_in_step.json, tools/gpu_r2s3i.sh), or None."""
-  path = os.path.join(ROOT, 'profiles', 'r2_gather_in_step.json')
-  try:
-    d = json.load(open(path))
-    return {k: d[k] for k in ('in_step_us', 'achieved_GBs', 'frac', 'b3_with_gather_us',
-                              'b3_without_gather_us')} | {'source': os.path.relpath(path, ROOT)}
-  except (OSError, KeyError, ValueError):
-    return None
 
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
@@ -411,6 +393,7 @@ def main():
   agent = None
   for zero in zeros:
     if agent is not None:
+      agent.close()                   # its RCCL communicators (N > 1) before the next pair
       del agent
       gc.collect()
       torch.cuda.empty_cache()
@@ -447,10 +430,7 @@ def main():
   for v in schedules.values():
     del v['_elapsed']
 
-  default_schedule = (world == 1 and not args.force_dist and not args.per_call and
-                      not args.no_graph and args.fuse_opt is None and args.ride is None and
-                      args.split_c51 is None)
-  graph_us, eager_us, algo_bytes, gname = time_gather(agent, args.gather_iters)
+  graph_us, algo_bytes, gname = time_gather(agent, args.gather_iters)
   large = time_gather_large(agent)
   traffic, traffic_src = gather_traffic(args.batch)
   achieved = algo_bytes / (graph_us * 1e-6) / 1e9
@@ -487,11 +467,8 @@ def main():
                      'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4),
                      'traffic': traffic, 'traffic_source': traffic_src,
                      'algo_bytes_per_launch': algo_bytes,
-                     'avg_launch_us': round(graph_us, 3), 'avg_launch_us_eager': round(eager_us, 3),
-                     'same_kernel_batch_1024': large,
-                     # the same kernel riding in the step (not the measured launch above):
-                     # a committed profile of the N = 1 default schedule, so only there
-                     'in_step_marginal': gather_in_step() if default_schedule else None},
+                     'avg_launch_us': round(graph_us, 3),
+                     'same_kernel_batch_1024': large},
         # supplementary: the whole step against the fp32 matrix peak (the CNN's fp32 MFMA
         # work; the step is launch- and latency-bound at B = 32, not MFMA-bound)
         'step_mfma': step_mfma(args.actions, args.batch, elapsed / args.steps),

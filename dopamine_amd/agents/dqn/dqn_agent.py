@@ -196,6 +196,24 @@ class DQNAgent(object):
       return None        # every rank agreed: torch.distributed's collectives instead
     return (parallel.RcclComm(self._pg, self._device), parallel.RcclComm(self._pg, self._device))
 
+  def close(self):
+    """Releases the learner's RCCL communicators (each holds proxy threads and device
+    buffers until destroyed): waits for the device, drops the HIP graphs that captured
+    their collectives, then destroys them.  The agent cannot train afterwards.  A no-op
+    for a single replica."""
+    self._join_fc()
+    torch.cuda.synchronize(self._device)
+    if self._rccl is not None:
+      self._graph_sets = {}
+      self._graph_pool = None
+      parallel.forget_capture_probes(self._rccl)
+      for c in self._rccl:
+        c.destroy()
+      self._rccl = None
+      self._closed = True
+
+  _closed = False
+
   def _ar_fc(self, t):
     """The fc bucket's all-reduce (mean), on the current (comm) stream."""
     if self._rccl is not None:
@@ -663,11 +681,21 @@ class DQNAgent(object):
     return o + (n - o) % (4 * self._world()), n
 
   # with the optimizer fused into the backward (single replica), also write the gradients
-  # it consumes to the flat gradient buffer (``_store_grads``); bench.py turns it off
-  keep_gradients = True
-  # ZeRO-1: the slice's Adam update on its own stream between the reduce-scatter and the
-  # all-gather (comm -> comm_opt -> comm) instead of on the comm stream
-  zero_update_stream = False
+  # it consumes to the flat gradient buffer (``_store_grads``); bench.py turns it off.
+  # Captured graphs bake the choice in, so it is fixed once the first graph exists.
+  _keep_gradients = True
+
+  @property
+  def keep_gradients(self):
+    return self._keep_gradients
+
+  @keep_gradients.setter
+  def keep_gradients(self, value):
+    value = bool(value)
+    if value != self._keep_gradients and self._graph_sets:
+      raise RuntimeError('keep_gradients must be set before the first captured gradient step '
+                         '(the HIP graphs already captured bake in the gradient stores)')
+    self._keep_gradients = value
   # HIP stream priority of the prefetch stream (the pipelined non-rider schedule, e.g. IQN's
   # target network beside the online backward): 0 normal, -1 high
   side_priority = 0
@@ -749,26 +777,16 @@ class DQNAgent(object):
       lo, n = self._shard_bounds()
       S = (n - lo) // self._world()
       r = torch.distributed.get_rank(self._pg)
-      # all three on the comm stream (1/N of the update is small beside the collectives;
-      # with the update on the second stream, comm -> comm_opt -> comm, the captured 4-step
-      # chunk graphs ended in a segfault at capture end on ROCm 7.2)
+      # all three on the comm stream: they are dependent, so a second stream for the
+      # update buys no overlap -- and that arrangement (comm -> second stream -> comm) made
+      # the captured chunk graphs segfault in hipStreamEndCapture on ROCm 7.2 (DESIGN §6;
+      # the repro is tools/capture_fork_repro.py, outside the product)
       with torch.cuda.stream(self._comm):
         if self._rccl is not None:
           self._rccl[0].reduce_scatter_mean_(grad[lo:n])
         else:
           parallel.reduce_scatter_mean_(grad[lo:n], self._pg)
-      upd = self._comm_opt if self.zero_update_stream else self._comm
-      if upd is not self._comm:
-        e = torch.cuda.Event()
-        e.record(self._comm)
-        upd.wait_event(e)
-      with torch.cuda.stream(upd):
         self._opt.step_part(grad, lo + r * S, lo + (r + 1) * S, slot=k, bump=False)
-      if upd is not self._comm:
-        e = torch.cuda.Event()
-        e.record(upd)
-        self._comm.wait_event(e)
-      with torch.cuda.stream(self._comm):
         if self._rccl is not None:
           self._rccl[0].all_gather_(self._opt.params[lo:n])
         else:
@@ -977,8 +995,6 @@ class DQNAgent(object):
     same graph, with N GPUs it is a second graph after the RCCL all-reduce."""
     pipe = self.pipeline if pipe is None else pipe
     torch.cuda.synchronize(self._device)
-    if self._pg is not None and self._rccl is None:
-      parallel.settle_watchdog()
     graphs, graphs_opt, pool = [], [], self._graph_pool
     if self._split_allreduce():
       for k in (0, 1):
@@ -994,8 +1010,8 @@ class DQNAgent(object):
           gr = None
           if fn is not None:
             gr = torch.cuda.CUDAGraph()
-            # thread_local: the process group's watchdog may still be querying the events
-            # of the collectives issued just before (global mode fails its queries)
+            # thread_local: torch's process-group watchdog thread polls the events of the
+            # collectives issued just before (global mode would fail its queries)
             with torch.cuda.graph(gr, pool=pool, capture_error_mode='thread_local'):
               fn()
             pool = gr.pool()
@@ -1158,6 +1174,8 @@ class DQNAgent(object):
     once per chunk); the steps, their order, RNG use and target syncs are exactly
     those of the per-call loop (tests/test_gpu_agent.py)."""
     n = int(n)
+    if self._closed:
+      raise RuntimeError('the agent was closed (its communicators are destroyed)')
     self._defer_fc = True
     try:
       self._train_gradient_steps(n)
@@ -1196,17 +1214,18 @@ class DQNAgent(object):
     return all(('chunk', self._UNROLL, k) in self._graph_sets for k in (0, 1))
 
   def _captures_collectives(self):
-    """N > 1 over RCCL with the split fused-head schedule: the gradient all-reduces
-    are captured inside the learner loop's chunk graphs (gloo's host-side
-    collectives cannot be)."""
+    """N > 1 over the learner's own RCCL communicators with the split fused-head schedule:
+    the gradient all-reduces are captured inside the learner loop's chunk graphs (gloo's
+    host-side collectives cannot be, torch.distributed's are not)."""
     if self._pg is None:
       return False
     import torch.distributed as dist
-    return (dist.get_backend(self._pg) == 'nccl' and self._split_allreduce() and
-            self._head_splits() and isinstance(self._opt, ops.TF1Adam) and
-            parallel.collectives_capturable(
-                self._pg, self._device, self._comm, sharded=self._sharded(),
-                group2=self._conv_group() if self._rccl is None else None, comms=self._rccl))
+    # (torch.distributed's own collectives are never captured: parallel.collectives_capturable)
+    return (dist.get_backend(self._pg) == 'nccl' and self._rccl is not None and
+            self._split_allreduce() and self._head_splits() and
+            isinstance(self._opt, ops.TF1Adam) and
+            parallel.collectives_capturable(self._pg, self._device, self._comm,
+                                            sharded=self._sharded(), comms=self._rccl))
 
   def _chunks_apply(self):
     return (self._hip is not None and self.pipeline and
@@ -1239,8 +1258,6 @@ class DQNAgent(object):
     if g is None:
       self._join_fc()                 # nothing outside the capture may be pending
       torch.cuda.synchronize(self._device)
-      if self._pg is not None and self._rccl is None:
-        parallel.settle_watchdog()
       g = torch.cuda.CUDAGraph()
       if self._pg is None:
         with torch.cuda.graph(g, pool=self._graph_pool):
@@ -1282,6 +1299,8 @@ class DQNAgent(object):
 
   def _train_step(self):
     """dqn_agent.py:418-442."""
+    if self._closed:
+      raise RuntimeError('the agent was closed (its communicators are destroyed)')
     if self._replay.memory.add_count > self.min_replay_history:
       if self.training_steps % self.update_period == 0:
         self._run_train_op()
@@ -1320,14 +1339,29 @@ class DQNAgent(object):
         d['opt_' + k] = v
     return d
 
+  def _rank_dir(self, checkpoint_dir):
+    """Where this learner's files go.  A single replica: ``checkpoint_dir`` itself, as the
+    reference (dqn_agent.py:482-551; crb:593-687).  Data-parallel learners (a process
+    group): ``checkpoint_dir/rank<r>`` per group rank -- each rank owns a different buffer
+    and sum tree, and the reference's file names (``$store$_*_ckpt.N.gz``, ``tf_ckpt-N``)
+    would otherwise collide in a shared run directory."""
+    if self._pg is None:
+      return checkpoint_dir
+    import torch.distributed as dist
+    return os.path.join(checkpoint_dir, 'rank%d' % dist.get_rank(self._pg))
+
   def bundle_and_checkpoint(self, checkpoint_dir, iteration_number):
-    """dqn_agent.py:482-510 (torch tensors instead of a tf.train.Saver)."""
+    """dqn_agent.py:482-510 (torch tensors instead of a tf.train.Saver).  With a process
+    group every rank calls it (ZeRO-1 gathers the moments first) and writes under
+    ``checkpoint_dir/rank<r>`` (_rank_dir)."""
     self._join_fc()
     # ZeRO-1: complete moments on every rank -- a collective, so every rank reaches it
     # before any rank-local early return
     self._gather_opt_state()
     if not os.path.isdir(checkpoint_dir):
       return None
+    checkpoint_dir = self._rank_dir(checkpoint_dir)
+    os.makedirs(checkpoint_dir, exist_ok=True)
     torch.save({k: v.detach().cpu() for k, v in self._ckpt_tensors().items()},
                os.path.join(checkpoint_dir, 'tf_ckpt-{}'.format(iteration_number)))
     stale = iteration_number - self.max_tf_checkpoints_to_keep
@@ -1342,7 +1376,8 @@ class DQNAgent(object):
             '_opt_steps': self._opt_steps}
 
   def unbundle(self, checkpoint_dir, iteration_number, bundle_dictionary):
-    """dqn_agent.py:512-551."""
+    """dqn_agent.py:512-551 (with a process group: from ``checkpoint_dir/rank<r>``)."""
+    checkpoint_dir = self._rank_dir(checkpoint_dir)
     self._discard_prefetch()          # the buffer (and its RNG use) is replaced below
     self._replay.memory.sync_rng(raise_errors=False)
     try:

@@ -15,31 +15,29 @@
 // RCCL is opened with dlopen on first use, so the library loads (and its exports can be
 // checked) on a host without a GPU or RCCL.
 #include <dlfcn.h>
+#include <rccl/rccl.h>   // types, enums and prototypes only: the library itself is dlopened
 
 #include <cstring>
 #include <mutex>
 
 #include "common.h"
 
+static_assert(DQ_COMM_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "ncclUniqueId size changed");
+static_assert(sizeof(ncclUniqueId) == DQ_COMM_ID_BYTES, "ncclUniqueId layout changed");
+
 namespace dq {
 namespace {
 
-// the subset of rccl.h (/opt/rocm/include/rccl/rccl.h) used here
-typedef struct ncclComm* ncclComm_t;
-typedef struct { char internal[128]; } ncclUniqueId;
-typedef int ncclResult_t;            // ncclSuccess = 0
-constexpr int kNcclFloat32 = 7;
-constexpr int kNcclAvg = 4;
-
+// the entry points used here, typed by rccl.h's own declarations
 struct Rccl {
-  ncclResult_t (*GetUniqueId)(ncclUniqueId*);
-  ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int);
-  ncclResult_t (*CommDestroy)(ncclComm_t);
-  ncclResult_t (*AllReduce)(const void*, void*, size_t, int, int, ncclComm_t, hipStream_t);
-  ncclResult_t (*ReduceScatter)(const void*, void*, size_t, int, int, ncclComm_t, hipStream_t);
-  ncclResult_t (*AllGather)(const void*, void*, size_t, int, ncclComm_t, hipStream_t);
-  const char* (*GetErrorString)(ncclResult_t);
-  ncclResult_t (*GetVersion)(int*);
+  decltype(&ncclGetUniqueId) GetUniqueId;
+  decltype(&ncclCommInitRank) CommInitRank;
+  decltype(&ncclCommDestroy) CommDestroy;
+  decltype(&ncclAllReduce) AllReduce;
+  decltype(&ncclReduceScatter) ReduceScatter;
+  decltype(&ncclAllGather) AllGather;
+  decltype(&ncclGetErrorString) GetErrorString;
+  decltype(&ncclGetVersion) GetVersion;
 };
 
 Rccl g_rccl;
@@ -72,6 +70,12 @@ bool open_rccl() {
     DQ_SYM(GetErrorString, "ncclGetErrorString")
     DQ_SYM(GetVersion, "ncclGetVersion")
 #undef DQ_SYM
+    int v = 0;
+    if (g_rccl.GetVersion(&v) != ncclSuccess || v / 100 != NCCL_VERSION_CODE / 100) {
+      g_open_error = "librccl.so.1 version " + std::to_string(v) + " differs from rccl.h's " +
+                     std::to_string(NCCL_VERSION_CODE) + " (major.minor)";
+      return;
+    }
     ok = true;
   });
   if (!ok) set_error(g_open_error);
@@ -79,7 +83,7 @@ bool open_rccl() {
 }
 
 int nccl_status(ncclResult_t r, const char* what) {
-  if (r == 0) return DQ_OK;
+  if (r == ncclSuccess) return DQ_OK;
   set_error(std::string(what) + ": " + g_rccl.GetErrorString(r));
   return DQ_E_HIP;
 }
@@ -88,7 +92,7 @@ int nccl_status(ncclResult_t r, const char* what) {
 }  // namespace dq
 
 struct dq_comm {
-  dq::ncclComm_t comm;
+  ncclComm_t comm;
   int32_t nranks, rank, device;
 };
 
@@ -131,21 +135,21 @@ int dq_comm_destroy(dq_comm* c) {
 int dq_comm_allreduce_mean(dq_comm* c, float* buf, int64_t n, void* stream) {
   DQ_CHECK_ARG(c && (buf || n == 0) && n >= 0, "dq_comm_allreduce_mean: bad argument");
   if (n == 0) return DQ_OK;
-  return nccl_status(g_rccl.AllReduce(buf, buf, (size_t)n, kNcclFloat32, kNcclAvg, c->comm,
+  return nccl_status(g_rccl.AllReduce(buf, buf, (size_t)n, ncclFloat32, ncclAvg, c->comm,
                                       (hipStream_t)stream), "ncclAllReduce");
 }
 
 int dq_comm_reduce_scatter_mean(dq_comm* c, float* buf, int64_t n_per_rank, void* stream) {
   DQ_CHECK_ARG(c && buf && n_per_rank > 0, "dq_comm_reduce_scatter_mean: bad argument");
   float* mine = buf + (int64_t)c->rank * n_per_rank;   // in place: recv = send + rank * count
-  return nccl_status(g_rccl.ReduceScatter(buf, mine, (size_t)n_per_rank, kNcclFloat32, kNcclAvg,
+  return nccl_status(g_rccl.ReduceScatter(buf, mine, (size_t)n_per_rank, ncclFloat32, ncclAvg,
                                           c->comm, (hipStream_t)stream), "ncclReduceScatter");
 }
 
 int dq_comm_all_gather(dq_comm* c, float* buf, int64_t n_per_rank, void* stream) {
   DQ_CHECK_ARG(c && buf && n_per_rank > 0, "dq_comm_all_gather: bad argument");
   const float* mine = buf + (int64_t)c->rank * n_per_rank;   // in place
-  return nccl_status(g_rccl.AllGather(mine, buf, (size_t)n_per_rank, kNcclFloat32, c->comm,
+  return nccl_status(g_rccl.AllGather(mine, buf, (size_t)n_per_rank, ncclFloat32, c->comm,
                                       (hipStream_t)stream), "ncclAllGather");
 }
 

@@ -413,9 +413,16 @@ __global__ __launch_bounds__(1024) void k_c51_online(C51Args a, LS ol, const flo
   }
 }
 
+// bytes the LDS-DMA of N rows x H floats writes: every wave instruction lands a whole 1 KB
+// (64 lanes x 16 B, the tail lanes re-reading in-bounds chunks), so the region is rounded up
+// to 1 KB -- the destination is not clamped, only the source
+static size_t c51_w2_lds_bytes(int N, int H) {
+  return ((size_t)N * H * sizeof(float) + 1023) / 1024 * 1024;
+}
+
 // dynamic LDS of k_c51 (bytes): the head, plus the W2 rows in the LDS-DMA form
 static size_t c51_lds(int A, int N, int H, int nw) {
-  return ((size_t)c51_head_floats(A, N, nw) + (size_t)N * H) * sizeof(float);
+  return (size_t)c51_head_floats(A, N, nw) * sizeof(float) + (H ? c51_w2_lds_bytes(N, H) : 0);
 }
 
 // mean(w * loss) for summaries (rb:298-301); launched only when requested.
@@ -768,6 +775,7 @@ int dq_c51_loss_fused(const float* online_parts, const float* online_bias,
   // d h split over S blocks per sample when the column slices stay whole 16-B chunks
   const int S = fc2_w && hidden % (4 * DQ_C51_SPLIT) == 0 ? DQ_C51_SPLIT : 1;
   const size_t shm = c51_lds(num_actions, num_atoms, fc2_w ? hidden / S : 0, waves);
+  DQ_CHECK_ARG(shm <= 160 * 1024, "num_atoms * hidden exceeds the LDS");
   static void (*const kerns[8])(C51Args, LogitsParts, LogitsParts, C51Extra) = {
       k_c51<LogitsParts, 0>, k_c51<LogitsParts, 1>, k_c51<LogitsParts, 2>, k_c51<LogitsParts, 3>,
       k_c51<LogitsParts, 4>, k_c51<LogitsParts, 5>, k_c51<LogitsParts, 6>, k_c51<LogitsParts, 7>};
@@ -794,8 +802,9 @@ int dq_c51_loss_online(const float* online_parts, const float* online_bias, int3
   C51Args a{nullptr, nullptr, actions, nullptr, nullptr, probs, nullptr, batch, num_actions,
             num_atoms, 0.0f, grad_logits, loss_out, priorities_out, nullptr};
   const int NO = num_actions * num_atoms;
-  const size_t shm = ((size_t)(num_atoms + 3) / 4 * 4 + (fc2_w ? (size_t)num_atoms * hidden : 0)) *
-                     sizeof(float);
+  const size_t shm = (size_t)(num_atoms + 3) / 4 * 4 * sizeof(float) +
+                     (fc2_w ? c51_w2_lds_bytes(num_atoms, hidden) : 0);
+  DQ_CHECK_ARG(shm <= 160 * 1024, "num_atoms * hidden exceeds the LDS");
   hipLaunchKernelGGL(k_c51_online<LogitsParts>, dim3(batch), dim3(512), shm, (hipStream_t)stream, a,
                      LogitsParts{online_parts, online_bias, (int64_t)batch * NO, n_parts, NO},
                      target_m, C51Extra{online_logits_out, nullptr, fc2_w, h, dh, hidden});

@@ -11,7 +11,6 @@ ranks' single-GPU gradients, not a single B*N batch.
 """
 import ctypes
 import os
-import time
 
 import torch
 import torch.distributed as dist
@@ -30,7 +29,16 @@ def allreduce_mean_(flat_grad, group=None):
   if dist.get_backend(group) == 'nccl':     # RCCL averages in the collective (no extra kernel)
     dist.all_reduce(flat_grad, op=dist.ReduceOp.AVG, group=group)
     return flat_grad
-  dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, group=group)
+  # gloo (the CPU tests and one-GPU rehearsals of N ranks): every rank's gradient gathered,
+  # summed in group-rank order, then scaled -- (((g0 + g1) + g2) + ...) * (1 / N) on every
+  # rank, a fixed order a single-process reference can restate bit for bit at any N
+  # (gloo's own all-reduce sums in a ring/chunk order that depends on N; with 2 ranks the
+  # two agree, a + b being commutative)
+  parts = [torch.empty_like(flat_grad) for _ in range(world)]
+  dist.all_gather(parts, flat_grad, group=group)
+  flat_grad.copy_(parts[0])
+  for p in parts[1:]:
+    flat_grad.add_(p)
   flat_grad.mul_(1.0 / world)
   return flat_grad
 
@@ -90,7 +98,12 @@ class RcclComm(object):
     # bucket's all-reduce, issued first on the comm stream, then started only after the conv
     # bucket's, ~45 us late (rocprof, profiles/r3_dist).  The two buckets' kernels are small
     # grids that fit on the GPU together, so no cross-communicator order is needed for progress.
-    # Read by this package's own RCCL instance (dlopened at its first call), not torch's.
+    # This package dlopens /opt/rocm/lib/librccl.so.1 by path: a second RCCL instance beside
+    # the torch/lib/librccl.so torch links (two mappings in /proc/self/maps,
+    # tests/test_cabi.py), with its own parameter cache, read at its first communicator init
+    # here.  The variable is process-wide, but torch's instance has created its
+    # communicators and run its first collectives (replica broadcast, the availability
+    # check) before this point, and it serves one communicator per process group.
     os.environ.setdefault('NCCL_LAUNCH_ORDER_IMPLICIT', '0')
     self._lib = _lib
     self.world = dist.get_world_size(group)
@@ -169,31 +182,39 @@ def replicas_in_sync(flat_params, group=None):
 _CAPTURABLE = {}
 
 
-def settle_watchdog():
-  """Before capturing torch.distributed collectives: torch's process-group watchdog polls
-  the events of the works it still holds (~every 100 ms) from its own thread; one held
-  when a capture started was seen queried as "recorded in a capturing stream", and the
-  watchdog aborted the process (ROCm 7.2, torch 2.10; one run in many, tests/test_gpu_rccl
-  capture probe).  The caller has synchronized the device; this lets the watchdog retire
-  the completed eager works first.  (The learner's own RCCL communicators, RcclComm, have
-  no watchdog.)"""
-  time.sleep(0.5)
+def forget_capture_probes(comms):
+  """Drops the cached probe results of a communicator pair about to be destroyed (the
+  cache is keyed by object identity, which a later pair may reuse)."""
+  ids = tuple(id(c) for c in comms)
+  for key in [k for k in _CAPTURABLE if k[3] == ids]:
+    del _CAPTURABLE[key]
 
 
 def collectives_capturable(group, device, stream=None, sharded=False, group2=None, comms=None):
-  """Whether every rank of ``group`` can capture this backend's all-reduce into a HIP
-  graph and replay it correctly -- probed once per group on a small tensor, the ranks
-  agreeing (eager MIN all-reduces) after each phase so no rank replays a collective the
-  others did not capture.  False for gloo (host-side collectives).  The learner loop
-  captures its all-reduces only where this holds, else it replays per-step graphs with
-  the collectives issued between them.  comms: a pair of RcclComm -- probe the learner's own
-  communicators (fc bucket on the comm stream, conv bucket on the origin) instead of
-  ``group`` / ``group2``'s torch collectives."""
+  """Whether every rank of ``group`` can capture the learner's collectives into a HIP
+  graph and replay them correctly -- probed once per communicator pair on a small tensor,
+  the ranks agreeing (eager MIN all-reduces) after each phase so no rank replays a
+  collective the others did not capture.  comms: the learner's RcclComm pair (fc bucket on
+  the comm stream, conv bucket on the origin).  False for gloo (host-side collectives) and
+  for torch.distributed's own collectives (comms None; see below).  The learner loop
+  captures its collectives only where this holds, else it replays per-step graphs with the
+  collectives issued between them.  (group2: accepted for the old call form; unused.)"""
   key = (id(group), bool(sharded), id(group2) if group2 is not None else None,
          None if comms is None else tuple(id(c) for c in comms))
   if key in _CAPTURABLE:
     return _CAPTURABLE[key]
-  if dist.get_backend(group) != 'nccl':
+  if dist.get_backend(group) != 'nccl' or comms is None:
+    # gloo: host-side collectives.  torch.distributed's RCCL collectives: never captured.
+    # ProcessGroupNCCL issues every collective on its internal stream S and its watchdog
+    # thread polls each work's end event, recorded on S, until it retires the work (~100 ms
+    # after completion).  A captured collective makes S a capturing stream, and HIP 7.2's
+    # hipEventQuery fails with hipErrorCapturedEvent for an event whose stream is capturing
+    # now, even one recorded eagerly before the capture (CUDA would report the eager record
+    # complete; tools/micro/event_query_capture.hip, DESIGN §6) -- the watchdog then
+    # aborts the process.  Whether an eager work is still on the watchdog's list when a
+    # capture starts is a race no caller can close, so only the learner's own
+    # communicators (RcclComm: no internal stream, no watchdog) are captured; with torch's
+    # the learner loop replays per-step graphs with the collectives issued between them.
     _CAPTURABLE[key] = False
     return False
 
@@ -217,22 +238,12 @@ def collectives_capturable(group, device, stream=None, sharded=False, group2=Non
     e.record(origin)
     comm.wait_event(e)
     with torch.cuda.stream(comm):
-      if comms is not None:
-        comms[0].allreduce_mean_(x)
-        if sharded:
-          comms[0].reduce_scatter_mean_(x)
-          comms[0].all_gather_(x)
-      else:
-        allreduce_mean_(x, group)
-        if sharded:
-          reduce_scatter_mean_(x, group)
-          all_gather_(x, group)
-    if comms is not None:
-      with torch.cuda.stream(origin):
-        comms[1].allreduce_mean_(y)
-    elif group2 is not None:
-      with torch.cuda.stream(origin):
-        allreduce_mean_(y, group2)
+      comms[0].allreduce_mean_(x)
+      if sharded:
+        comms[0].reduce_scatter_mean_(x)
+        comms[0].all_gather_(x)
+    with torch.cuda.stream(origin):
+      comms[1].allreduce_mean_(y)
     e = torch.cuda.Event()
     e.record(comm)
     origin.wait_event(e)
@@ -243,8 +254,6 @@ def collectives_capturable(group, device, stream=None, sharded=False, group2=Non
   # failure there is fatal on every rank instead of one rank leaving the others blocked
   collectives(torch.cuda.current_stream(device))
   torch.cuda.synchronize(device)
-  if comms is None:
-    settle_watchdog()
   try:
     cap.wait_stream(torch.cuda.current_stream(device))
     with torch.cuda.stream(cap):
@@ -261,8 +270,7 @@ def collectives_capturable(group, device, stream=None, sharded=False, group2=Non
       torch.cuda.synchronize(device)
       want = sum(range(1, world + 1)) / world if (world > 1 or FORCE_COLLECTIVES) else 1.0
       ok = bool(torch.allclose(x, torch.full_like(x, want)))
-      if group2 is not None or comms is not None:
-        ok = ok and bool(torch.allclose(y, torch.full_like(y, want)))
+      ok = ok and bool(torch.allclose(y, torch.full_like(y, want)))
     except Exception:                             # noqa: BLE001
       ok = False
     ok = agree(ok)

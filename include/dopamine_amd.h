@@ -392,7 +392,9 @@ typedef struct dq_adam_args {
                               parameters and moments come out bitwise the same); 0: write it */
 } dq_adam_args;
 /* backward + optimizer step in one pass (single-replica training: no gradient
-   all-reduce between them).  Gradients are still written to g. */
+   all-reduce between them).  Gradients are written to g unless opt->no_grad_store = 1, in
+   which case the updates fused into gradient epilogues consume them in registers and those
+   ranges of g are left unwritten (parameters and moments bitwise the same either way). */
 int dq_cnn_backward_adam(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch,
                          const float* x, const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d,
                          float* ws, const dq_adam_args* opt, void* stream);

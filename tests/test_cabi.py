@@ -88,3 +88,24 @@ def test_missing_library_fails_loudly(tmp_path, monkeypatch):
     importlib.reload(L)
   monkeypatch.undo()
   importlib.reload(L)
+
+
+def test_learner_rccl_is_a_separate_instance_of_the_header_version():
+  """RcclComm's RCCL (dlopened by path in comm.hip) is a second instance beside the one torch
+  links, so its parameters (NCCL_LAUNCH_ORDER_IMPLICIT, parallel.RcclComm) are its own
+  cache; and its version is the rccl.h comm.hip compiles against (major.minor)."""
+  code = r'''
+import torch, re
+from dopamine_amd import _lib
+v = int(_lib.lib.dq_comm_version())
+hdr = open('/opt/rocm/include/rccl/rccl.h').read()
+code = int(re.search(r'#define NCCL_VERSION_CODE (\d+)', hdr).group(1))
+assert v // 100 == code // 100, (v, code)
+maps = set(l.split()[-1] for l in open('/proc/self/maps') if 'librccl' in l)
+assert len(maps) == 2, maps
+print('ok')
+'''
+  if not os.path.exists('/opt/rocm/include/rccl/rccl.h'):
+    pytest.skip('no rccl.h')
+  out = subprocess.run(['python', '-c', code], cwd=ROOT, capture_output=True, text=True)
+  assert out.returncode == 0 and out.stdout.strip().endswith('ok'), out.stderr[-2000:]

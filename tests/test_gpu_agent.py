@@ -367,3 +367,7 @@ def test_fused_optimizer_without_gradient_stores_is_bitwise_the_same(kind):
   if kind == 'rainbow':
     np.testing.assert_array_equal(res[0][2], res[1][2])
   assert res[0][3] == res[1][3]
+  # the captured graphs bake the choice in: changing it afterwards is refused
+  with pytest.raises(RuntimeError, match='keep_gradients'):
+    a.keep_gradients = True
+  a.keep_gradients = False                   # unchanged: allowed

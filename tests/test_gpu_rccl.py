@@ -78,15 +78,22 @@ def test_rccl_one_rank_sharded_optimizer_equals_single_learner_bitwise(rccl_grou
 
 
 def test_collective_capture_probe(rccl_group):
-  """The probe that gates captured all-reduces in the learner loop says yes on RCCL."""
+  """The probe that gates captured all-reduces in the learner loop: yes for the learner's
+  own RCCL communicators, no for torch.distributed's collectives (their watchdog polls
+  events on the stream a capture would take over: parallel.collectives_capturable)."""
   from dopamine_amd import parallel
   parallel._CAPTURABLE.clear()
-  assert parallel.collectives_capturable(rccl_group, torch.device('cuda', 0))
-  assert parallel.collectives_capturable(rccl_group, torch.device('cuda', 0), sharded=True)
-  import torch.distributed as dist
-  second = dist.new_group(ranks=[0], backend='nccl')
-  assert parallel.collectives_capturable(rccl_group, torch.device('cuda', 0), sharded=True,
-                                         group2=second)
+  assert not parallel.collectives_capturable(rccl_group, torch.device('cuda', 0))
+  assert not parallel.collectives_capturable(rccl_group, torch.device('cuda', 0), sharded=True)
+  comms = (parallel.RcclComm(rccl_group, 'cuda:0'), parallel.RcclComm(rccl_group, 'cuda:0'))
+  try:
+    for sharded in (False, True):
+      assert parallel.collectives_capturable(rccl_group, torch.device('cuda', 0), sharded=sharded,
+                                             comms=comms)
+  finally:
+    parallel.forget_capture_probes(comms)
+    for c in comms:
+      c.destroy()
 
 
 def test_allreduce_mean_over_rccl_is_identity_for_one_rank(rccl_group):
@@ -110,6 +117,8 @@ def test_rccl_torch_collectives_schedule_equals_single_learner_bitwise(rccl_grou
   agent = _agent(rccl_group, 0, native_comm=False)
   assert agent._rccl is None
   flat = _run(agent, loop).numpy()
+  # never captured: per-step graphs with the collectives issued between them
+  assert not any(k[0] == 'chunk' for k in agent._graph_sets if isinstance(k, tuple))
   single = _run(_agent(None, 0), loop).numpy()
   assert np.array_equal(flat, single)
 
@@ -144,3 +153,8 @@ def test_native_comm_is_used_and_collectives_are_identity_for_one_rank(rccl_grou
   parallel._CAPTURABLE.clear()
   assert parallel.collectives_capturable(rccl_group, torch.device('cuda', 0), sharded=True,
                                          comms=agent._rccl)
+  # close(): the communicators destroyed, the graphs that captured them dropped
+  agent.close()
+  assert agent._rccl is None and not agent._graph_sets
+  with pytest.raises(RuntimeError, match='closed'):
+    agent.train_gradient_steps(1)

@@ -125,3 +125,44 @@ def test_reduce_scatter_and_all_gather_slices():
   for r in range(world):
     assert np.array_equal(res[r][0], mean[r * S:(r + 1) * S].numpy())
     assert np.array_equal(res[r][1], want.numpy())
+
+
+def _order_worker(rank, world, port, q):
+  os.environ['MASTER_ADDR'] = '127.0.0.1'
+  os.environ['MASTER_PORT'] = str(port)
+  dist.init_process_group('gloo', rank=rank, world_size=world)
+  from dopamine_amd import parallel
+  g = torch.from_numpy(np.random.RandomState(rank).standard_normal(4099).astype(np.float32) *
+                       np.float32(10.0 ** (rank - 2)))
+  parallel.allreduce_mean_(g)
+  q.put((rank, g.numpy().copy()))
+  dist.barrier()
+  dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_gloo_mean_is_the_rank_ordered_sum_bitwise():
+  """Over gloo (the multi-rank tests' backend) the mean is (((g0 + g1) + g2) + g3) * 1/4 on
+  every rank -- the order a single-process reference restates bit for bit at any world size
+  (tests/test_gpu_multirank.py's world-8 test depends on it)."""
+  world = 4
+  ctx = mp.get_context('spawn')
+  q = ctx.Queue()
+  port = _free_port()
+  procs = [ctx.Process(target=_order_worker, args=(r, world, port, q)) for r in range(world)]
+  for p in procs:
+    p.start()
+  res = dict(q.get(timeout=240) for _ in range(world))
+  for p in procs:
+    p.join(timeout=60)
+    assert p.exitcode == 0
+  gs = [np.random.RandomState(r).standard_normal(4099).astype(np.float32) *
+        np.float32(10.0 ** (r - 2)) for r in range(world)]
+  acc = gs[0].copy()
+  for g in gs[1:]:
+    acc = acc + g
+  want = acc * np.float32(1.0 / world)
+  for r in range(world):
+    assert np.array_equal(res[r], want)
+  other = ((gs[3] + gs[2]) + gs[1]) + gs[0]          # the order matters for these inputs
+  assert not np.array_equal(other * np.float32(1.0 / world), want)

@@ -1,18 +1,41 @@
-# A/B on one box: optional k_c51 stamps of a -DDQ_C51_PROF variant, chosen GPU tests, then
-# alternating bench runs of the in-tree library and the named variants.
-#   DQ_TAG=name DQ_TESTS="tests/a.py" DQ_STAMPS=ab/c51prof/libdopamine_amd.so \
-#   gpurun -- bash tools/gpu_ab.sh ab/base/libdopamine_amd.so ...
+# A/B of alternate builds on one box (tools/build_variant.py ab/<name>/libdopamine_amd.so):
+# chosen GPU tests on each build, then the bench (or CFG=iqn_breakout|dqn_pong through
+# tools/bench_configs.py) alternating in-tree / builds twice, then (DQ_TIMELINE=1) a rocprof
+# step timeline of each.
+#   DQ_TESTS="tests/test_gpu_cnn.py ..." CFG=rainbow DQ_TIMELINE=1 \
+#   gpurun -- bash tools/gpu_ab.sh <out-name> ab/X/libdopamine_amd.so ...
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-OUT=gpurun_out/${DQ_TAG:-ab}
+OUT=gpurun_out/${1:-ab}
+shift
 mkdir -p $OUT
-if [ -n "$DQ_STAMPS" ]; then
-  DOPAMINE_AMD_LIB=$DQ_STAMPS timeout -k 10 200 python -u tools/c51_stamps.py > $OUT/stamps.log 2>&1 || exit $?
-  tail -12 $OUT/stamps.log
-fi
 if [ -n "$DQ_TESTS" ]; then
-  timeout -k 10 600 python -u -m pytest $DQ_TESTS -m gpu -x -v --timeout 240 --timeout-method thread > $OUT/tests.log 2>&1
-  rc=$?; tail -2 $OUT/tests.log; grep FAILED $OUT/tests.log | head; [ $rc -eq 0 ] || exit $rc
+  for lib in "$@"; do
+    n=$(basename $(dirname $lib))
+    DOPAMINE_AMD_LIB=$lib timeout -k 10 600 python -u -m pytest $DQ_TESTS -m gpu -v \
+      --timeout 300 --timeout-method thread > $OUT/tests_$n.log 2>&1
+    rc=$?; echo "[$n] tests rc=$rc"; tail -1 $OUT/tests_$n.log; grep FAILED $OUT/tests_$n.log | head
+    if [ $rc -ne 0 ]; then exit $rc; fi
+  done
 fi
-bash tools/ab_lib.sh "$@" 2>&1 | tee $OUT/ab.log
+for rep in 1 2; do
+  for lib in "" "$@"; do
+    if [ "${CFG:-rainbow}" = rainbow ]; then
+      line=$(DOPAMINE_AMD_LIB=$lib timeout -k 10 240 python bench.py --steps ${STEPS:-2000} --skip-cpu-baseline --skip-configs --gather-iters 20 2>>$OUT/err.log | tail -1) || exit 1
+      v=$(echo "$line" | python3 -c 'import sys,json; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')
+    else
+      v=$(DOPAMINE_AMD_LIB=$lib timeout -k 10 240 python tools/bench_configs.py ${STEPS:-300} $CFG 2>>$OUT/err.log | tail -1) || exit 1
+    fi
+    echo "[${lib:-in-tree}] $v" | tee -a $OUT/ab.log
+  done
+done
+if [ -n "$DQ_TIMELINE" ]; then
+  for lib in "" "$@"; do
+    n=$(basename $(dirname ${lib:-in-tree/x}))
+    DOPAMINE_AMD_LIB=$lib timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/r_$n -o run -- python3 bench.py --skip-cpu-baseline --skip-configs --gather-iters 20 > $OUT/prof_$n.log 2>&1 || exit 1
+    python3 tools/step_timeline_db.py /tmp/r_$n/run_results.db k_c51 30 > $OUT/timeline_$n.txt
+    python3 tools/prof_summary.py /tmp/r_$n/run_results.db 30 > $OUT/kernels_$n.txt
+    head -16 $OUT/timeline_$n.txt
+  done
+fi
