@@ -326,6 +326,11 @@ struct Fc1EpiOpt<2> {       // centered RMSProp (DQN, config 2): DQ_FC1_EPI_RMS
 #define DQ_FC1_EPI_RMS 1
 #endif
 
+// timing experiments only (DQ_ABL_*): the GEMM's result is dropped
+struct EpiNone {
+  __device__ __forceinline__ void operator()(int, int, float, int) const {}
+};
+
 // A recorded replay operation (replay_dev.h) riding in a grouped launch: its
 // blocks come first in the launch so the single-wave sum-tree update / sampler
 // chains start before the GEMM blocks fill the machine.
@@ -807,6 +812,27 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
             GE::make(g->conv2_w, g->conv2_b, Conv2::K, p->conv2_w, p->conv2_b, opt, 0)};
         if (in(0)) group_r(c, rd(0), dX_fc2);
         if (in(1)) group_r(c, rd(1), dW_fc2, dX_fc1);
+#ifndef DQ_ABL_B2
+#define DQ_ABL_B2 0
+#endif
+        // DQ_ABL_B2 (timing experiments only, tools/build_variant.py; results are wrong):
+        // launch 2 without  1: its rider  2: fc1's Adam epilogue (the GEMM, no stores)
+        // 4: dX conv3  8: fc2's Adam part
+        if constexpr (DQ_ABL_B2 != 0) {
+          if (in(2)) {
+            auto dW_none = gemm_op<4, 4, 1>(ColK{d->h, kHidden}, ColKOnes{a->a3, kFlat},
+                                            EpiNone{}, kHidden, kFlat + 1, B, B);
+            const RiderDesc* r2 = (DQ_ABL_B2 & 1) ? nullptr : rd(2);
+            auto fc2p = part(p->fc2_w, (DQ_ABL_B2 & 8) ? p->fc2_w + 4 : p->fc2_b + NO);
+            auto x3 = dX_c3;
+            if (DQ_ABL_B2 & 4) x3.gx = x3.gy = x3.gz = 0;
+            if (DQ_ABL_B2 & 2) {
+              group_r(c, r2, dW_none, x3, fc2p);
+            } else {
+              group_r(c, r2, dW_fc1a, x3, fc2p);
+            }
+          }
+        } else
         if (in(2)) group_r(c, rd(2), dW_fc1a, dX_c3, part(p->fc2_w, p->fc2_b + NO));
         if (kHeadFrom == 6) {
           if (in(3)) group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11, dW_c2);

@@ -205,16 +205,18 @@ def collectives_capturable(group, device, stream=None, sharded=False, group2=Non
     return _CAPTURABLE[key]
   if dist.get_backend(group) != 'nccl' or comms is None:
     # gloo: host-side collectives.  torch.distributed's RCCL collectives: never captured.
-    # ProcessGroupNCCL issues every collective on its internal stream S and its watchdog
-    # thread polls each work's end event, recorded on S, until it retires the work (~100 ms
-    # after completion).  A captured collective makes S a capturing stream, and HIP 7.2's
-    # hipEventQuery fails with hipErrorCapturedEvent for an event whose stream is capturing
-    # now, even one recorded eagerly before the capture (CUDA would report the eager record
-    # complete; tools/micro/event_query_capture.hip) -- the watchdog then
-    # aborts the process.  Whether an eager work is still on the watchdog's list when a
-    # capture starts is a race no caller can close, so only the learner's own
-    # communicators (RcclComm: no internal stream, no watchdog) are captured; with torch's
-    # the learner loop replays per-step graphs with the collectives issued between them.
+    # Capturing them once aborted the process from torch's process-group watchdog (round 3;
+    # ROCm 7.2, torch 2.10), which keeps every eager work on a list and polls its events from
+    # its own thread until it retires it.  Measured on HIP 7.2 (tools/micro/
+    # event_query_capture.hip, profiles/r4_dist/event_query_capture.log): a thread-local
+    # capture fails -- hipErrorStreamCaptureUnsupported, and the capture is invalidated --
+    # on ANY hipEventQuery made by the capturing thread, while queries from other threads
+    # return success even for events recorded inside the capture.  So whether a capture
+    # survives depends on what torch's collective path and its watchdog do with their event
+    # lists at that moment -- state this package cannot see or wait on (a sleep only made
+    # the race rarer).  Only the learner's own communicators (RcclComm: no internal
+    # stream, no work list, no watchdog) are captured; with torch's collectives the learner
+    # loop replays per-step graphs with the collectives issued between them.
     _CAPTURABLE[key] = False
     return False
 

@@ -1,7 +1,7 @@
 # A/B of alternate builds on one box (tools/build_variant.py ab/<name>/libdopamine_amd.so):
 # chosen GPU tests on each build, then the bench (or CFG=iqn_breakout|dqn_pong through
 # tools/bench_configs.py) alternating in-tree / builds twice, then (DQ_TIMELINE=1) a rocprof
-# step timeline of each.
+# step timeline of each (DQ_NOAB=1: the timelines only).
 #   DQ_TESTS="tests/test_gpu_cnn.py ..." CFG=rainbow DQ_TIMELINE=1 \
 #   gpurun -- bash tools/gpu_ab.sh <out-name> ab/X/libdopamine_amd.so ...
 set -o pipefail
@@ -19,7 +19,7 @@ if [ -n "$DQ_TESTS" ]; then
     if [ $rc -ne 0 ]; then exit $rc; fi
   done
 fi
-for rep in 1 2; do
+for rep in $([ -z "$DQ_NOAB" ] && echo 1 2); do
   for lib in "" "$@"; do
     if [ "${CFG:-rainbow}" = rainbow ]; then
       line=$(DOPAMINE_AMD_LIB=$lib timeout -k 10 240 python bench.py --steps ${STEPS:-2000} --skip-cpu-baseline --skip-configs --gather-iters 20 2>>$OUT/err.log | tail -1) || exit 1
