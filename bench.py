@@ -63,9 +63,15 @@ def parse():
   ap.add_argument('--branch-first', action='store_true',
                   help='N > 1: capture the fc bucket\'s branch before the backward tail '
                        '(DQNAgent.branch_first; a schedule experiment)')
+  ap.add_argument('--sample-launch', type=int, default=None,
+                  help='override DQNAgent.sample_launch (2/3): the backward launch the PER '
+                       'sample rides in (a schedule experiment)')
   ap.add_argument('--comm', choices=('native', 'torch'), default='native',
                   help='N > 1 over RCCL: the learner\'s own communicators (parallel.RcclComm) '
                        'or torch.distributed\'s collectives')
+  ap.add_argument('--skip-bf16', action='store_true',
+                  help='do not time the separate bf16 throughput row (N = 1)')
+  ap.add_argument('--bf16-child', action='store_true', help=argparse.SUPPRESS)
   ap.add_argument('--force-dist', action='store_true',
                   help='one rank only: run the N > 1 learner schedule over a one-rank RCCL group '
                        'with every collective executed (a hardware check of the data-parallel '
@@ -318,6 +324,63 @@ def step_mfma(actions, batch, sec_per_step):
           'unit': 'TFLOP/s', 'frac': round(achieved / FP32_MFMA_PEAK_TFLOPS, 4)}
 
 
+def bf16_child(args):
+  """In a child process on the bf16 build (DOPAMINE_AMD_LIB = the bf16 library): the
+  headline's Rainbow agent and config 5's IQN, same protocol; one JSON line."""
+  dev = torch.device('cuda', 0)
+  torch.cuda.set_device(0)
+  from dopamine_amd import _lib
+  res = {'library': os.path.relpath(_lib.LIB_PATH, ROOT)}
+  import random
+  for name, make, A, n in (
+      ('rainbow', lambda: build_agent(args.actions, args.capacity, args.batch, dev), args.actions,
+       args.steps),
+      ('iqn_breakout', lambda: build_iqn_breakout(dev), 4, max(args.steps // 3, 50))):
+    agent = make()
+    random.seed(0)
+    fill_synthetic(agent._replay.memory, A, seed=1)
+    torch.cuda.synchronize()
+    elapsed, _ = timed_steps(agent, n, 10 if name != 'rainbow' else args.warmup)
+    agent._replay.memory.sync_rng()
+    loss = agent.mean_loss()
+    res[name] = {'value': round(n / elapsed, 2), 'unit': 'gradient-steps/s', 'steps': n,
+                 'ms_per_step': round(1e3 * elapsed / n, 4), 'final_mean_loss': round(loss, 5),
+                 'finite': bool(np.isfinite(loss))}
+    del agent
+    gc.collect()
+    torch.cuda.empty_cache()
+  print(json.dumps(res), flush=True)
+
+
+def bf16_throughput(args):
+  """BASELINE.md §4's separate throughput row, timed by the driver's run of this script:
+  the same agents on the bf16 build (dopamine_amd/libdopamine_amd_bf16.so, built by
+  __graft_entry__.build()), in a child process after this one has released the GPU.
+  NOT the headline and NOT fp32 parity: one bf16 product per MFMA (fp32 accumulate)
+  fails the 1e-5 tests by construction."""
+  import subprocess
+  from dopamine_amd import _build
+  base = {'dtype': 'bf16 (fp32 accumulate)',
+          'parity': 'fails the fp32 1e-5 parity tests by construction; a throughput row '
+                    'beside the fp32 headline, not a supported mode',
+          'gemm_form': 'one v_mfma_f32_32x32x16_bf16 product (hi.hi) in every Nature-CNN '
+                       'wave-private tile and the IQN heads\' split GEMMs '
+                       '(-DDQ_CNN_X6=1 -DDQ_X6_PAIRS=1)'}
+  if not os.path.exists(_build.BF16_LIB_PATH):
+    return dict(base, error='bf16 library not built (__graft_entry__.build())')
+  env = dict(os.environ, DOPAMINE_AMD_LIB=_build.BF16_LIB_PATH)
+  cmd = [sys.executable, os.path.abspath(__file__), '--bf16-child', '--steps', str(args.steps),
+         '--warmup', str(args.warmup), '--capacity', str(args.capacity), '--batch',
+         str(args.batch), '--actions', str(args.actions)]
+  try:
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    line = out.stdout.strip().splitlines()[-1] if out.stdout.strip() else ''
+    return dict(base, **json.loads(line)) if out.returncode == 0 else dict(
+        base, error='child rc %d: %s' % (out.returncode, out.stderr[-500:]))
+  except (subprocess.TimeoutExpired, ValueError, IndexError) as e:
+    return dict(base, error=repr(e)[:500])
+
+
 def host_cores():
   """CPUs this process may run on: the affinity mask, capped by a cgroup CPU quota."""
   n = len(os.sched_getaffinity(0))
@@ -355,6 +418,8 @@ def cpu_baseline(seconds, A, batch):
 
 def main():
   args = parse()
+  if args.bf16_child:
+    return bf16_child(args)
   world = int(os.environ.get('WORLD_SIZE', '1'))
   rank = int(os.environ.get('RANK', '0'))
   local = int(os.environ.get('LOCAL_RANK', '0'))
@@ -383,6 +448,9 @@ def main():
   if args.branch_first:
     from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
     DQNAgent.branch_first = True
+  if args.sample_launch is not None:
+    from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
+    DQNAgent.sample_launch = int(args.sample_launch)
   if args.split_c51 is not None:
     from dopamine_amd.agents.rainbow.rainbow_agent import RainbowAgent
     RainbowAgent.split_c51 = bool(args.split_c51)
@@ -442,6 +510,14 @@ def main():
     torch.cuda.empty_cache()
     configs = other_configs(dev, args.steps)
 
+  bf16 = None
+  if rank == 0 and world == 1 and not args.force_dist and not args.skip_bf16:
+    agent = None
+    gc.collect()
+    torch.cuda.empty_cache()
+    torch.cuda.synchronize()
+    bf16 = bf16_throughput(args)
+
   cpu = None
   if rank == 0 and world == 1 and not args.skip_cpu_baseline:
     cpu = cpu_baseline(args.cpu_seconds, args.actions, args.batch)
@@ -479,6 +555,8 @@ def main():
         'schedules': schedules if pg is not None else None,
         # supplementary: BASELINE configs 2 and 5 (N = 1), same protocol, not the metric
         'other_configs': configs,
+        # BASELINE.md §4's separate bf16 row (N = 1): NOT fp32 parity, not the headline
+        'throughput_mode': bf16,
     }
     print(json.dumps(line), flush=True)
   if pg is not None:

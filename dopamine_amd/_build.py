@@ -10,12 +10,23 @@ HEADER = os.path.join(os.path.dirname(_HERE), 'include', 'dopamine_amd.h')
 ARCH = os.environ.get('DQ_OFFLOAD_ARCH', 'gfx950')
 
 
-def build(verbose=False, out=None, sources=None):
+# The bf16 throughput build (BASELINE.md §4's separate row; NOT fp32 parity): the same
+# sources with every Nature-CNN wave-private tile and the IQN heads' split GEMMs on ONE bf16
+# product (hi.hi, fp32 accumulate) -- bench.py times it beside the fp32 headline.
+BF16_LIB_PATH = os.path.join(_HERE, 'libdopamine_amd_bf16.so')
+BF16_FLAGS = ['-DDQ_CNN_X6=1', '-DDQ_X6_PAIRS=1']
+
+
+def build_bf16(verbose=False):
+  return build(verbose=verbose, out=BF16_LIB_PATH, extra=BF16_FLAGS)
+
+
+def build(verbose=False, out=None, sources=None, extra=()):
   """Compile the HIP sources into libdopamine_amd.so next to this file: one hipcc per
   translation unit, in parallel, then one link."""
   out = out or LIB_PATH
   flags = ['--offload-arch=' + ARCH, '-O3', '-fPIC', '-std=c++17', '-ffp-contract=off', '-Wall',
-           '-I', os.path.join(_HERE, 'csrc')]
+           '-I', os.path.join(_HERE, 'csrc')] + list(extra)
   objs, procs = [], []
   bdir = os.path.join(_HERE, 'build')
   os.makedirs(bdir, exist_ok=True)
@@ -44,3 +55,4 @@ def build(verbose=False, out=None, sources=None):
 
 if __name__ == '__main__':
   build(verbose=True)
+  build_bf16(verbose=True)

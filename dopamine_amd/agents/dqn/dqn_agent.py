@@ -456,9 +456,14 @@ class DQNAgent(object):
     if self._gather_plan is not None and len(riders) == 2 and self.chunk_gather_launch > 2:
       empty = [_lib.Rider() for _ in range(self.chunk_gather_launch - 2)]
       return riders[:1] + empty + riders[1:]
+    if len(riders) == 3 and self.sample_launch > 2:   # PER: write-back, sample, gather
+      return riders[:1] + [_lib.Rider() for _ in range(self.sample_launch - 2)] + riders[1:]
     return riders
 
   chunk_gather_launch = 3
+  # the backward launch the PER sample rides in (the gather in the next one; the target
+  # head, from launch 5 on, needs the gathered batch): 2, or 3 (a schedule experiment)
+  sample_launch = 2
 
   def _forward_fused_c51(self, c, part=None):
     raise NotImplementedError

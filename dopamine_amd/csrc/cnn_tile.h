@@ -1178,6 +1178,39 @@ __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& 
     if constexpr (HasVecPre<EP>::value) {
       const int c = 4 * (lane & 7), n = n0 + wn * 32 + c;
       auto mrow = [&](int it) { return m0 + wm * 32 + 8 * it + (lane >> 3); };
+#ifndef DQ_VEC_DEPTH
+#define DQ_VEC_DEPTH 1
+#endif
+      if constexpr (DQ_VEC_DEPTH >= 3) {
+        // every row group's parameter / moment loads in flight before the first update
+        typename EP::VPre p[4];
+#pragma unroll
+        for (int it = 0; it < 4; ++it) p[it] = E.vpre(min(mrow(it), M - 1), n);
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+          const float* q = W + (8 * it + (lane >> 3)) * 33 + c;
+          const int m = mrow(it);
+          if (m < M && n < N) E.vcommit(m, n, make_float4(q[0], q[1], q[2], q[3]), p[it]);
+        }
+        return;
+      }
+      if constexpr (DQ_VEC_DEPTH == 2) {
+        // three row groups' loads in flight, the fourth issued after the first update
+        typename EP::VPre p0 = E.vpre(min(mrow(0), M - 1), n);
+        typename EP::VPre p1 = E.vpre(min(mrow(1), M - 1), n);
+        typename EP::VPre p2 = E.vpre(min(mrow(2), M - 1), n);
+        auto commit = [&](int it, const typename EP::VPre& pp) {
+          const float* q = W + (8 * it + (lane >> 3)) * 33 + c;
+          const int m = mrow(it);
+          if (m < M && n < N) E.vcommit(m, n, make_float4(q[0], q[1], q[2], q[3]), pp);
+        };
+        commit(0, p0);
+        p0 = E.vpre(min(mrow(3), M - 1), n);
+        commit(1, p1);
+        commit(2, p2);
+        commit(3, p0);
+        return;
+      }
       typename EP::VPre p = E.vpre(min(mrow(0), M - 1), n);
 #pragma unroll
       for (int it = 0; it < 4; ++it) {

@@ -832,11 +832,25 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
               group_r(c, r2, dW_fc1a, x3, fc2p);
             }
           }
-        } else
-        if (in(2)) group_r(c, rd(2), dW_fc1a, dX_c3, part(p->fc2_w, p->fc2_b + NO));
+        } else if (in(2)) {
+#ifndef DQ_FC2_OPT_LAUNCH
+#define DQ_FC2_OPT_LAUNCH 2
+#endif
+          // fc2's optimizer part: launch 2 (its gradient is final after launch 1), or 4
+          // (launch 2 holds the fc1 update's stream; nothing reads fc2_w before the next C)
+          if (DQ_FC2_OPT_LAUNCH == 2 || kHeadFrom != 6)
+            group_r(c, rd(2), dW_fc1a, dX_c3, part(p->fc2_w, p->fc2_b + NO));
+          else
+            group_r(c, rd(2), dW_fc1a, dX_c3);
+        }
         if (kHeadFrom == 6) {
           if (in(3)) group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11, dW_c2);
-          if (in(4)) group_r(c, rd(4), sum_c3, dW_c1);
+          if (in(4)) {
+            if (DQ_FC2_OPT_LAUNCH == 4)
+              group_r(c, rd(4), sum_c3, dW_c1, part(p->fc2_w, p->fc2_b + NO));
+            else
+              group_r(c, rd(4), sum_c3, dW_c1);
+          }
           if (in(5)) {
             if (head)
               group_r(c, rd(5), sum_c2a, sum_c1, part(p->conv3_w, p->fc1_w), head->conv1());

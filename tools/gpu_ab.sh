@@ -2,8 +2,9 @@
 # chosen GPU tests on each build, then the bench (or CFG=iqn_breakout|dqn_pong through
 # tools/bench_configs.py) alternating in-tree / builds twice, then (DQ_TIMELINE=1) a rocprof
 # step timeline of each (DQ_NOAB=1: the timelines only).
-#   DQ_TESTS="tests/test_gpu_cnn.py ..." CFG=rainbow DQ_TIMELINE=1 \
-#   gpurun -- bash tools/gpu_ab.sh <out-name> ab/X/libdopamine_amd.so ...
+#   gpurun -- 'DQ_TESTS="tests/test_gpu_cnn.py ..." CFG=rainbow DQ_TIMELINE=1 \
+#     bash tools/gpu_ab.sh <out-name> ab/X/libdopamine_amd.so "args:--split-c51 1" ...'
+# (the environment is set inside the gpurun command: gpurun does not forward it)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -20,20 +21,23 @@ if [ -n "$DQ_TESTS" ]; then
   done
 fi
 for rep in $([ -z "$DQ_NOAB" ] && echo 1 2); do
-  for lib in "" "$@"; do
+  for spec in "" "$@"; do
+    # a build (ab/X/libdopamine_amd.so) or "args:<bench flags>" on the in-tree build
+    lib=$spec; extra=
+    case "$spec" in args:*) lib=; extra=${spec#args:};; esac
     if [ "${CFG:-rainbow}" = rainbow ]; then
-      line=$(DOPAMINE_AMD_LIB=$lib timeout -k 10 240 python bench.py --steps ${STEPS:-2000} --skip-cpu-baseline --skip-configs --gather-iters 20 2>>$OUT/err.log | tail -1) || exit 1
+      line=$(DOPAMINE_AMD_LIB=$lib timeout -k 10 240 python bench.py --steps ${STEPS:-2000} --skip-cpu-baseline --skip-bf16 --skip-configs --gather-iters 20 $extra 2>>$OUT/err.log | tail -1) || exit 1
       v=$(echo "$line" | python3 -c 'import sys,json; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')
     else
       v=$(DOPAMINE_AMD_LIB=$lib timeout -k 10 240 python tools/bench_configs.py ${STEPS:-300} $CFG 2>>$OUT/err.log | tail -1) || exit 1
     fi
-    echo "[${lib:-in-tree}] $v" | tee -a $OUT/ab.log
+    echo "[${spec:-in-tree}] $v" | tee -a $OUT/ab.log
   done
 done
 if [ -n "$DQ_TIMELINE" ]; then
   for lib in "" "$@"; do
     n=$(basename $(dirname ${lib:-in-tree/x}))
-    DOPAMINE_AMD_LIB=$lib timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/r_$n -o run -- python3 bench.py --skip-cpu-baseline --skip-configs --gather-iters 20 > $OUT/prof_$n.log 2>&1 || exit 1
+    DOPAMINE_AMD_LIB=$lib timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/r_$n -o run -- python3 bench.py --skip-cpu-baseline --skip-bf16 --skip-configs --gather-iters 20 > $OUT/prof_$n.log 2>&1 || exit 1
     python3 tools/step_timeline_db.py /tmp/r_$n/run_results.db k_c51 30 > $OUT/timeline_$n.txt
     python3 tools/prof_summary.py /tmp/r_$n/run_results.db 30 > $OUT/kernels_$n.txt
     head -16 $OUT/timeline_$n.txt

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/${1:-roofline}
 shift
 mkdir -p $OUT
-ARGS="--skip-cpu-baseline --skip-configs --gather-iters 20 $*"
+ARGS="--skip-cpu-baseline --skip-bf16 --skip-configs --gather-iters 20 $*"
 timeout -k 10 300 rocprofv3 --kernel-trace -d /tmp/rt -o run -- python3 bench.py $ARGS > $OUT/trace.log 2>&1 || exit 1
 timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE -d /tmp/rf -o run --output-format csv -- python3 bench.py $ARGS --steps 120 --no-graph > $OUT/fetch.log 2>&1 || exit 1
 timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE -d /tmp/rw -o run --output-format csv -- python3 bench.py $ARGS --steps 120 --no-graph > $OUT/write.log 2>&1 || exit 1

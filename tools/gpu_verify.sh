@@ -15,6 +15,7 @@ if [ "${2:-tests}" = tests ]; then
   timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit $?
 fi
 timeout -k 10 400 python -u bench.py > $OUT/bench.log 2>&1 && tail -1 $OUT/bench.log && \
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d /tmp/prof -o run -- python3 bench.py --skip-cpu-baseline > $OUT/prof.log 2>&1 && \
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d /tmp/prof -o run -- python3 bench.py --skip-cpu-baseline --skip-bf16 > $OUT/prof.log 2>&1 && \
 python3 tools/prof_summary.py /tmp/prof/run_results.db 30 > $OUT/kernel_summary.txt && \
-python3 tools/step_timeline_db.py /tmp/prof/run_results.db k_c51 30 > $OUT/step_timeline.txt
+python3 tools/step_timeline_db.py /tmp/prof/run_results.db k_c51 30 > $OUT/step_timeline.txt && \
+python3 tools/gather_launches.py /tmp/prof/run_results.db 400 32 $OUT/prof.log > $OUT/gather_launches.txt
