@@ -66,6 +66,9 @@ def parse():
   ap.add_argument('--sample-launch', type=int, default=None,
                   help='override DQNAgent.sample_launch (2/3): the backward launch the PER '
                        'sample rides in (a schedule experiment)')
+  ap.add_argument('--comm-priority', type=int, default=None,
+                  help='override DQNAgent.comm_priority (0 / -1): the N > 1 comm stream\'s HIP '
+                       'priority (a schedule experiment)')
   ap.add_argument('--comm', choices=('native', 'torch'), default='native',
                   help='N > 1 over RCCL: the learner\'s own communicators (parallel.RcclComm) '
                        'or torch.distributed\'s collectives')
@@ -448,6 +451,9 @@ def main():
   if args.branch_first:
     from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
     DQNAgent.branch_first = True
+  if args.comm_priority is not None:
+    from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
+    DQNAgent.comm_priority = int(args.comm_priority)
   if args.sample_launch is not None:
     from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
     DQNAgent.sample_launch = int(args.sample_launch)

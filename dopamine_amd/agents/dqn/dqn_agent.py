@@ -170,7 +170,9 @@ class DQNAgent(object):
       self._opt = self.optimizer.build(self.online_convnet.fp.flat,
                                        segments=self.online_convnet.fp.segments())
       self._side = torch.cuda.Stream(self._device, priority=self.side_priority)
-      self._comm = torch.cuda.Stream(self._device)        # N > 1: the fc bucket's all-reduces
+      # N > 1: the fc bucket's all-reduces (comm_priority -1: a high-priority queue, whose
+      # workgroups are dispatched ahead of the main queue's pending ones)
+      self._comm = torch.cuda.Stream(self._device, priority=self.comm_priority)
       self._comm_opt = torch.cuda.Stream(self._device)    # ... and the Adam parts behind them
       if self._pg is not None:
         self._broadcast_replica()
@@ -701,6 +703,8 @@ class DQNAgent(object):
       raise RuntimeError('keep_gradients must be set before the first captured gradient step '
                          '(the HIP graphs already captured bake in the gradient stores)')
     self._keep_gradients = value
+  # HIP stream priority of the N > 1 comm stream (0 normal, -1 high)
+  comm_priority = 0
   # HIP stream priority of the prefetch stream (the pipelined non-rider schedule, e.g. IQN's
   # target network beside the online backward): 0 normal, -1 high
   side_priority = 0

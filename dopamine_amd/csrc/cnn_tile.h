@@ -417,6 +417,14 @@ struct EpiGradAdamVec {
     }
   }
   __device__ __forceinline__ void operator()(int m, int n, float g, int) const { scalar(m, n, g); }
+  // the same epilogue over rows [r0, ...) of the weight (a row range of the GEMM)
+  EpiGradAdamVec rows_from(int r0) const {
+    EpiGradAdamVec e = *this;
+    const int64_t o = (int64_t)r0 * nw;
+    e.gw += o; e.w += o; e.mw += o; e.vw += o;
+    e.gb += r0; e.b += r0; e.mb += r0; e.vb += r0;
+    return e;
+  }
 #ifndef DQ_VEC_PRE
 #define DQ_VEC_PRE 1
 #endif
@@ -528,6 +536,13 @@ struct EpiGradRmsVec {
   EpiGradRms s;            // the scalar form: pointers, constants, the bias column
   static constexpr bool kVec = true;
   static constexpr bool kVecPre = true;
+  EpiGradRmsVec rows_from(int r0) const {
+    EpiGradRmsVec e = *this;
+    const int64_t o = (int64_t)r0 * s.nw;
+    e.s.gw += o; e.s.w += o; e.s.mw += o; e.s.vw += o; e.s.gw2 += o;
+    e.s.gb += r0; e.s.b += r0; e.s.mb += r0; e.s.vb += r0; e.s.gb2 += r0;
+    return e;
+  }
   struct VPre {
     float4 w, m, v, g2;
   };
@@ -902,7 +917,7 @@ using X6Of = typename std::conditional<kFast, X6Img<ROWS, BKT>, X6ImgT<ROWS, BKT
 template <int WM, int WN, int WK, class AL, class BL, class EP, bool kLate = true, bool kX6 = false>
 __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& E, int M, int N,
                                             int K, int kchunk, int bx, int by, int bz,
-                                            float* smem) {
+                                            float* smem, int tid_base = 0) {
 #ifdef DQ_ABLATE_ALL      // timing experiments only: the launch floor of these grids
   if (M > 0) return;
 #endif
@@ -915,7 +930,8 @@ __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& 
   float* As = smem;
   float* Bs = smem + BKT * SA;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // tid_base: the tile's first thread (several tiles sharing a block, PairOp)
+  const int tid = (int)threadIdx.x - tid_base, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = (wave / WM) % WN, wk = wave / (WM * WN);
   const int m0 = bx * BM, n0 = by * BN;
   const int kbeg = bz * kchunk;

@@ -891,7 +891,11 @@ int dq_adam_tf1_part(float* var, const float* grad, float* m, float* v, float* s
   DQ_CHECK_ARG(var && grad && m && v && state && n >= 0 && (slot == 0 || slot == 1), "bad arguments");
   DQ_CHECK_ARG(((uintptr_t)var | (uintptr_t)grad | (uintptr_t)m | (uintptr_t)v) % 16 == 0,
                "adam buffers must be 16-byte aligned");
-  hipLaunchKernelGGL(k_adam_part, dim3(elementwise_grid(n)), dim3(256), 0, (hipStream_t)stream,
+#ifndef DQ_ADAM_PART_MAXB
+#define DQ_ADAM_PART_MAXB 2048   // N > 1's fc update beside the main queue: a cap leaves it CUs
+#endif
+  hipLaunchKernelGGL(k_adam_part, dim3(std::min(elementwise_grid(n), DQ_ADAM_PART_MAXB)), dim3(256), 0,
+                     (hipStream_t)stream,
                      var, grad, m, v, state, slot, n, lr, beta1, beta2, eps, bump);
   DQ_CHECK_LAUNCH("k_adam_part");
   return DQ_OK;

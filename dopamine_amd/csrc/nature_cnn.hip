@@ -54,13 +54,33 @@ struct GemmOp {
   BL b;
   EP e;
   int M, N, K, kchunk, gx, gy, gz;
-  __device__ __forceinline__ void run(int blk, float* smem) const {
+  __device__ __forceinline__ void run(int blk, float* smem, int tid_base = 0) const {
     const int bx = blk % gx, by = (blk / gx) % gy, bz = blk / (gx * gy);
     igemm_block<WM, WN, WK, AL, BL, EP, kLate, cnn_x6<WM, WN, WK, AL>()>(a, b, e, M, N, K, kchunk,
-                                                                      bx, by, bz, smem);
+                                                                      bx, by, bz, smem, tid_base);
   }
-  int blocks() const { return gx * gy * gz; }
+  __host__ __device__ int blocks() const { return gx * gy * gz; }
 };
+
+// Two tiles of a GemmOp per block (threads [0, kT) and [kT, 2 kT), LDS halves): an 8-wave
+// op in a launch of 16-wave blocks then fills its slots instead of leaving half of each
+// block's waves idle.  With an odd tile count the last block's second half recomputes the
+// last tile (pure-store epilogues only: the same bits stored twice).
+template <class Op>
+struct PairOp {
+  static constexpr int kT = 2 * Op::kT;
+  static constexpr int kLds = 2 * Op::kLds;
+  static constexpr bool kLateFetch = Op::kLateFetch;
+  Op op;
+  __device__ __forceinline__ void run(int blk, float* smem) const {
+    const int half = (int)threadIdx.x >= Op::kT ? 1 : 0;
+    op.run(min(2 * blk + half, op.blocks() - 1), smem + half * Op::kLds, half * Op::kT);
+  }
+  int blocks() const { return (op.blocks() + 1) / 2; }
+};
+#ifndef DQ_SP_PAIR
+#define DQ_SP_PAIR 0
+#endif
 
 template <class EP, int T = kGroupT>
 struct ReduceOp {                 // ordered split-K sum of nz slabs + epilogue
@@ -761,10 +781,15 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
                                  EpiMask{d->a2, a->a2, 64}, K3, 64, Conv3::K, Conv3::K);
   auto dW_c3 = gemm_op<1, 1, 16>(DyT<64>{d->a3}, Im2colT<Conv3>{a->a2},
                                  EpiPartial{ws + o3, 64, Conv3::K + 1}, 64, Conv3::K + 1, K3, ch3);
-  auto sp00 = subpix_op<0, 0>(p, a, d, B);
-  auto sp01 = subpix_op<0, 1>(p, a, d, B);
-  auto sp10 = subpix_op<1, 0>(p, a, d, B);
-  auto sp11 = subpix_op<1, 1>(p, a, d, B);
+  // DQ_SP_PAIR: two of the 8-wave sub-pixel tiles per 16-wave block of the grouped launch
+  auto sp_op = [](auto op) {
+    if constexpr (DQ_SP_PAIR != 0) return PairOp<decltype(op)>{op};
+    else return op;
+  };
+  auto sp00 = sp_op(subpix_op<0, 0>(p, a, d, B));
+  auto sp01 = sp_op(subpix_op<0, 1>(p, a, d, B));
+  auto sp10 = sp_op(subpix_op<1, 0>(p, a, d, B));
+  auto sp11 = sp_op(subpix_op<1, 1>(p, a, d, B));
   auto sum_c3 = ReduceOp<EpiGrad>{ws + o3, nz3, 64, Conv3::K + 1,
                                   EpiGrad{g->conv3_w, g->conv3_b, Conv3::K}};
   auto dW_c2 = gemm_op<1, 1, 16>(DyT<64>{d->a2}, Im2colT<Conv2>{a->a1},
@@ -807,6 +832,19 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
         auto dW_fc1a = gemm_op<4, 4, 1>(ColK{d->h, kHidden}, ColKOnes{a->a3, kFlat},
                                         Fc1EpiOpt<kOpt>::make(p, g, opt.a), kHidden, kFlat + 1,
                                         B, B);
+#ifndef DQ_FC1_SPLIT_L
+#define DQ_FC1_SPLIT_L 0
+#endif
+        // DQ_FC1_SPLIT_L = L > 2 (kHeadFrom 6): fc1's weight gradient + update for its rows
+        // [256, 512) in launch L instead of 2 (the gradient needs only d h and a3; fc1_w's
+        // last read is dX fc1 in launch 1)
+        constexpr int kFc1Lo = DQ_FC1_SPLIT_L > 2 ? kHidden / 2 : kHidden;
+        auto dW_fc1lo = gemm_op<4, 4, 1>(ColK{d->h, kHidden}, ColKOnes{a->a3, kFlat},
+                                         Fc1EpiOpt<kOpt>::make(p, g, opt.a), kFc1Lo, kFlat + 1,
+                                         B, B);
+        auto dW_fc1hi = gemm_op<4, 4, 1>(ColK{d->h + kFc1Lo, kHidden}, ColKOnes{a->a3, kFlat},
+                                         Fc1EpiOpt<kOpt>::make(p, g, opt.a).rows_from(kFc1Lo),
+                                         kHidden - kFc1Lo, kFlat + 1, B, B);
         auto sum_c2a = ReduceOp<decltype(GE::make(0, 0, 0, 0, 0, opt, 0))>{
             ws + o2, nz3, 64, Conv2::K + 1,
             GE::make(g->conv2_w, g->conv2_b, Conv2::K, p->conv2_w, p->conv2_b, opt, 0)};
@@ -838,24 +876,39 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
 #endif
           // fc2's optimizer part: launch 2 (its gradient is final after launch 1), or 4
           // (launch 2 holds the fc1 update's stream; nothing reads fc2_w before the next C)
-          if (DQ_FC2_OPT_LAUNCH == 2 || kHeadFrom != 6)
+          if (DQ_FC1_SPLIT_L > 2 && kHeadFrom == 6)
+            group_r(c, rd(2), dW_fc1lo, dX_c3, part(p->fc2_w, p->fc2_b + NO));
+          else if (DQ_FC2_OPT_LAUNCH == 2 || kHeadFrom != 6)
             group_r(c, rd(2), dW_fc1a, dX_c3, part(p->fc2_w, p->fc2_b + NO));
           else
             group_r(c, rd(2), dW_fc1a, dX_c3);
         }
         if (kHeadFrom == 6) {
-          if (in(3)) group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11, dW_c2);
+          if (in(3)) {
+            if (DQ_FC1_SPLIT_L == 3)
+              group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11, dW_c2, dW_fc1hi);
+            else
+              group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11, dW_c2);
+          }
           if (in(4)) {
-            if (DQ_FC2_OPT_LAUNCH == 4)
+            if (DQ_FC1_SPLIT_L == 4)
+              group_r(c, rd(4), sum_c3, dW_c1, dW_fc1hi);
+            else if (DQ_FC2_OPT_LAUNCH == 4)
               group_r(c, rd(4), sum_c3, dW_c1, part(p->fc2_w, p->fc2_b + NO));
             else
               group_r(c, rd(4), sum_c3, dW_c1);
           }
           if (in(5)) {
-            if (head)
+            if (DQ_FC1_SPLIT_L == 5) {
+              if (head)
+                group_r(c, rd(5), sum_c2a, sum_c1, part(p->conv3_w, p->fc1_w), head->conv1(), dW_fc1hi);
+              else
+                group_r(c, rd(5), sum_c2a, sum_c1, part(p->conv3_w, p->fc1_w), dW_fc1hi);
+            } else if (head) {
               group_r(c, rd(5), sum_c2a, sum_c1, part(p->conv3_w, p->fc1_w), head->conv1());
-            else
+            } else {
               group_r(c, rd(5), sum_c2a, sum_c1, part(p->conv3_w, p->fc1_w));
+            }
           }
           return;
         }

@@ -166,3 +166,36 @@ def test_gloo_mean_is_the_rank_ordered_sum_bitwise():
     assert np.array_equal(res[r], want)
   other = ((gs[3] + gs[2]) + gs[1]) + gs[0]          # the order matters for these inputs
   assert not np.array_equal(other * np.float32(1.0 / world), want)
+
+
+def _rank_dir_worker(rank, world, port, q):
+  os.environ['MASTER_ADDR'] = '127.0.0.1'
+  os.environ['MASTER_PORT'] = str(port)
+  dist.init_process_group('gloo', rank=rank, world_size=world)
+  import types
+  from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
+  got = DQNAgent._rank_dir(types.SimpleNamespace(_pg=dist.group.WORLD), '/ck')
+  alone = DQNAgent._rank_dir(types.SimpleNamespace(_pg=None), '/ck')
+  q.put((rank, got, alone))
+  dist.barrier()
+  dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_data_parallel_checkpoints_go_to_rank_directories():
+  """bundle_and_checkpoint / unbundle's directory (DQNAgent._rank_dir): a data-parallel rank
+  writes under checkpoint_dir/rank<r> (its own buffer; the reference's names would collide
+  in a shared directory), a single replica into checkpoint_dir itself as the reference."""
+  world = 2
+  ctx = mp.get_context('spawn')
+  q = ctx.Queue()
+  port = _free_port()
+  procs = [ctx.Process(target=_rank_dir_worker, args=(r, world, port, q)) for r in range(world)]
+  for p in procs:
+    p.start()
+  res = dict((r, (g, a)) for r, g, a in (q.get(timeout=240) for _ in range(world)))
+  for p in procs:
+    p.join(timeout=60)
+    assert p.exitcode == 0
+  for r in range(world):
+    assert res[r] == (os.path.join('/ck', 'rank%d' % r), '/ck')

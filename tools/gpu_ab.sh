@@ -22,9 +22,10 @@ if [ -n "$DQ_TESTS" ]; then
 fi
 for rep in $([ -z "$DQ_NOAB" ] && echo 1 2); do
   for spec in "" "$@"; do
-    # a build (ab/X/libdopamine_amd.so) or "args:<bench flags>" on the in-tree build
+    # a build (ab/X/libdopamine_amd.so), "args:<bench flags>" on the in-tree build, or
+    # "ab/X/libdopamine_amd.so|<bench flags>"
     lib=$spec; extra=
-    case "$spec" in args:*) lib=; extra=${spec#args:};; esac
+    case "$spec" in args:*) lib=; extra=${spec#args:};; *"|"*) lib=${spec%%|*}; extra=${spec#*|};; esac
     if [ "${CFG:-rainbow}" = rainbow ]; then
       line=$(DOPAMINE_AMD_LIB=$lib timeout -k 10 240 python bench.py --steps ${STEPS:-2000} --skip-cpu-baseline --skip-bf16 --skip-configs --gather-iters 20 $extra 2>>$OUT/err.log | tail -1) || exit 1
       v=$(echo "$line" | python3 -c 'import sys,json; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')
@@ -35,11 +36,17 @@ for rep in $([ -z "$DQ_NOAB" ] && echo 1 2); do
   done
 done
 if [ -n "$DQ_TIMELINE" ]; then
-  for lib in "" "$@"; do
-    n=$(basename $(dirname ${lib:-in-tree/x}))
-    DOPAMINE_AMD_LIB=$lib timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/r_$n -o run -- python3 bench.py --skip-cpu-baseline --skip-bf16 --skip-configs --gather-iters 20 > $OUT/prof_$n.log 2>&1 || exit 1
+  i=0
+  for spec in "" "$@"; do
+    i=$((i + 1))
+    lib=$spec; extra=
+    case "$spec" in args:*) lib=; extra=${spec#args:};; *"|"*) lib=${spec%%|*}; extra=${spec#*|};; esac
+    n=t$i
+    DOPAMINE_AMD_LIB=$lib timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/r_$n -o run -- python3 bench.py --skip-cpu-baseline --skip-bf16 --skip-configs --gather-iters 20 $extra > $OUT/prof_$n.log 2>&1 || exit 1
+    echo "== [$n] ${spec:-in-tree}" >> $OUT/timelines.txt
     python3 tools/step_timeline_db.py /tmp/r_$n/run_results.db k_c51 30 > $OUT/timeline_$n.txt
+    cat $OUT/timeline_$n.txt >> $OUT/timelines.txt
     python3 tools/prof_summary.py /tmp/r_$n/run_results.db 30 > $OUT/kernels_$n.txt
-    head -16 $OUT/timeline_$n.txt
+    echo "[$n] ${spec:-in-tree}"; head -2 $OUT/timeline_$n.txt
   done
 fi
