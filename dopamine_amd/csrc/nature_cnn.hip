@@ -725,6 +725,43 @@ bool backward_layer(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int 
   }
 }
 
+// The torso's backward (conv3 .. conv1 from d a3, e.g. IQN's d state) in four grouped
+// launches of the full backward's tiles -- [dX conv3 | dW conv3 slabs] · [conv2's input
+// gradient by sub-pixel class | dW conv2 slabs | sum conv3] · [dW conv1 slabs | sum conv2] ·
+// [sum conv1] -- instead of nine per-layer GEMM and split-K-sum launches: bitwise the same
+// gradients (same tiles, same slab order).
+void backward_torso_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int B,
+                            const float* x, const dq_cnn_acts* a, dq_cnn_acts* d) {
+  using W16 = Tile<1, 1, 16>;
+  const int K3 = B * 121, K1 = B * 441;
+  const int ch3 = split_chunk(K3, kSplitConvW, W16::BKT), nz3 = (K3 + ch3 - 1) / ch3;
+  const int ch1 = split_chunk(K1, kSplitConv1W, W16::BKT), nz1 = (K1 + ch1 - 1) / ch1;
+  const size_t o3 = c.take((size_t)nz3 * 64 * (Conv3::K + 1));
+  const size_t o2 = c.take((size_t)nz3 * 64 * (Conv2::K + 1));
+  const size_t o1 = c.take((size_t)nz1 * 32 * (Conv1::K + 1));
+  float* ws = c.ws;
+  if (c.dry) return;
+  auto dX_c3 = gemm_op<1, 1, 16>(Col2im<Conv3>{d->a3}, WeightT<Conv3>{p->conv3_w},
+                                 EpiMask{d->a2, a->a2, 64}, K3, 64, Conv3::K, Conv3::K);
+  auto dW_c3 = gemm_op<1, 1, 16>(DyT<64>{d->a3}, Im2colT<Conv3>{a->a2},
+                                 EpiPartial{ws + o3, 64, Conv3::K + 1}, 64, Conv3::K + 1, K3, ch3);
+  auto sum_c3 = ReduceOp<EpiGrad>{ws + o3, nz3, 64, Conv3::K + 1,
+                                  EpiGrad{g->conv3_w, g->conv3_b, Conv3::K}};
+  auto dW_c2 = gemm_op<1, 1, 16>(DyT<64>{d->a2}, Im2colT<Conv2>{a->a1},
+                                 EpiPartial{ws + o2, 64, Conv2::K + 1}, 64, Conv2::K + 1, K3, ch3);
+  auto sum_c2 = ReduceOp<EpiGrad>{ws + o2, nz3, 64, Conv2::K + 1,
+                                  EpiGrad{g->conv2_w, g->conv2_b, Conv2::K}};
+  auto dW_c1 = gemm_op<1, 1, 16>(DyT<32>{d->a1}, Im2colT<Conv1>{x},
+                                 EpiPartial{ws + o1, 32, Conv1::K + 1}, 32, Conv1::K + 1, K1, ch1);
+  auto sum_c1 = ReduceOp<EpiGrad>{ws + o1, nz1, 32, Conv1::K + 1,
+                                  EpiGrad{g->conv1_w, g->conv1_b, Conv1::K}};
+  group(c, dW_c3, dX_c3);
+  group(c, dW_c2, subpix_op<0, 0>(p, a, d, B), subpix_op<0, 1>(p, a, d, B),
+        subpix_op<1, 0>(p, a, d, B), subpix_op<1, 1>(p, a, d, B), sum_c3);
+  group(c, dW_c1, sum_c2);
+  group(c, sum_c1);
+}
+
 // Backward in 7 grouped launches (numbered 0..6 below):
 //   0: dh                      (fc2 input grad)
 //   1: dW fc2     | da3        (fc1 input grad)
@@ -1273,9 +1310,16 @@ int dq_cnn_backward_torso(const dq_cnn_params* p, const dq_cnn_params* g, int32_
   DQ_CHECK_ARG(p && g && a && d && x && ws && batch >= 1, "null argument");
   DQ_CHECK_ARG(p->in_channels == 4, "the Nature CNN takes 84x84x4 NHWC input");
   Ctx c{(hipStream_t)stream, ws, false, 0};
-  for (int layer = 2; layer <= 4; ++layer) {        // conv3, conv2, conv1 (same tiles as
-    backward_layer(c, p, g, batch, x, a, nullptr, d, layer, 1);   // the full backward)
-    if (layer < 4) backward_layer(c, p, g, batch, x, a, nullptr, d, layer, 0);
+#ifndef DQ_TORSO_GROUPED
+#define DQ_TORSO_GROUPED 1
+#endif
+  if (DQ_TORSO_GROUPED) {
+    backward_torso_grouped(c, p, g, batch, x, a, d);
+  } else {
+    for (int layer = 2; layer <= 4; ++layer) {        // conv3, conv2, conv1 (same tiles as
+      backward_layer(c, p, g, batch, x, a, nullptr, d, layer, 1);   // the full backward)
+      if (layer < 4) backward_layer(c, p, g, batch, x, a, nullptr, d, layer, 0);
+    }
   }
   DQ_CHECK_LAUNCH("dq_cnn_backward_torso");
   return DQ_OK;
@@ -1312,6 +1356,9 @@ size_t dq_cnn_workspace_floats(int32_t batch, int32_t n_out) {
   Ctx g{nullptr, nullptr, true, 0};
   backward_grouped<0>(g, &p, &p, batch, nullptr, &a, nullptr, &a, AdamHost{nullptr});
   need = g.need > need ? g.need : need;
+  Ctx t{nullptr, nullptr, true, 0};
+  backward_torso_grouped(t, &p, &p, batch, nullptr, &a, &a);
+  need = t.need > need ? t.need : need;
   Ctx f0{nullptr, nullptr, true, 0}, f1{nullptr, nullptr, true, 0};
   forward_fused(f0, f1, FwdOps{&p, nullptr, &a, nullptr, batch}, FwdOps{&p, nullptr, &a, nullptr, batch},
                 true);

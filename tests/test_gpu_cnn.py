@@ -318,3 +318,49 @@ def test_fused_forward_and_dqn_loss_equal_separate_path(B, A):
   ho.backward(got['grad'], groups=(1, 7), head_from=6)
   torch.cuda.synchronize()
   assert torch.equal(torch.cat([v.reshape(-1) for v in on.fp.grad_views]), ref_g)
+
+
+def test_grouped_torso_backward_equals_per_layer_bitwise():
+  """dq_cnn_backward_torso (IQN's torso: conv3 .. conv1 from d a3) in its four grouped
+  launches == the per-layer launches of the same tiles (dq_cnn_backward_layer), bit for bit:
+  every conv weight / bias gradient and the input gradients d a2, d a1."""
+  import ctypes
+  from dopamine_amd import _lib
+  from dopamine_amd.agents.networks import RainbowNetwork
+  from dopamine_amd.cnn import HipNatureCNN
+  torch.manual_seed(3)
+  net = RainbowNetwork(9, device='cuda', seed=2)
+  hip = HipNatureCNN(net, 32)
+  x = torch.rand(32, 84, 84, 4, device='cuda')
+  hip.forward(x)
+  da3 = torch.randn_like(hip.dacts['a3']) * (hip.acts['a3'] > 0)
+  stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+  names = [n for n in net.fp.offsets if n.startswith('conv')]
+
+  def run(grouped):
+    net.fp.grad.fill_(float('nan'))
+    hip.dacts['a3'].copy_(da3)
+    hip.dacts['a2'].fill_(float('nan'))
+    hip.dacts['a1'].fill_(float('nan'))
+    if grouped:
+      _lib.check(_lib.lib.dq_cnn_backward_torso(
+          ctypes.byref(hip._p), ctypes.byref(hip._g), 32, hip._x.data_ptr(), ctypes.byref(hip._a),
+          ctypes.byref(hip._d), hip.ws.data_ptr(), stream), 'dq_cnn_backward_torso')
+    else:
+      for layer, part in ((2, 1), (2, 0), (3, 1), (3, 0), (4, 1)):
+        _lib.check(_lib.lib.dq_cnn_backward_layer(
+            ctypes.byref(hip._p), ctypes.byref(hip._g), 32, hip._x.data_ptr(),
+            ctypes.byref(hip._a), hip.dacts['a3'].data_ptr(), ctypes.byref(hip._d),
+            hip.ws.data_ptr(), layer, part, stream), 'dq_cnn_backward_layer')
+    torch.cuda.synchronize()
+    import math
+    g = {n: net.fp.grad[net.fp.offsets[n][0]:net.fp.offsets[n][0] +
+                        math.prod(net.fp.offsets[n][1])].clone() for n in names}
+    return g, hip.dacts['a2'].clone(), hip.dacts['a1'].clone()
+
+  ga, a2a, a1a = run(True)
+  gb, a2b, a1b = run(False)
+  for n in names:
+    assert torch.isfinite(ga[n]).all(), n
+    assert torch.equal(ga[n], gb[n]), n
+  assert torch.equal(a2a, a2b) and torch.equal(a1a, a1b)
