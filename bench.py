@@ -301,13 +301,18 @@ def time_gather_large(agent, batch=1024, iters=50):
 def gather_traffic(batch):
   """HBM bytes per gather launch from the committed PMC passes (rocprofv3 --pmc
   FETCH_SIZE / WRITE_SIZE, calibrated as MI355X_MICROARCH.md prescribes;
-  tools/gather_traffic.py, profiles/r2_gather_traffic.json), or None."""
-  path = os.path.join(ROOT, 'profiles', 'r2_gather_traffic.json')
-  try:
-    d = json.load(open(path))
-    return round(float(d['traffic_bytes_per_launch'][str(batch)])), os.path.relpath(path, ROOT)
-  except (OSError, KeyError, ValueError):
-    return None, None
+  tools/gpu_gather_pmc.sh + tools/gather_traffic.py): the newest of
+  profiles/r<N>_gather_traffic.json, or None."""
+  import glob
+  paths = sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*_gather_traffic.json')),
+                 key=lambda q: int(os.path.basename(q)[1:].split('_')[0]))
+  for path in reversed(paths):
+    try:
+      d = json.load(open(path))
+      return round(float(d['traffic_bytes_per_launch'][str(batch)])), os.path.relpath(path, ROOT)
+    except (OSError, KeyError, ValueError):
+      continue
+  return None, None
 
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense

@@ -590,6 +590,14 @@ template <class EP>
 struct HasPre<EP, decltype((void)EP::kPre)> {
   static constexpr bool value = EP::kPre;
 };
+template <class EP, class = void>
+struct PreOf {
+  using type = int;
+};
+template <class EP>
+struct PreOf<EP, decltype((void)sizeof(typename EP::Pre))> {
+  using type = typename EP::Pre;
+};
 
 // EP::kVec: the epilogue takes 4 consecutive columns at a time (E.vec4(m, n, float4)),
 // so its loads and stores are 16 B per lane: igemm_block passes each wave's 32 x 32
@@ -1362,15 +1370,25 @@ __device__ __forceinline__ void splitk_sum(const float* ws, int splits, int M, i
                                            int64_t i) {
   if (i >= (int64_t)M * N) return;
   const int64_t MN = (int64_t)M * N;
+  // a two-phase epilogue (the optimizer's parameter / moment loads) issues its loads first:
+  // they do not depend on the sum, so they share its memory round
+  typename std::conditional<HasPre<EP>::value, typename PreOf<EP>::type, int>::type q{};
+  if constexpr (HasPre<EP>::value) q = E.pre((int)(i / N), (int)(i % N));
   float s = ws[i];
-  for (int z0 = 1; z0 < splits; z0 += 8) {
-    float v[8];
+#ifndef DQ_SPLITK_BATCH
+#define DQ_SPLITK_BATCH 16   // slab loads in flight per memory round (conv1's 28 slabs: 2 rounds)
+#endif
+  for (int z0 = 1; z0 < splits; z0 += DQ_SPLITK_BATCH) {
+    float v[DQ_SPLITK_BATCH];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = ws[(int64_t)min(z0 + u, splits - 1) * MN + i];
+    for (int u = 0; u < DQ_SPLITK_BATCH; ++u) v[u] = ws[(int64_t)min(z0 + u, splits - 1) * MN + i];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) s = z0 + u < splits ? __fadd_rn(s, v[u]) : s;
+    for (int u = 0; u < DQ_SPLITK_BATCH; ++u) s = z0 + u < splits ? __fadd_rn(s, v[u]) : s;
   }
-  E((int)(i / N), (int)(i % N), s, 0);
+  if constexpr (HasPre<EP>::value)
+    E.commit((int)(i / N), (int)(i % N), s, q);
+  else
+    E((int)(i / N), (int)(i % N), s, 0);
 }
 
 template <class EP>

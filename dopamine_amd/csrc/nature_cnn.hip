@@ -120,26 +120,66 @@ struct FcHeadOp {
   __device__ __forceinline__ void run(int blk, float* smem) const {
     const int g = blk % ng, j = (blk / ng) % kBands, m0 = 32 * (blk / (ng * kBands));
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nt = 4 * g + wave;
+    const int r = lane & 31, hh = lane >> 5, n = 32 * nt + r;
+#ifndef DQ_FCHEAD_EARLY_W2
+#define DQ_FCHEAD_EARLY_W2 1
+#endif
+    // B operand: lane r's 8 k of each half, straight from W2's row n (k contiguous) --
+    // independent of the slab sums, so (DQ_FCHEAD_EARLY_W2) issued before them: one
+    // dependent memory round fewer
+    float bv[2][8];
+    auto load_w2 = [&]() {
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        const float* src = w2 + (int64_t)min(n, NO - 1) * kHidden + 32 * j + 16 * hf + 8 * hh;
+        const float4 x0 = *reinterpret_cast<const float4*>(src);
+        const float4 x1 = *reinterpret_cast<const float4*>(src + 4);
+        const bool ok = n < NO;
+        bv[hf][0] = ok ? x0.x : 0.0f; bv[hf][1] = ok ? x0.y : 0.0f;
+        bv[hf][2] = ok ? x0.z : 0.0f; bv[hf][3] = ok ? x0.w : 0.0f;
+        bv[hf][4] = ok ? x1.x : 0.0f; bv[hf][5] = ok ? x1.y : 0.0f;
+        bv[hf][6] = ok ? x1.z : 0.0f; bv[hf][7] = ok ? x1.w : 0.0f;
+      }
+    };
+    if (DQ_FCHEAD_EARLY_W2) load_w2();
     {
       const int r = tid >> 3, c = 4 * (tid & 7);
       const int m = min(m0 + r, B - 1);
       const int64_t i = (int64_t)m * kHidden + 32 * j + c, MN = (int64_t)B * kHidden;
+      const float4 bb = *reinterpret_cast<const float4*>(b1 + 32 * j + c);
       float4 s = *reinterpret_cast<const float4*>(ws + i);
-      for (int z0 = 1; z0 < nz; z0 += 8) {
-        float4 v[8];
+      if (nz <= 16) {
+        // all (up to 16) slabs' loads in flight together, then the sum in slab order: one
+        // memory round instead of one per 8 slabs (a runtime loop splits the batches)
+        float4 v[15];
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-          v[u] = *reinterpret_cast<const float4*>(ws + (int64_t)min(z0 + u, nz - 1) * MN + i);
+        for (int u = 0; u < 15; ++u)
+          v[u] = *reinterpret_cast<const float4*>(ws + (int64_t)min(1 + u, nz - 1) * MN + i);
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (z0 + u < nz) {
+        for (int u = 0; u < 15; ++u)
+          if (1 + u < nz) {
             s.x = __fadd_rn(s.x, v[u].x);
             s.y = __fadd_rn(s.y, v[u].y);
             s.z = __fadd_rn(s.z, v[u].z);
             s.w = __fadd_rn(s.w, v[u].w);
           }
+      } else {
+        for (int z0 = 1; z0 < nz; z0 += 8) {
+          float4 v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            v[u] = *reinterpret_cast<const float4*>(ws + (int64_t)min(z0 + u, nz - 1) * MN + i);
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            if (z0 + u < nz) {
+              s.x = __fadd_rn(s.x, v[u].x);
+              s.y = __fadd_rn(s.y, v[u].y);
+              s.z = __fadd_rn(s.z, v[u].z);
+              s.w = __fadd_rn(s.w, v[u].w);
+            }
+        }
       }
-      const float4 bb = *reinterpret_cast<const float4*>(b1 + 32 * j + c);
       s.x = fmaxf(__fadd_rn(s.x, bb.x), 0.0f);
       s.y = fmaxf(__fadd_rn(s.y, bb.y), 0.0f);
       s.z = fmaxf(__fadd_rn(s.z, bb.z), 0.0f);
@@ -152,22 +192,8 @@ struct FcHeadOp {
       q[3] = s.w;
     }
     __syncthreads();
-    const int nt = 4 * g + wave;
     if (32 * nt >= NO) return;
-    const int r = lane & 31, hh = lane >> 5, n = 32 * nt + r;
-    // B operand: lane r's 8 k of each half, straight from W2's row n (k contiguous)
-    float bv[2][8];
-#pragma unroll
-    for (int hf = 0; hf < 2; ++hf) {
-      const float* src = w2 + (int64_t)min(n, NO - 1) * kHidden + 32 * j + 16 * hf + 8 * hh;
-      const float4 x0 = *reinterpret_cast<const float4*>(src);
-      const float4 x1 = *reinterpret_cast<const float4*>(src + 4);
-      const bool ok = n < NO;
-      bv[hf][0] = ok ? x0.x : 0.0f; bv[hf][1] = ok ? x0.y : 0.0f;
-      bv[hf][2] = ok ? x0.z : 0.0f; bv[hf][3] = ok ? x0.w : 0.0f;
-      bv[hf][4] = ok ? x1.x : 0.0f; bv[hf][5] = ok ? x1.y : 0.0f;
-      bv[hf][6] = ok ? x1.z : 0.0f; bv[hf][7] = ok ? x1.w : 0.0f;
-    }
+    if (!DQ_FCHEAD_EARLY_W2) load_w2();
     f32x16 acc;
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[e] = 0.0f;
@@ -838,6 +864,15 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
   auto sum_c1 = ReduceOp<decltype(GE::make(0, 0, 0, 0, 0, opt, 0))>{
       ws + o1, nz1, 32, Conv1::K + 1,
       GE::make(g->conv1_w, g->conv1_b, Conv1::K, p->conv1_w, p->conv1_b, opt, 1)};
+#ifndef DQ_T1_PAIR
+#define DQ_T1_PAIR 0
+#endif
+  // the target head's conv1 (8-wave tiles) riding in a 16-wave launch: DQ_T1_PAIR puts two
+  // of its tiles in each block (PairOp) instead of leaving half of every block's waves idle
+  auto t1 = [&]() {
+    if constexpr (DQ_T1_PAIR != 0) return PairOp<decltype(head->conv1())>{head->conv1()};
+    else return head->conv1();
+  };
   auto in = [&](int i) { return first <= i && i < last; };
   auto rd = [&](int i) {   // rider of launch i
     return i >= first && i - first < n_riders ? riders + (i - first) : nullptr;
@@ -938,11 +973,11 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
           if (in(5)) {
             if (DQ_FC1_SPLIT_L == 5) {
               if (head)
-                group_r(c, rd(5), sum_c2a, sum_c1, part(p->conv3_w, p->fc1_w), head->conv1(), dW_fc1hi);
+                group_r(c, rd(5), sum_c2a, sum_c1, part(p->conv3_w, p->fc1_w), t1(), dW_fc1hi);
               else
                 group_r(c, rd(5), sum_c2a, sum_c1, part(p->conv3_w, p->fc1_w), dW_fc1hi);
             } else if (head) {
-              group_r(c, rd(5), sum_c2a, sum_c1, part(p->conv3_w, p->fc1_w), head->conv1());
+              group_r(c, rd(5), sum_c2a, sum_c1, part(p->conv3_w, p->fc1_w), t1());
             } else {
               group_r(c, rd(5), sum_c2a, sum_c1, part(p->conv3_w, p->fc1_w));
             }
@@ -1030,7 +1065,7 @@ if constexpr (kHeadFrom == 4) {
       if (in(4)) group_r(c, rd(4), sum_c3, dW_c1);
       if (in(5)) {
         if (head)
-          group_r(c, rd(5), sum_c2, sum_c1, head->conv1());
+          group_r(c, rd(5), sum_c2, sum_c1, t1());
         else
           group_r(c, rd(5), sum_c2, sum_c1);
       }

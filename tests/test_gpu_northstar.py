@@ -262,6 +262,42 @@ def test_rainbow_bench_path_matches_float64_oracle():
 
 
 @pytest.mark.timeout(600)
+def test_rainbow_bench_drive_without_gradient_stores_is_the_traced_run_bitwise():
+  """The bench's exact drive (keep_gradients = False: the fused TF1 Adam consumes fc1's
+  gradient in registers and no flat gradient is stored) at the bench's size (1M buffer,
+  B = 32, graph + chunk path) against the traced run the lockstep test above checks against
+  float64 (tracing forces the gradient stores on): the same step sequence gives bitwise the
+  same parameters, Adam moments, target network and sum tree."""
+  import bench
+  torch.cuda.set_device(0)
+  res = []
+  for traced in (True, False):
+    agent = bench.build_agent(9, 1_000_000, 32, torch.device('cuda', 0))
+    if traced:
+      agent.enable_trace()
+    assert agent._store_grads() == traced
+    random.seed(0)
+    bench.fill_synthetic(agent._replay.memory, 9, seed=1)
+    _prime(agent)
+    agent.train_gradient_steps(1)
+    for _ in range(CHUNKS):
+      agent.train_gradient_steps(agent._UNROLL)
+    agent._discard_prefetch()
+    agent._replay.memory.sync_rng()
+    torch.cuda.synchronize()
+    res.append([t.detach().cpu().clone() for t in (agent.online_convnet.fp.flat,
+                                                   agent.target_convnet.fp.flat,
+                                                   agent._opt.m, agent._opt.v,
+                                                   agent._replay.memory._tree)] +
+               [random.getstate()])
+    del agent
+    torch.cuda.empty_cache()
+  for a, b in zip(res[0][:-1], res[1][:-1]):
+    assert torch.equal(a, b)
+  assert res[0][-1] == res[1][-1]
+
+
+@pytest.mark.timeout(600)
 def test_c51_uniform_bench_path_matches_float64_oracle():
   """C51 as c51.gin binds it (RainbowAgent, replay_scheme 'uniform', n = 1, Adam 2.5e-4 /
   3.125e-4; rb:175-198, 331), 9 actions, 1M buffer, B = 32, on the same graph / chunk path:
