@@ -8,7 +8,7 @@ import os
 
 from dopamine_amd._build import HEADER, LIB_PATH  # noqa: F401
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 OK = 0
 (ST_OK, ST_EMPTY_TREE, ST_MAX_ATTEMPTS, ST_TAPE_EXHAUSTED, ST_NEG_PRIORITY, ST_TOO_FEW, ST_BAD_INDEX,
  ST_BROADCAST) = range(8)
@@ -185,6 +185,9 @@ SIGNATURES = {
     'dq_cnn_forward_torso': [ctypes.POINTER(CnnParams), _I32, _P, ctypes.POINTER(CnnActs), _P, _P],
     'dq_cnn_backward_torso': [ctypes.POINTER(CnnParams), ctypes.POINTER(CnnParams), _I32, _P,
                               ctypes.POINTER(CnnActs), ctypes.POINTER(CnnActs), _P, _P],
+    'dq_cnn_backward_torso_opt': [ctypes.POINTER(CnnParams), ctypes.POINTER(CnnParams), _I32, _P,
+                                  ctypes.POINTER(CnnActs), ctypes.POINTER(CnnActs), _P,
+                                  ctypes.POINTER(AdamArgs), _P, _P, _P],
     'dq_iqn_head_forward': [ctypes.POINTER(IqnHead), _I32, _I32, _P, _P, ctypes.POINTER(IqnActs),
                             _P, _P],
     'dq_iqn_head_backward': [ctypes.POINTER(IqnHead), ctypes.POINTER(IqnHead), _I32, _I32, _P,

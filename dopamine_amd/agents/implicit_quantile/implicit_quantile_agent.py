@@ -147,9 +147,21 @@ class ImplicitQuantileAgent(rainbow_agent.RainbowAgent):
     self._last_ta = ta
     return qv, out['grad']
 
+  def _fused_opt(self):
+    """The HIP executor with TF1 Adam / RMSProp, a single replica and no double DQN: the
+    optimizer step runs inside the torso's backward launches (HipIqnNet.backward(adam=...),
+    dq_cnn_backward_torso_opt) instead of a launch of its own after the step.  double_dqn
+    reads the online network on s' on the prefetch stream during the backward, so there the
+    update waits for it (the separate step after the streams join)."""
+    return (self.fuse_optimizer and self._iqn is not None and self._pg is None and
+            not self.double_dqn and isinstance(self._opt, (ops.TF1Adam, ops.TF1RMSProp)))
+
   def _backward(self, y, g, k=0):
     if self._iqn is not None:
-      self._iqn['online'].backward(g)
+      if self._fused_opt():
+        self._iqn['online'].backward(g, adam=self._opt, slot=k, store_grads=self._store_grads())
+      else:
+        self._iqn['online'].backward(g)
       return
     super()._backward(y, g, k)
 

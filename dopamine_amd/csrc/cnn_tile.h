@@ -1372,8 +1372,12 @@ __device__ __forceinline__ void splitk_sum(const float* ws, int splits, int M, i
   const int64_t MN = (int64_t)M * N;
   // a two-phase epilogue (the optimizer's parameter / moment loads) issues its loads first:
   // they do not depend on the sum, so they share its memory round
+#ifndef DQ_SPLITK_PRE
+#define DQ_SPLITK_PRE 1
+#endif
+  constexpr bool kEarly = HasPre<EP>::value && DQ_SPLITK_PRE;
   typename std::conditional<HasPre<EP>::value, typename PreOf<EP>::type, int>::type q{};
-  if constexpr (HasPre<EP>::value) q = E.pre((int)(i / N), (int)(i % N));
+  if constexpr (kEarly) q = E.pre((int)(i / N), (int)(i % N));
   float s = ws[i];
 #ifndef DQ_SPLITK_BATCH
 #define DQ_SPLITK_BATCH 16   // slab loads in flight per memory round (conv1's 28 slabs: 2 rounds)
@@ -1385,7 +1389,7 @@ __device__ __forceinline__ void splitk_sum(const float* ws, int splits, int M, i
 #pragma unroll
     for (int u = 0; u < DQ_SPLITK_BATCH; ++u) s = z0 + u < splits ? __fadd_rn(s, v[u]) : s;
   }
-  if constexpr (HasPre<EP>::value)
+  if constexpr (kEarly)
     E.commit((int)(i / N), (int)(i % N), s, q);
   else
     E((int)(i / N), (int)(i % N), s, 0);

@@ -756,8 +756,15 @@ bool backward_layer(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int 
 // gradient by sub-pixel class | dW conv2 slabs | sum conv3] · [dW conv1 slabs | sum conv2] ·
 // [sum conv1] -- instead of nine per-layer GEMM and split-K-sum launches: bitwise the same
 // gradients (same tiles, same slab order).
+// kOpt (1 Adam, 2 RMSProp): the same four launches with the whole network's optimizer step
+// spread over them -- [head_begin, head_end) (gradients final before the torso's backward) as
+// float4 riders of launches 1-2, conv3 (final after launch 2) in launch 3, conv2 and conv1 in
+// their split-K sums' epilogues (launches 3, 4; conv1's advances the beta powers).
+template <int kOpt = 0>
 void backward_torso_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int B,
-                            const float* x, const dq_cnn_acts* a, dq_cnn_acts* d) {
+                            const float* x, const dq_cnn_acts* a, dq_cnn_acts* d,
+                            const AdamHost& opt = AdamHost{nullptr}, float* head_begin = nullptr,
+                            float* head_end = nullptr) {
   using W16 = Tile<1, 1, 16>;
   const int K3 = B * 121, K1 = B * 441;
   const int ch3 = split_chunk(K3, kSplitConvW, W16::BKT), nz3 = (K3 + ch3 - 1) / ch3;
@@ -781,11 +788,28 @@ void backward_torso_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params*
                                  EpiPartial{ws + o1, 32, Conv1::K + 1}, 32, Conv1::K + 1, K1, ch1);
   auto sum_c1 = ReduceOp<EpiGrad>{ws + o1, nz1, 32, Conv1::K + 1,
                                   EpiGrad{g->conv1_w, g->conv1_b, Conv1::K}};
-  group(c, dW_c3, dX_c3);
-  group(c, dW_c2, subpix_op<0, 0>(p, a, d, B), subpix_op<0, 1>(p, a, d, B),
-        subpix_op<1, 0>(p, a, d, B), subpix_op<1, 1>(p, a, d, B), sum_c3);
-  group(c, dW_c1, sum_c2);
-  group(c, sum_c1);
+  if constexpr (kOpt == 0) {
+    group(c, dW_c3, dX_c3);
+    group(c, dW_c2, subpix_op<0, 0>(p, a, d, B), subpix_op<0, 1>(p, a, d, B),
+          subpix_op<1, 0>(p, a, d, B), subpix_op<1, 1>(p, a, d, B), sum_c3);
+    group(c, dW_c1, sum_c2);
+    group(c, sum_c1);
+  } else {
+    using GE = GradEpi<kOpt>;
+    auto part = [&](float* w0, float* w1) { return OptPart<kOpt>::make(p, g, opt.a, w0, w1); };
+    float* hm = head_begin + (((head_end - head_begin) / 2) & ~(int64_t)3);
+    auto sum_c2o = ReduceOp<decltype(GE::make(0, 0, 0, 0, 0, opt, 0))>{
+        ws + o2, nz3, 64, Conv2::K + 1,
+        GE::make(g->conv2_w, g->conv2_b, Conv2::K, p->conv2_w, p->conv2_b, opt, 0)};
+    auto sum_c1o = ReduceOp<decltype(GE::make(0, 0, 0, 0, 0, opt, 0))>{
+        ws + o1, nz1, 32, Conv1::K + 1,
+        GE::make(g->conv1_w, g->conv1_b, Conv1::K, p->conv1_w, p->conv1_b, opt, 1)};
+    group(c, dW_c3, dX_c3, part(head_begin, hm));
+    group(c, dW_c2, subpix_op<0, 0>(p, a, d, B), subpix_op<0, 1>(p, a, d, B),
+          subpix_op<1, 0>(p, a, d, B), subpix_op<1, 1>(p, a, d, B), sum_c3, part(hm, head_end));
+    group(c, dW_c1, sum_c2o, part(p->conv3_w, head_begin));
+    group(c, sum_c1o);
+  }
 }
 
 // Backward in 7 grouped launches (numbered 0..6 below):
@@ -1357,6 +1381,26 @@ int dq_cnn_backward_torso(const dq_cnn_params* p, const dq_cnn_params* g, int32_
     }
   }
   DQ_CHECK_LAUNCH("dq_cnn_backward_torso");
+  return DQ_OK;
+}
+
+int dq_cnn_backward_torso_opt(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch,
+                              const float* x, const dq_cnn_acts* a, dq_cnn_acts* d, float* ws,
+                              const dq_adam_args* opt, float* head_begin, float* head_end,
+                              void* stream) {
+  DQ_CHECK_ARG(p && g && a && d && x && ws && opt && batch >= 1, "null argument");
+  DQ_CHECK_ARG(p->in_channels == 4, "the Nature CNN takes 84x84x4 NHWC input");
+  const int rc = check_adam(p, g, opt);
+  if (rc) return rc;
+  DQ_CHECK_ARG(head_begin && head_end && head_begin >= p->conv3_b + 64 && head_end > head_begin &&
+                   ((head_begin - opt->var) & 3) == 0 && ((p->conv3_w - opt->var) & 3) == 0,
+               "head range: 16-byte aligned, after conv3 in opt->var");
+  Ctx c{(hipStream_t)stream, ws, false, 0};
+  if (opt->kind == DQ_OPT_RMSPROP)
+    backward_torso_grouped<2>(c, p, g, batch, x, a, d, AdamHost{opt}, head_begin, head_end);
+  else
+    backward_torso_grouped<1>(c, p, g, batch, x, a, d, AdamHost{opt}, head_begin, head_end);
+  DQ_CHECK_LAUNCH("dq_cnn_backward_torso_opt");
   return DQ_OK;
 }
 

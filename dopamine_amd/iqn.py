@@ -100,16 +100,32 @@ class HipIqnNet(object):
                                             _stream(self.device)), 'dq_iqn_head_forward')
     return self.acts['q'], self.taus
 
-  def backward(self, dq):
-    """dq: (R, A) = d loss / d q.  Writes every parameter gradient into net.fp.grad."""
+  def backward(self, dq, adam=None, slot=0, store_grads=True):
+    """dq: (R, A) = d loss / d q.  Writes every parameter gradient into net.fp.grad.
+    adam: an ops.TF1Adam / TF1RMSProp over net.fp.flat -- its whole step is applied in the
+    torso's backward launches (dq_cnn_backward_torso_opt: the head's range as float4 riders,
+    conv2 / conv1 in their split-K sums' epilogues), bitwise the separate optimizer launch;
+    slot: Adam's beta-power slot; store_grads False: the fused epilogues skip the gradient
+    stores they consume (no_grad_store)."""
     assert self.keep and dq.shape == (self.R, self.A) and dq.is_contiguous()
     t = self.torso
     _lib.check(_lib.lib.dq_iqn_head_backward(
         ctypes.byref(self._p), ctypes.byref(self._g), self.B, self.nq, t.acts['a3'].data_ptr(),
         ctypes.byref(self._a), dq.data_ptr(), ctypes.byref(self._d), t.dacts['a3'].data_ptr(),
         self.ws.data_ptr(), _stream(self.device)), 'dq_iqn_head_backward')
-    _lib.check(_lib.lib.dq_cnn_backward_torso(ctypes.byref(t._p), ctypes.byref(t._g), self.B,
-                                              t._x.data_ptr(), ctypes.byref(t._a),
-                                              ctypes.byref(t._d), t.ws.data_ptr(),
-                                              _stream(self.device)), 'dq_cnn_backward_torso')
+    if adam is None:
+      _lib.check(_lib.lib.dq_cnn_backward_torso(ctypes.byref(t._p), ctypes.byref(t._g), self.B,
+                                                t._x.data_ptr(), ctypes.byref(t._a),
+                                                ctypes.byref(t._d), t.ws.data_ptr(),
+                                                _stream(self.device)), 'dq_cnn_backward_torso')
+      return self.net.fp.grad
+    fp = self.net.fp
+    t.store_grads = bool(store_grads)
+    args = t._adam_args(adam, slot)
+    head0 = fp.flat.data_ptr() + 4 * fp.offsets['emb_w'][0]
+    head1 = fp.flat.data_ptr() + 4 * fp.flat.numel()
+    _lib.check(_lib.lib.dq_cnn_backward_torso_opt(
+        ctypes.byref(t._p), ctypes.byref(t._g), self.B, t._x.data_ptr(), ctypes.byref(t._a),
+        ctypes.byref(t._d), t.ws.data_ptr(), ctypes.byref(args), ctypes.c_void_p(head0),
+        ctypes.c_void_p(head1), _stream(self.device)), 'dq_cnn_backward_torso_opt')
     return self.net.fp.grad

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define DQ_ABI_VERSION 5
+#define DQ_ABI_VERSION 6
 
 /* host-side return codes */
 #define DQ_OK 0
@@ -499,6 +499,17 @@ int dq_cnn_forward_torso(const dq_cnn_params* p, int32_t batch, const float* x, 
 int dq_cnn_backward_torso(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch,
                           const float* x, const dq_cnn_acts* a, dq_cnn_acts* d, float* ws,
                           void* stream);
+/* dq_cnn_backward_torso + the whole network's optimizer step (ABI 6; IQN's single-replica
+   learner: the head's gradients are already final in g): TF1 Adam / RMSProp (opt->kind) on
+   [head_begin, head_end) -- the parameters after the torso in opt->var, e.g. IQN's quantile
+   head -- and on conv3 as float4 riders of the torso's launches, conv2 and conv1 in their
+   split-K sums' epilogues (conv1's advances Adam's beta powers).  Parameters, moments and
+   gradients bitwise those of dq_cnn_backward_torso followed by dq_adam_tf1 / dq_rmsprop_tf1
+   over the whole buffer (replaces the separate optimizer launch of dqn:322 / iqn:321). */
+int dq_cnn_backward_torso_opt(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch,
+                              const float* x, const dq_cnn_acts* a, dq_cnn_acts* d, float* ws,
+                              const dq_adam_args* opt, float* head_begin, float* head_end,
+                              void* stream);
 
 /* ImplicitQuantileNetwork's quantile head (atari_lib.py:147-199) on the fp32 matrix cores.
    R = nq * batch rows ordered q * batch + b (tf.tile, atari_lib.py:174). */

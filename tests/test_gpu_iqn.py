@@ -109,3 +109,34 @@ def test_tau_sampler_is_uniform_and_replays_in_graphs():
     got.append(out.cpu().numpy().copy())
   for e, r in zip(eager, got):
     np.testing.assert_array_equal(e, r)
+
+
+@pytest.mark.parametrize('store', [True, False])
+def test_fused_optimizer_torso_backward_equals_backward_then_adam(store):
+  """dq_cnn_backward_torso_opt (the IQN learner's TF1 Adam inside the torso's grouped
+  backward launches: the head as float4 riders, conv3 after its sum, conv2 / conv1 in their
+  split-K sums' epilogues) == head + torso backward followed by dq_adam_tf1 over the whole
+  flat buffer, bitwise, over two steps (both beta-power slots); store False: the fused
+  epilogues skip the gradient stores, the parameters and moments unchanged."""
+  from dopamine_amd import ops
+  from dopamine_amd.agents.networks import ImplicitQuantileNetwork
+  from dopamine_amd.iqn import HipIqnNet
+  B, nq, A = 16, 8, 4
+  nets = [ImplicitQuantileNetwork(A, device='cuda', seed=7) for _ in range(2)]
+  exs = [HipIqnNet(n, B, nq, keep=True) for n in nets]
+  opts = [ops.TF1Adam(n.fp.flat, learning_rate=5e-5, epsilon=3.125e-4) for n in nets]
+  rs = np.random.RandomState(1)
+  for step in range(2):
+    x = torch.from_numpy(rs.rand(B, 84, 84, 4).astype(np.float32)).cuda()
+    taus = torch.from_numpy(rs.rand(nq * B).astype(np.float32)).cuda()
+    dq = torch.from_numpy(rs.randn(nq * B, A).astype(np.float32) / (nq * B)).cuda()
+    for ex in exs:
+      ex.forward(x, taus)
+    exs[0].backward(dq, adam=opts[0], slot=step % 2, store_grads=store)
+    exs[1].backward(dq)
+    opts[1].step(nets[1].fp.grad, slot=step % 2)
+    torch.cuda.synchronize()
+    for n in ('params', 'm', 'v', 'state'):
+      assert torch.equal(getattr(opts[0], n), getattr(opts[1], n)), (step, n)
+    if store:
+      assert torch.equal(nets[0].fp.grad, nets[1].fp.grad)

@@ -30,7 +30,7 @@ for rep in $([ -z "$DQ_NOAB" ] && echo 1 2); do
       line=$(DOPAMINE_AMD_LIB=$lib timeout -k 10 240 python bench.py --steps ${STEPS:-2000} --skip-cpu-baseline --skip-bf16 --skip-configs --gather-iters 20 $extra 2>>$OUT/err.log | tail -1) || exit 1
       v=$(echo "$line" | python3 -c 'import sys,json; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')
     else
-      v=$(DOPAMINE_AMD_LIB=$lib timeout -k 10 240 python tools/bench_configs.py ${STEPS:-300} $CFG 2>>$OUT/err.log | tail -1) || exit 1
+      v=$(DOPAMINE_AMD_LIB=$lib timeout -k 10 240 python tools/bench_configs.py ${STEPS:-300} $CFG $extra 2>>$OUT/err.log | tail -1) || exit 1
     fi
     echo "[${spec:-in-tree}] $v" | tee -a $OUT/ab.log
   done
