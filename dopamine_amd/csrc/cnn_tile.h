@@ -435,10 +435,31 @@ struct EpiGradAdamVec {
   struct VPre {
     float4 w, m, v;
   };
+#ifndef DQ_ADAM_NT
+#define DQ_ADAM_NT 0   // 1: the streamed state's stores non-temporal; 2: its loads too
+#endif
+  __device__ static __forceinline__ float4 ldst(const float* p) {
+    if constexpr (DQ_ADAM_NT >= 2) {
+      typedef float f4v __attribute__((ext_vector_type(4)));
+      const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+      return make_float4(v.x, v.y, v.z, v.w);
+    } else {
+      return ld4(p);
+    }
+  }
+  __device__ static __forceinline__ void stst(float* p, float4 v) {
+    if constexpr (DQ_ADAM_NT >= 1) {
+      typedef float f4v __attribute__((ext_vector_type(4)));
+      const f4v x = {v.x, v.y, v.z, v.w};
+      __builtin_nontemporal_store(x, reinterpret_cast<f4v*>(p));
+    } else {
+      *reinterpret_cast<float4*>(p) = v;
+    }
+  }
   __device__ __forceinline__ VPre vpre(int m, int n) const {
     if (n >= nw) return VPre{zero4(), zero4(), zero4()};
     const int64_t i = (int64_t)m * nw + n;
-    return VPre{ld4(w + i), ld4(mw + i), ld4(vw + i)};
+    return VPre{ldst(w + i), ldst(mw + i), ldst(vw + i)};
   }
   __device__ __forceinline__ void vcommit(int m, int n, float4 g, const VPre& p) const {
     if (n >= nw) {                 // the bias column (and the tile's padding past it)
@@ -454,9 +475,9 @@ struct EpiGradAdamVec {
     adam1(pw.z, g.z, pm.z, pv.z, alpha, omb1, omb2, o.eps);
     adam1(pw.w, g.w, pm.w, pv.w, alpha, omb1, omb2, o.eps);
     if (o.store_grad) *reinterpret_cast<float4*>(gw + i) = g;
-    *reinterpret_cast<float4*>(w + i) = pw;
-    *reinterpret_cast<float4*>(mw + i) = pm;
-    *reinterpret_cast<float4*>(vw + i) = pv;
+    stst(w + i, pw);
+    stst(mw + i, pm);
+    stst(vw + i, pv);
   }
   __device__ __forceinline__ void vec4(int m, int n, float4 g) const {
     if (n >= nw) {                 // the bias column (and the tile's padding past it)
@@ -1373,14 +1394,14 @@ __device__ __forceinline__ void splitk_sum(const float* ws, int splits, int M, i
   // a two-phase epilogue (the optimizer's parameter / moment loads) issues its loads first:
   // they do not depend on the sum, so they share its memory round
 #ifndef DQ_SPLITK_PRE
-#define DQ_SPLITK_PRE 1
+#define DQ_SPLITK_PRE 0     // 1: the optimizer's loads before the sum (measured slower, round 4)
 #endif
   constexpr bool kEarly = HasPre<EP>::value && DQ_SPLITK_PRE;
   typename std::conditional<HasPre<EP>::value, typename PreOf<EP>::type, int>::type q{};
   if constexpr (kEarly) q = E.pre((int)(i / N), (int)(i % N));
   float s = ws[i];
 #ifndef DQ_SPLITK_BATCH
-#define DQ_SPLITK_BATCH 16   // slab loads in flight per memory round (conv1's 28 slabs: 2 rounds)
+#define DQ_SPLITK_BATCH 8   // slab loads in flight per memory round (16 measured slower, round 4)
 #endif
   for (int z0 = 1; z0 < splits; z0 += DQ_SPLITK_BATCH) {
     float v[DQ_SPLITK_BATCH];

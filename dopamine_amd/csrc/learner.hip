@@ -892,7 +892,7 @@ int dq_adam_tf1_part(float* var, const float* grad, float* m, float* v, float* s
   DQ_CHECK_ARG(((uintptr_t)var | (uintptr_t)grad | (uintptr_t)m | (uintptr_t)v) % 16 == 0,
                "adam buffers must be 16-byte aligned");
 #ifndef DQ_ADAM_PART_MAXB
-#define DQ_ADAM_PART_MAXB 2048   // N > 1's fc update beside the main queue: a cap leaves it CUs
+#define DQ_ADAM_PART_MAXB 256   // N > 1's fc update beside the main queue: a cap leaves it CUs
 #endif
   hipLaunchKernelGGL(k_adam_part, dim3(std::min(elementwise_grid(n), DQ_ADAM_PART_MAXB)), dim3(256), 0,
                      (hipStream_t)stream,

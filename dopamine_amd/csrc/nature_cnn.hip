@@ -123,7 +123,7 @@ struct FcHeadOp {
     const int nt = 4 * g + wave;
     const int r = lane & 31, hh = lane >> 5, n = 32 * nt + r;
 #ifndef DQ_FCHEAD_EARLY_W2
-#define DQ_FCHEAD_EARLY_W2 1
+#define DQ_FCHEAD_EARLY_W2 0   // 1 measured slower with the 16-slab batch (round 4)
 #endif
     // B operand: lane r's 8 k of each half, straight from W2's row n (k contiguous) --
     // independent of the slab sums, so (DQ_FCHEAD_EARLY_W2) issued before them: one
@@ -149,7 +149,10 @@ struct FcHeadOp {
       const int64_t i = (int64_t)m * kHidden + 32 * j + c, MN = (int64_t)B * kHidden;
       const float4 bb = *reinterpret_cast<const float4*>(b1 + 32 * j + c);
       float4 s = *reinterpret_cast<const float4*>(ws + i);
-      if (nz <= 16) {
+#ifndef DQ_FCHEAD_SLAB_BATCH
+#define DQ_FCHEAD_SLAB_BATCH 0
+#endif
+      if (DQ_FCHEAD_SLAB_BATCH && nz <= 16) {
         // all (up to 16) slabs' loads in flight together, then the sum in slab order: one
         // memory round instead of one per 8 slabs (a runtime loop splits the batches)
         float4 v[15];
