@@ -371,6 +371,30 @@ struct Fc1EpiOpt<2> {       // centered RMSProp (DQN, config 2): DQ_FC1_EPI_RMS
                                           AdamHost{o}, 0)};
   }
 };
+
+// the same for fc2 (DQ_FC2_EPI): fc2's weight gradient + optimizer in one vector epilogue
+template <int kOpt>
+struct Fc2EpiOpt;
+template <>
+struct Fc2EpiOpt<1> {
+  static EpiGradAdamVec make(const dq_cnn_params* p, const dq_cnn_params* g, const dq_adam_args* o) {
+    const ptrdiff_t ow = p->fc2_w - o->var, ob = p->fc2_b - o->var;
+    return EpiGradAdamVec{g->fc2_w, g->fc2_b, kHidden, p->fc2_w, o->m + ow, o->v + ow, p->fc2_b,
+                          o->m + ob, o->v + ob,
+                          AdamDev{o->state, o->slot, o->lr, o->beta1, o->beta2, o->epsilon,
+                                  o->no_grad_store == 0}};
+  }
+};
+template <>
+struct Fc2EpiOpt<2> {
+  static EpiGradRmsVec make(const dq_cnn_params* p, const dq_cnn_params* g, const dq_adam_args* o) {
+    return EpiGradRmsVec{GradEpi<2>::make(g->fc2_w, g->fc2_b, kHidden, p->fc2_w, p->fc2_b,
+                                          AdamHost{o}, 0)};
+  }
+};
+#ifndef DQ_FC2_EPI
+#define DQ_FC2_EPI 0
+#endif
 #ifndef DQ_FC1_EPI_RMS
 #define DQ_FC1_EPI_RMS 1
 #endif
@@ -947,11 +971,26 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
         auto sum_c2a = ReduceOp<decltype(GE::make(0, 0, 0, 0, 0, opt, 0))>{
             ws + o2, nz3, 64, Conv2::K + 1,
             GE::make(g->conv2_w, g->conv2_b, Conv2::K, p->conv2_w, p->conv2_b, opt, 0)};
-        if (in(0)) group_r(c, rd(0), dX_fc2);
-        if (in(1)) group_r(c, rd(1), dW_fc2, dX_fc1);
+        // DQ_FC2_EPI: fc2's weight gradient moves from launch 1 to 2 with its optimizer in the
+        // GEMM's vector epilogue (instead of a float4 range op in launch 2): launch 1 keeps
+        // only dX fc1 (+ rider), one round of blocks at one 16-wave block per CU
+        auto dW_fc2a = gemm_op<4, 4, 1>(ColKScalar{dout, NO}, ColKOnes{a->h, kHidden},
+                                        Fc2EpiOpt<kOpt>::make(p, g, opt.a), NO, kHidden + 1, B, B);
 #ifndef DQ_ABL_B2
 #define DQ_ABL_B2 0
 #endif
+#ifndef DQ_FC2_OPT_LAUNCH
+#define DQ_FC2_OPT_LAUNCH 2
+#endif
+        constexpr bool kFc2Epi = DQ_FC2_EPI && DQ_ABL_B2 == 0 && DQ_FC1_SPLIT_L == 0 &&
+                                 DQ_FC2_OPT_LAUNCH == 2;
+        if (in(0)) group_r(c, rd(0), dX_fc2);
+        if (in(1)) {
+          if constexpr (kFc2Epi)
+            group_r(c, rd(1), dX_fc1);
+          else
+            group_r(c, rd(1), dW_fc2, dX_fc1);
+        }
         // DQ_ABL_B2 (timing experiments only, tools/build_variant.py; results are wrong):
         // launch 2 without  1: its rider  2: fc1's Adam epilogue (the GEMM, no stores)
         // 4: dX conv3  8: fc2's Adam part
@@ -970,12 +1009,11 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
             }
           }
         } else if (in(2)) {
-#ifndef DQ_FC2_OPT_LAUNCH
-#define DQ_FC2_OPT_LAUNCH 2
-#endif
           // fc2's optimizer part: launch 2 (its gradient is final after launch 1), or 4
           // (launch 2 holds the fc1 update's stream; nothing reads fc2_w before the next C)
-          if (DQ_FC1_SPLIT_L > 2 && kHeadFrom == 6)
+          if constexpr (kFc2Epi)
+            group_r(c, rd(2), dW_fc1a, dX_c3, dW_fc2a);
+          else if (DQ_FC1_SPLIT_L > 2 && kHeadFrom == 6)
             group_r(c, rd(2), dW_fc1lo, dX_c3, part(p->fc2_w, p->fc2_b + NO));
           else if (DQ_FC2_OPT_LAUNCH == 2 || kHeadFrom != 6)
             group_r(c, rd(2), dW_fc1a, dX_c3, part(p->fc2_w, p->fc2_b + NO));

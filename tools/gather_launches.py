@@ -22,9 +22,11 @@ def main():
   iters = int(sys.argv[2]) if len(sys.argv) > 2 else 400
   batch = int(sys.argv[3]) if len(sys.argv) > 3 else 32
   algo = batch * (2 * 4 * 7056 + 2 * 4 * 7056 * 4)
-  rows = sorted((s, e) for s, e, name, gx, wx in db.execute(
-      'select start, end, name, grid_x, workgroup_x from kernels')
-      if 'k_gather_nhwc4' in name and gx // max(wx, 1) == 8)
+  # the bench batch's grid only (8 x 2B blocks): the DQN chunk gather (8 x 8B) and the
+  # batch-1024 launches run the same kernel at other grids
+  rows = sorted((s, e) for s, e, name, gx, wx, gy, wy in db.execute(
+      'select start, end, name, grid_x, workgroup_x, grid_y, workgroup_y from kernels')
+      if 'k_gather_nhwc4' in name and gx // max(wx, 1) == 8 and gy // max(wy, 1) == 2 * batch)
   print('k_gather_nhwc4 launches at grid 8 x (B = %d): %d (expected 10 + 2 x %d)' %
         (batch, len(rows), iters))
   timed = rows[-iters:]
@@ -38,7 +40,8 @@ def main():
          'frac_mean_kernel': round(algo / (mean * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
          'frac_span': round(algo / (span * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
   if len(sys.argv) > 4:
-    line = json.loads(open(sys.argv[4]).read().strip().splitlines()[-1])
+    line = json.loads([ln for ln in open(sys.argv[4]).read().splitlines()
+                       if ln.startswith('{"metric"')][-1])   # rocprofv3 logs after the line
     r = line['roofline']
     out['bench_line_event_us'] = r['avg_launch_us']
     out['bench_line_frac'] = r['frac']
