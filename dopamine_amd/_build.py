@@ -21,9 +21,20 @@ def build_bf16(verbose=False):
   return build(verbose=verbose, out=BF16_LIB_PATH, extra=BF16_FLAGS)
 
 
+def build_all(verbose=False):
+  """Both libraries (the product and the bf16 throughput build): every translation unit of
+  the two compiled concurrently, then the two links."""
+  jobs = [_start(verbose, LIB_PATH, None, ()), _start(verbose, BF16_LIB_PATH, None, BF16_FLAGS)]
+  return [_finish(verbose, *j) for j in jobs]
+
+
 def build(verbose=False, out=None, sources=None, extra=()):
   """Compile the HIP sources into libdopamine_amd.so next to this file: one hipcc per
   translation unit, in parallel, then one link."""
+  return _finish(verbose, *_start(verbose, out, sources, extra))
+
+
+def _start(verbose, out, sources, extra):
   out = out or LIB_PATH
   flags = ['--offload-arch=' + ARCH, '-O3', '-fPIC', '-std=c++17', '-ffp-contract=off', '-Wall',
            '-I', os.path.join(_HERE, 'csrc')] + list(extra)
@@ -43,16 +54,21 @@ def build(verbose=False, out=None, sources=None, extra=()):
     if verbose:
       print(' '.join(cmd))
     procs.append((subprocess.Popen(cmd), cmd))
+  return out, objs, procs
+
+
+def _finish(verbose, out, objs, procs):
   for p, cmd in procs:
     if p.wait() != 0:
       raise subprocess.CalledProcessError(p.returncode, cmd)
-  cmd = ['hipcc', '--offload-arch=' + ARCH, '-shared', '-fPIC', '-o', out] + objs + ['-ldl']
+  tmp = out + '.tmp'            # linked aside, then renamed: a reader never sees half a file
+  cmd = ['hipcc', '--offload-arch=' + ARCH, '-shared', '-fPIC', '-o', tmp] + objs + ['-ldl']
   if verbose:
     print(' '.join(cmd))
   subprocess.run(cmd, check=True)
+  os.replace(tmp, out)
   return out
 
 
 if __name__ == '__main__':
-  build(verbose=True)
-  build_bf16(verbose=True)
+  build_all(verbose=True)

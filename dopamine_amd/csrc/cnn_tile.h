@@ -821,6 +821,8 @@ __device__ __forceinline__ bf16x8 peel8(float* v) {
 __device__ __forceinline__ f32x16 mfma_x6_lazy(const bf16x8& ah, const bf16x8& am, const bf16x8& al,
                                                float* bv, f32x16 acc) {
   const bf16x8 bh = peel8(bv);
+  // the bf16 throughput build: one product, as mfma_x6 (am / al are then dead code)
+  if (DQ_X6_PAIRS == 1) return __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc, 0, 0, 0);
   {

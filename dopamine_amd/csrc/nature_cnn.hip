@@ -55,6 +55,17 @@ struct GemmOp {
   EP e;
   int M, N, K, kchunk, gx, gy, gz;
   __device__ __forceinline__ void run(int blk, float* smem, int tid_base = 0) const {
+#ifndef DQ_GROUP_XCD
+#define DQ_GROUP_XCD 0
+#endif
+    if (DQ_GROUP_XCD && gz > 1) {
+      // split-K ops (a speed choice only): the dispatcher deals consecutive block ids round-
+      // robin over the 8 XCDs, so blocks with the same id mod 8 share an L2.  Give each such
+      // class a contiguous run of tiles, k slab slowest, so the tiles of one slab (which
+      // read the same k range of the shared operand) run on one XCD (bijective for any G)
+      const int G = gx * gy * gz, x = blk & 7, q = blk >> 3, per = G >> 3, rem = G & 7;
+      blk = (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + q;
+    }
     const int bx = blk % gx, by = (blk / gx) % gy, bz = blk / (gx * gy);
     igemm_block<WM, WN, WK, AL, BL, EP, kLate, cnn_x6<WM, WN, WK, AL>()>(a, b, e, M, N, K, kchunk,
                                                                       bx, by, bz, smem, tid_base);
@@ -524,7 +535,13 @@ void group_r(Ctx& c, const RiderDesc* r, Ops... ops) {
 // Tile shapes: WM = WN = 1 with WK k-bands sized so K takes one or two slices
 // (BKT = 32 * WK); split-K only where the grid would otherwise leave most of the
 // 256 CUs idle (weight streaming of fc1, the pixel-deep weight gradients).
-constexpr int kSplitFc1 = 16, kSplitConvW = 8, kSplitConv1W = 28;
+#ifndef DQ_SPLIT_CONVW
+#define DQ_SPLIT_CONVW 8     // conv2 / conv3 weight gradients: split-K slabs over B * 121
+#endif
+#ifndef DQ_SPLIT_CONV1W
+#define DQ_SPLIT_CONV1W 28   // conv1's over B * 441
+#endif
+constexpr int kSplitFc1 = 16, kSplitConvW = DQ_SPLIT_CONVW, kSplitConv1W = DQ_SPLIT_CONV1W;
 
 void forward(Ctx& c, const dq_cnn_params* p, int B, const float* x, dq_cnn_acts* a) {
   // conv1 / conv2 / conv3 + bias + ReLU  (implicit GEMM: M = pixels, N = out channels)
@@ -1022,10 +1039,31 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
         }
         if (kHeadFrom == 6) {
           if (in(3)) {
-            if (DQ_FC1_SPLIT_L == 3)
+#ifndef DQ_ABL_B3
+#define DQ_ABL_B3 0
+#endif
+            // DQ_ABL_B3 (timing experiments only, results wrong): launch 3 without
+            // 1: its rider (the gather)  2: dW conv3's slabs  4: the sub-pixel GEMMs
+            // 8: dW conv2's slabs
+            if constexpr (DQ_ABL_B3 != 0) {
+              auto w3 = dW_c3;
+              auto w2 = dW_c2;
+              auto s0 = sp00;
+              auto s1 = sp01;
+              auto s2 = sp10;
+              auto s3 = sp11;
+              if (DQ_ABL_B3 & 2) w3.gx = w3.gy = w3.gz = 0;
+              if (DQ_ABL_B3 & 8) w2.gx = w2.gy = w2.gz = 0;
+              if (DQ_ABL_B3 & 4) {
+                s0.gx = s0.gy = s0.gz = 0; s1.gx = s1.gy = s1.gz = 0;
+                s2.gx = s2.gy = s2.gz = 0; s3.gx = s3.gy = s3.gz = 0;
+              }
+              group_r(c, (DQ_ABL_B3 & 1) ? nullptr : rd(3), w3, s0, s1, s2, s3, w2);
+            } else if (DQ_FC1_SPLIT_L == 3) {
               group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11, dW_c2, dW_fc1hi);
-            else
+            } else {
               group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11, dW_c2);
+            }
           }
           if (in(4)) {
             if (DQ_FC1_SPLIT_L == 4)
