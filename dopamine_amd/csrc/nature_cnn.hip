@@ -90,7 +90,7 @@ struct PairOp {
   int blocks() const { return (op.blocks() + 1) / 2; }
 };
 #ifndef DQ_SP_PAIR
-#define DQ_SP_PAIR 0
+#define DQ_SP_PAIR 1   // round 4 session 2: +0.7% with the riders in launches 2-4
 #endif
 
 template <class EP, int T = kGroupT>
@@ -404,7 +404,7 @@ struct Fc2EpiOpt<2> {
   }
 };
 #ifndef DQ_FC2_EPI
-#define DQ_FC2_EPI 0
+#define DQ_FC2_EPI 1   // round 4 session 2: +0.8% with the riders in launches 2-4
 #endif
 #ifndef DQ_FC1_EPI_RMS
 #define DQ_FC1_EPI_RMS 1

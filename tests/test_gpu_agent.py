@@ -261,6 +261,43 @@ def test_learner_loop_chunks_equal_per_call_loop(kind):
       assert x == y
 
 
+@pytest.mark.parametrize('chunked', [False, True])
+def test_per_rider_launch_placements_are_bitwise_the_same(chunked):
+  """The PER riders' backward launches (write-back, sample, gather) are a schedule choice
+  only: (1, 2, 3), (2, 3, 4), (1, 3, 4) and (2, 2, 3) (write-back and sample chained in one
+  block of launch 2) give the same batches, parameters, target net, sum tree and RNG state,
+  bit for bit, per call and in the learner loop (target syncs inside chunks)."""
+  from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
+  res = []
+  for at in ((1, 2, 3), (2, 3, 4), (1, 3, 4), (2, 2, 3)):
+    random.seed(5); np.random.seed(5); torch.manual_seed(5)
+    old = DQNAgent.rider_launches
+    DQNAgent.rider_launches = at
+    try:
+      a = _rainbow(target_update_period=28)
+      idx = []
+      for n in (6, 5, 9):
+        if chunked:
+          a.train_gradient_steps(n)
+        else:
+          for _ in range(n * a.update_period):
+            a._train_step()
+        idx.append(a._replay.transition['indices'].cpu().numpy().copy())
+      a._discard_prefetch()
+      a._replay.memory.sync_rng()
+      res.append((np.stack(idx), a.online_convnet.fp.flat.cpu().numpy(),
+                  a.target_convnet.fp.flat.cpu().numpy(), a._replay.memory.sum_tree.nodes[-1].copy(),
+                  a._replay.transition['next_state'].cpu().numpy(), random.getstate()))
+    finally:
+      DQNAgent.rider_launches = old
+  for r in res[1:]:
+    for x, y in zip(res[0], r):
+      if isinstance(x, np.ndarray):
+        np.testing.assert_array_equal(x, y)
+      else:
+        assert x == y
+
+
 def test_chunk_gather_equals_per_step_gather_chunks():
   """DQN (uniform replay) learner loop: chunks whose K batches are drawn by one grouped
   sample and gathered by one K*B launch (chunk_gather) == chunks that sample and gather per

@@ -12,7 +12,11 @@ OUT=gpurun_out/${1:-ab}
 shift
 mkdir -p $OUT
 if [ -n "$DQ_TESTS" ]; then
-  for lib in "$@"; do
+  # DQ_TESTS_INTREE=1: the in-tree build's run first
+  for spec in $([ -n "$DQ_TESTS_INTREE" ] && echo dopamine_amd/libdopamine_amd.so) "$@"; do
+    # the build a spec runs on: "args:<flags>" the in-tree one, "<lib>|<flags>" that lib
+    lib=$spec
+    case "$spec" in args:*) continue;; *"|"*) lib=${spec%%|*};; esac
     n=$(basename $(dirname $lib))
     DOPAMINE_AMD_LIB=$lib timeout -k 10 600 python -u -m pytest $DQ_TESTS -m gpu -v \
       --timeout 300 --timeout-method thread > $OUT/tests_$n.log 2>&1
