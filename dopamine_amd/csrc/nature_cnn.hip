@@ -832,10 +832,18 @@ void backward_torso_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params*
                                  EpiPartial{ws + o1, 32, Conv1::K + 1}, 32, Conv1::K + 1, K1, ch1);
   auto sum_c1 = ReduceOp<EpiGrad>{ws + o1, nz1, 32, Conv1::K + 1,
                                   EpiGrad{g->conv1_w, g->conv1_b, Conv1::K}};
+#ifndef DQ_SP_PAIR_TORSO
+#define DQ_SP_PAIR_TORSO 0
+#endif
+  // DQ_SP_PAIR_TORSO: two of the 8-wave sub-pixel tiles per 16-wave block here too
+  auto tsp = [](auto op) {
+    if constexpr (DQ_SP_PAIR_TORSO != 0) return PairOp<decltype(op)>{op};
+    else return op;
+  };
   if constexpr (kOpt == 0) {
     group(c, dW_c3, dX_c3);
-    group(c, dW_c2, subpix_op<0, 0>(p, a, d, B), subpix_op<0, 1>(p, a, d, B),
-          subpix_op<1, 0>(p, a, d, B), subpix_op<1, 1>(p, a, d, B), sum_c3);
+    group(c, dW_c2, tsp(subpix_op<0, 0>(p, a, d, B)), tsp(subpix_op<0, 1>(p, a, d, B)),
+          tsp(subpix_op<1, 0>(p, a, d, B)), tsp(subpix_op<1, 1>(p, a, d, B)), sum_c3);
     group(c, dW_c1, sum_c2);
     group(c, sum_c1);
   } else {
@@ -849,8 +857,9 @@ void backward_torso_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params*
         ws + o1, nz1, 32, Conv1::K + 1,
         GE::make(g->conv1_w, g->conv1_b, Conv1::K, p->conv1_w, p->conv1_b, opt, 1)};
     group(c, dW_c3, dX_c3, part(head_begin, hm));
-    group(c, dW_c2, subpix_op<0, 0>(p, a, d, B), subpix_op<0, 1>(p, a, d, B),
-          subpix_op<1, 0>(p, a, d, B), subpix_op<1, 1>(p, a, d, B), sum_c3, part(hm, head_end));
+    group(c, dW_c2, tsp(subpix_op<0, 0>(p, a, d, B)), tsp(subpix_op<0, 1>(p, a, d, B)),
+          tsp(subpix_op<1, 0>(p, a, d, B)), tsp(subpix_op<1, 1>(p, a, d, B)), sum_c3,
+          part(hm, head_end));
     group(c, dW_c1, sum_c2o, part(p->conv3_w, head_begin));
     group(c, sum_c1o);
   }
