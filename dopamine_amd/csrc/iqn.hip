@@ -324,6 +324,20 @@ void backward(Ctx& c, const dq_iqn_head* hp, const dq_iqn_head* hg, int B, int n
   // the bias gradient of the embedding from the dX epilogue (d tiled's buffer, unused when
   // fuse_tile, holds the (R/128, F) column partials)
   const bool we_narrow = fuse_tile;
+  auto dw1 = [&]() {
+    if (a->x)
+      gemm_iqn<4, 4, 1>(c, ColK{d->dh, H}, ColKOnes{a->x, F}, EpiGrad{hg->fc1_w, hg->fc1_b, F}, H,
+                        F + 1, R, kSplitW1);
+    else
+      gemm_iqn<4, 4, 1>(c, ColK{d->dh, H}, ColKOnesHad{a->emb, state, B},
+                        EpiGrad{hg->fc1_w, hg->fc1_b, F}, H, F + 1, R, kSplitW1);
+  };
+#ifndef DQ_IQN_DW1_FIRST
+#define DQ_IQN_DW1_FIRST 0
+#endif
+  // DQ_IQN_DW1_FIRST: dW1 (it needs only d h) before dX, so on the two-stream step the
+  // store-bound target embedding runs beside dW1's matrix work and the target FC1 beside dX
+  if (DQ_IQN_DW1_FIRST) dw1();
   if (fuse_tile) {
     if (!c.dry)
       hipLaunchKernelGGL((k_igemm<4, 4, 1, RowKQ, ColK, EpiDxQ, kDxX6>), dim3((R + 127) / 128, (F + 127) / 128),
@@ -334,12 +348,7 @@ void backward(Ctx& c, const dq_iqn_head* hp, const dq_iqn_head* hg, int B, int n
     gemm_form<4, 4, 1, kDxX6>(c, RowK{d->dh, H}, ColK{hp->fc1_w, F},
                               EpiDx{d->dtl, d->dpre, a->emb, state, B}, R, F, H, 1);
   }
-  if (a->x)
-    gemm_iqn<4, 4, 1>(c, ColK{d->dh, H}, ColKOnes{a->x, F}, EpiGrad{hg->fc1_w, hg->fc1_b, F}, H,
-                  F + 1, R, kSplitW1);
-  else
-    gemm_iqn<4, 4, 1>(c, ColK{d->dh, H}, ColKOnesHad{a->emb, state, B},
-                  EpiGrad{hg->fc1_w, hg->fc1_b, F}, H, F + 1, R, kSplitW1);
+  if (!DQ_IQN_DW1_FIRST) dw1();
   if (we_narrow) {           // dWe over the E cosine columns, dbe from the row-tile partials
     gemm_iqn<4, 2, 2>(c, ColK{d->dpre, F}, ColK{a->cos, E}, EpiGrad{hg->emb_w, hg->emb_b, E}, F, E, R,
                   kSplitWe);
