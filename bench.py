@@ -63,6 +63,9 @@ def parse():
   ap.add_argument('--branch-first', action='store_true',
                   help='N > 1: capture the fc bucket\'s branch before the backward tail '
                        '(DQNAgent.branch_first; a schedule experiment)')
+  ap.add_argument('--chunk-steps', type=int, default=None,
+                  help='override DQNAgent._UNROLL: consecutive gradient steps per learner-loop '
+                       'HIP graph (a schedule experiment)')
   ap.add_argument('--rider-launches', default=None,
                   help='override DQNAgent.rider_launches, e.g. 2,3,4: the backward launches of the '
                        'PER write-back, sample and gather riders (a schedule experiment)')
@@ -462,6 +465,9 @@ def main():
   if args.comm_priority is not None:
     from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
     DQNAgent.comm_priority = int(args.comm_priority)
+  if args.chunk_steps is not None:
+    from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
+    DQNAgent._UNROLL = int(args.chunk_steps)
   if args.rider_launches is not None:
     from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
     DQNAgent.rider_launches = tuple(int(x) for x in args.rider_launches.split(','))
