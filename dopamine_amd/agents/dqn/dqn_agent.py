@@ -459,7 +459,10 @@ class DQNAgent(object):
     if self._gather_plan is not None and len(riders) == 2 and self.chunk_gather_launch > 2:
       empty = [_lib.Rider() for _ in range(self.chunk_gather_launch - 2)]
       return riders[:1] + empty + riders[1:]
-    if len(riders) == 3:                              # PER: write-back, sample, gather
+    if len(riders) == 3 and self._fused():            # PER: write-back, sample, gather
+      # (the fused head's backward starts at launch 1 and its target conv1 rides in launch 5;
+      # the plain schedule's starts at 0 with the target head from launch 3, so there the
+      # riders keep launches 0, 1, 2)
       at = self.rider_launches or (1, self.sample_launch, self.sample_launch + 1)
       if tuple(at) != (1, 2, 3):
         # the target conv1 (launch 5) reads the gather; write-back and sample in ONE launch
