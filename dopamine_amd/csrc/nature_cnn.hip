@@ -1011,8 +1011,11 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
         constexpr bool kFc2Epi = DQ_FC2_EPI && DQ_ABL_B2 == 0 && DQ_FC1_SPLIT_L == 0 &&
                                  DQ_FC2_OPT_LAUNCH == 2;
         if (in(0)) group_r(c, rd(0), dX_fc2);
+        // DQ_FC2_EPI == 2: fc2's gradient + optimizer epilogue in launch 1 beside dX fc1
         if (in(1)) {
-          if constexpr (kFc2Epi)
+          if constexpr (kFc2Epi && DQ_FC2_EPI == 2)
+            group_r(c, rd(1), dX_fc1, dW_fc2a);
+          else if constexpr (kFc2Epi)
             group_r(c, rd(1), dX_fc1);
           else
             group_r(c, rd(1), dW_fc2, dX_fc1);
@@ -1037,7 +1040,9 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
         } else if (in(2)) {
           // fc2's optimizer part: launch 2 (its gradient is final after launch 1), or 4
           // (launch 2 holds the fc1 update's stream; nothing reads fc2_w before the next C)
-          if constexpr (kFc2Epi)
+          if constexpr (kFc2Epi && DQ_FC2_EPI == 2)
+            group_r(c, rd(2), dW_fc1a, dX_c3);
+          else if constexpr (kFc2Epi)
             group_r(c, rd(2), dW_fc1a, dX_c3, dW_fc2a);
           else if (DQ_FC1_SPLIT_L > 2 && kHeadFrom == 6)
             group_r(c, rd(2), dW_fc1lo, dX_c3, part(p->fc2_w, p->fc2_b + NO));

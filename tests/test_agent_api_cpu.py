@@ -95,3 +95,36 @@ def test_linearly_decaying_epsilon():
   """dqn-test 297-311 on the agent module's own function."""
   for step, expected in [(0, 1.0), (16, 0.91), (107, 0.1)]:
     assert abs(dqn_agent.linearly_decaying_epsilon(100, step, 6, 0.1) - expected) < 0.01
+
+
+class _PlaceStub:
+  """The attributes DQNAgent._place_riders reads (no device, no replay)."""
+  _gather_plan = None
+  chunk_gather_launch = 3
+  sample_launch = 2
+
+  def __init__(self, fused, at):
+    self._f, self.rider_launches = fused, at
+
+  def _fused(self):
+    return self._f
+
+
+def test_per_rider_placement_lists():
+  """The PER riders (write-back, sample, gather) of the fused schedule go to backward launches
+  rider_launches (rider i of the list rides in launch 1 + i; empty dq_riders in between); the
+  plain schedule (target head from launch 3) keeps its launches 0, 1, 2 whatever the knob;
+  a gather at or after the target conv1's launch 5 is refused."""
+  from dopamine_amd import _lib
+  wb, smp, gat = _lib.Rider(), _lib.Rider(), _lib.Rider()
+  wb.words[0], smp.words[0], gat.words[0] = 11, 12, 13     # tags only (kind words unread here)
+  place = dqn_agent.DQNAgent._place_riders
+  tags = lambda rs: [int(r.words[0]) for r in rs]
+  assert tags(place(_PlaceStub(True, (2, 3, 4)), [wb, smp, gat])) == [0, 11, 12, 13]
+  assert tags(place(_PlaceStub(True, (1, 3, 4)), [wb, smp, gat])) == [11, 0, 12, 13]
+  assert tags(place(_PlaceStub(True, (1, 2, 3)), [wb, smp, gat])) == [11, 12, 13]
+  assert tags(place(_PlaceStub(True, None), [wb, smp, gat])) == [11, 12, 13]
+  assert tags(place(_PlaceStub(False, (2, 3, 4)), [wb, smp, gat])) == [11, 12, 13]
+  with pytest.raises(AssertionError):
+    place(_PlaceStub(True, (2, 3, 5)), [wb, smp, gat])
+  assert dqn_agent.DQNAgent.rider_launches == (2, 3, 4)
