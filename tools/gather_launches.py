@@ -29,11 +29,11 @@ def main():
       if 'k_gather_nhwc4' in name and gx // max(wx, 1) == 8 and gy // max(wy, 1) == 2 * batch)
   print('k_gather_nhwc4 launches at grid 8 x (B = %d): %d (expected 10 + 2 x %d)' %
         (batch, len(rows), iters))
-  # the timed replay: the last run of `iters` back-to-back launches (gaps < 50 us); launches
+  # the timed replay: the last run of `iters` back-to-back launches (gaps < 2 ms); launches
   # of the same grid elsewhere in the run (e.g. eager priming steps) fall outside it
   runs, cur = [], [rows[0]]
   for r in rows[1:]:
-    if r[0] - cur[-1][1] < 50_000:
+    if r[0] - cur[-1][1] < 2_000_000:
       cur.append(r)
     else:
       runs.append(cur)
