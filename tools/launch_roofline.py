@@ -45,10 +45,11 @@ DH = 51 * 512 * B                                      # d h = dlogits . W2 (cho
 # the step's launches in order from the loss kernel and what they compute
 LAUNCHES = [
     ('C  k_c51', 'loss + d h', DH),
-    ('B1', 'dW fc2 / dX fc1 + PER write-back', DW['fc2'] + DX['fc1']),
-    ('B2', 'dW fc1 + its Adam (epilogue) / dX conv3 + PER sample + Adam fc2', DW['fc1'] + DX['conv3']),
-    ('B3', 'dW conv3 / dX conv2 / dW conv2 + gather', DW['conv3'] + DX['conv2'] + DW['conv2']),
-    ('B4', 'sum conv3 / dW conv1', DW['conv1']),
+    ('B1', 'dX fc1', DX['fc1']),
+    ('B2', 'dW fc1 / dW fc2, their Adam (epilogues) / dX conv3 + PER write-back',
+     DW['fc1'] + DW['fc2'] + DX['conv3']),
+    ('B3', 'dW conv3 / dX conv2 / dW conv2 + PER sample', DW['conv3'] + DX['conv2'] + DW['conv2']),
+    ('B4', 'sum conv3 / dW conv1 + gather', DW['conv1']),
     ('B5', 'sum conv2/conv1 + Adam conv1-3 + target conv1', C1),
     ('F1', 'conv1', C1),
     ('F2', 'conv2 + target conv2', 2 * C2),
