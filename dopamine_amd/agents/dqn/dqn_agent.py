@@ -452,9 +452,10 @@ class DQNAgent(object):
     self._ptgt[c] = self._target_dict(tg)
 
   def _place_riders(self, riders):
-    """Rider i rides in backward launch first + i, in the recorded order (PER write-back,
-    sample, gather).  Other placements were measured and not kept.  A chunk
-    gather's K * B gather (a chunk's first step) rides in backward launch
+    """Rider i of the returned list rides in backward launch first + i.  The PER riders
+    (write-back, sample, gather, in that order) of the fused schedule go to rider_launches
+    (default (2, 3, 4); the other placements measured are in DESIGN.md 4.2; all are bitwise
+    the same).  A chunk gather's K * B gather (a chunk's first step) rides in backward launch
     chunk_gather_launch (it must precede the next batch's target head, launch 5)."""
     if self._gather_plan is not None and len(riders) == 2 and self.chunk_gather_launch > 2:
       empty = [_lib.Rider() for _ in range(self.chunk_gather_launch - 2)]
