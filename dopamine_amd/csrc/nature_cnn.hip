@@ -89,6 +89,10 @@ struct PairOp {
   }
   int blocks() const { return (op.blocks() + 1) / 2; }
 };
+template <class T>
+struct IsPairOp : std::false_type {};
+template <class O>
+struct IsPairOp<PairOp<O>> : std::true_type {};
 #ifndef DQ_SP_PAIR
 #define DQ_SP_PAIR 1   // round 4 session 2: +0.7% with the riders in launches 2-4
 #endif
@@ -1066,11 +1070,16 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
               auto s1 = sp01;
               auto s2 = sp10;
               auto s3 = sp11;
-              if (DQ_ABL_B3 & 2) w3.gx = w3.gy = w3.gz = 0;
-              if (DQ_ABL_B3 & 8) w2.gx = w2.gy = w2.gz = 0;
+              auto none = [](auto& o) {       // an op with no blocks (a GemmOp, or a PairOp's)
+                if constexpr (IsPairOp<std::decay_t<decltype(o)>>::value)
+                  o.op.gx = o.op.gy = o.op.gz = 0;
+                else
+                  o.gx = o.gy = o.gz = 0;
+              };
+              if (DQ_ABL_B3 & 2) none(w3);
+              if (DQ_ABL_B3 & 8) none(w2);
               if (DQ_ABL_B3 & 4) {
-                s0.gx = s0.gy = s0.gz = 0; s1.gx = s1.gy = s1.gz = 0;
-                s2.gx = s2.gy = s2.gz = 0; s3.gx = s3.gy = s3.gz = 0;
+                none(s0); none(s1); none(s2); none(s3);
               }
               group_r(c, (DQ_ABL_B3 & 1) ? nullptr : rd(3), w3, s0, s1, s2, s3, w2);
             } else if (DQ_FC1_SPLIT_L == 3) {
