@@ -31,7 +31,7 @@ import torch.distributed as dist  # noqa: E402
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md, HBM3E spec peak
 
 
-def parse():
+def parse(argv=None):
   ap = argparse.ArgumentParser()
   ap.add_argument('--gpus', type=int, default=1)
   ap.add_argument('--steps', type=int, default=300)
@@ -48,33 +48,11 @@ def parse():
                   help='drive the agent by update_period _train_step() calls per gradient '
                        'step (one graph replay per step) instead of train_gradient_steps')
   ap.add_argument('--gather-iters', type=int, default=400)
-  ap.add_argument('--fuse-opt', type=int, default=None,
-                  help='override the agent default fuse_optimizer (0/1)')
-  ap.add_argument('--ride', type=int, default=None,
-                  help='override the agent default ride_replay (0/1)')
-  ap.add_argument('--split-c51', type=int, default=None,
-                  help='override RainbowAgent.split_c51 (0/1): the C51 target half riding in '
-                       'the forward (head_from 8) or inside the loss kernel')
   ap.add_argument('--zero', type=int, default=None,
                   help='N > 1: time only the replicated all-reduce schedule (0) or only ZeRO-1 '
                        'for the fc bucket (1: DQNAgent shard_optimizer -- reduce-scatter, TF1 '
                        'Adam on the rank\'s slice, all-gather); default: both, headline from the '
                        'faster')
-  ap.add_argument('--branch-first', action='store_true',
-                  help='N > 1: capture the fc bucket\'s branch before the backward tail '
-                       '(DQNAgent.branch_first; a schedule experiment)')
-  ap.add_argument('--chunk-steps', type=int, default=None,
-                  help='override DQNAgent._UNROLL: consecutive gradient steps per learner-loop '
-                       'HIP graph (a schedule experiment)')
-  ap.add_argument('--rider-launches', default=None,
-                  help='override DQNAgent.rider_launches, e.g. 2,3,4: the backward launches of the '
-                       'PER write-back, sample and gather riders (a schedule experiment)')
-  ap.add_argument('--sample-launch', type=int, default=None,
-                  help='override DQNAgent.sample_launch (2/3): the backward launch the PER '
-                       'sample rides in (a schedule experiment)')
-  ap.add_argument('--comm-priority', type=int, default=None,
-                  help='override DQNAgent.comm_priority (0 / -1): the N > 1 comm stream\'s HIP '
-                       'priority (a schedule experiment)')
   ap.add_argument('--comm', choices=('native', 'torch'), default='native',
                   help='N > 1 over RCCL: the learner\'s own communicators (parallel.RcclComm) '
                        'or torch.distributed\'s collectives')
@@ -85,7 +63,7 @@ def parse():
                   help='one rank only: run the N > 1 learner schedule over a one-rank RCCL group '
                        'with every collective executed (a hardware check of the data-parallel '
                        'path on a one-GPU box; not the bench line)')
-  return ap.parse_args()
+  return ap.parse_args(argv)
 
 
 def fill_synthetic(mem, A, seed, priority=None):
@@ -147,16 +125,31 @@ def build_iqn_breakout(device, **kw):
 
 
 MIN_PRE_STEPS = 100
+# N > 1: every blocking phase (rendezvous, learner construction with its rank-0 broadcast,
+# the barriers and collectives of the timed steps) must complete within DEADLINE_S seconds,
+# else the rank reports which one and exits (parallel.Deadline): a cross-rank ordering bug
+# or a dead peer ends the run instead of hanging it
+DEADLINE_S = float(os.environ.get('DQ_DEADLINE_S', '600'))
+# rehearsal only (DQ_BENCH_REHEARSE=1, gloo on one GPU): this group rank withholds the barrier
+# before the timed window, so the other ranks' deadline fires (tests/test_gpu_rccl.py)
+WITHHOLD_RANK = (int(os.environ['DQ_BENCH_WITHHOLD_RANK'])
+                 if os.environ.get('DQ_BENCH_REHEARSE') == '1'
+                 and 'DQ_BENCH_WITHHOLD_RANK' in os.environ else None)
 
 
-def timed_steps(agent, steps, warmup, per_call=False, pg=None):
+def timed_steps(agent, steps, warmup, per_call=False, pg=None, deadline=None):
   """The bench protocol on one agent: untimed priming, whatever ``warmup`` is, until every
   graph the timed loop replays is captured (both step parities, the 4-step chunk graphs of
   both starting parities) and the device has been busy for at least MIN_PRE_STEPS steps
   (its clocks ramp under load: a 20-step window after 5 warmup steps read 7% low); then
   the warmup; then exactly ``steps`` gradient steps between barriers + synchronize.  No
   cyclic-garbage collection pass inside the window (a full pass over a torch process's
-  objects takes milliseconds).  Returns (elapsed seconds, priming steps)."""
+  objects takes milliseconds).  deadline (N > 1): a parallel.Deadline armed for each
+  blocking phase.  Returns (elapsed seconds, priming steps)."""
+  def phase(label):
+    if deadline is not None:
+      deadline.phase(label, DEADLINE_S)
+
   def grad_steps(n):
     if per_call:
       for _ in range(n):
@@ -169,20 +162,28 @@ def timed_steps(agent, steps, warmup, per_call=False, pg=None):
   gc.disable()
   try:
     prime = 0
+    phase('priming (graph capture, steps with their fc / conv bucket all-reduces)')
     while ((not agent.graphs_primed() or prime + warmup < MIN_PRE_STEPS) and prime < 400):
       grad_steps(5)
       prime += 5
     grad_steps(warmup)
     torch.cuda.synchronize()
     if pg is not None:
+      phase('the barrier before the timed window')
+      if WITHHOLD_RANK == dist.get_rank(pg):
+        time.sleep(DEADLINE_S + 60)     # rehearsal only: this rank never joins the barrier
       dist.barrier()
     torch.cuda.synchronize()
+    phase('the timed window (%d steps, each with its fc / conv bucket all-reduces)' % steps)
     t0 = time.perf_counter()
     grad_steps(steps)
     torch.cuda.synchronize()
     if pg is not None:
+      phase('the barrier after the timed window')
       dist.barrier()
     elapsed = time.perf_counter() - t0
+    if deadline is not None:
+      deadline.done()
   finally:
     gc.enable()
   return elapsed, prime
@@ -430,8 +431,15 @@ def cpu_baseline(seconds, A, batch):
                     (k, dt, threads, cpu_model(), threads, os.cpu_count() or 0)}
 
 
-def main():
-  args = parse()
+# constructor overrides of the benchmarked agent and a note of changed agent-class
+# attributes: both empty for the bench line (the product defaults); tools/bench_ab.py sets
+# schedule experiments here and on the agent classes
+AGENT_OVERRIDES = {}
+CLASS_OVERRIDES = {}
+
+
+def main(argv=None):
+  args = parse(argv)
   if args.bf16_child:
     return bf16_child(args)
   world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -444,7 +452,12 @@ def main():
     local = 0
   torch.cuda.set_device(local)
   dev = torch.device('cuda', local)
-  pg = None
+  pg = deadline = None
+  if world > 1 or args.force_dist:
+    from dopamine_amd import parallel
+    deadline = parallel.Deadline(rank)
+    deadline.phase('init_process_group (rendezvous at %s:%s)' % (
+        os.environ.get('MASTER_ADDR', '127.0.0.1'), os.environ.get('MASTER_PORT', '?')), DEADLINE_S)
   if world > 1:
     os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
     if rehearse:
@@ -453,30 +466,11 @@ def main():
       dist.init_process_group('nccl', device_id=dev)
     pg = dist.group.WORLD
   elif args.force_dist:
-    from dopamine_amd import parallel
     parallel.FORCE_COLLECTIVES = True
     os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
     os.environ.setdefault('MASTER_PORT', '29533')
     dist.init_process_group('nccl', rank=0, world_size=1, device_id=dev)
     pg = dist.group.WORLD
-  if args.branch_first:
-    from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
-    DQNAgent.branch_first = True
-  if args.comm_priority is not None:
-    from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
-    DQNAgent.comm_priority = int(args.comm_priority)
-  if args.chunk_steps is not None:
-    from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
-    DQNAgent._UNROLL = int(args.chunk_steps)
-  if args.rider_launches is not None:
-    from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
-    DQNAgent.rider_launches = tuple(int(x) for x in args.rider_launches.split(','))
-  if args.sample_launch is not None:
-    from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
-    DQNAgent.sample_launch = int(args.sample_launch)
-  if args.split_c51 is not None:
-    from dopamine_amd.agents.rainbow.rainbow_agent import RainbowAgent
-    RainbowAgent.split_c51 = bool(args.split_c51)
   # N > 1: the replicated all-reduce schedule and ZeRO-1 are both timed, one
   # after the other on fresh agents, and the headline is the faster (both are reported)
   zeros = [0, 1] if (pg is not None and args.zero is None) else [int(args.zero or 0)]
@@ -488,24 +482,26 @@ def main():
       del agent
       gc.collect()
       torch.cuda.empty_cache()
+    if deadline is not None:
+      deadline.phase('building the learner (RCCL communicators, rank-0 broadcast)', DEADLINE_S)
     agent = build_agent(args.actions, args.capacity, args.batch, dev, pg=pg,
                         use_hip_graph=not args.no_graph, native_comm=args.comm == 'native',
-                        **({} if args.fuse_opt is None else {'fuse_optimizer': bool(args.fuse_opt)}),
-                        **({} if args.ride is None else {'ride_replay': bool(args.ride)}),
-                        **({'shard_optimizer': True} if zero else {}))
+                        **AGENT_OVERRIDES, **({'shard_optimizer': True} if zero else {}))
     import random
     random.seed(0 + rank)
     fill_synthetic(agent._replay.memory, args.actions, seed=1 + rank)
     torch.cuda.synchronize()
-    elapsed, prime = timed_steps(agent, args.steps, args.warmup, args.per_call, pg)
+    elapsed, prime = timed_steps(agent, args.steps, args.warmup, args.per_call, pg, deadline)
     per_rank = [elapsed]
     if pg is not None:
+      deadline.phase('the all_reduce of the per-rank times', DEADLINE_S)
       t = torch.zeros(dist.get_world_size(pg), dtype=torch.float64,
                       device='cpu' if rehearse else dev)
       t[dist.get_rank(pg)] = elapsed
       dist.all_reduce(t, op=dist.ReduceOp.SUM)
       per_rank = [float(x) for x in t.cpu()]
       elapsed = max(per_rank)
+      deadline.done()
     agent._replay.memory.sync_rng()   # raises if the device latched a sampling error
     loss = agent.mean_loss()
     assert np.isfinite(loss), 'non-finite loss'
@@ -546,6 +542,7 @@ def main():
     cpu = cpu_baseline(args.cpu_seconds, args.actions, args.batch)
 
   if rank == 0:
+    from dopamine_amd import _lib
     value = world * args.steps / elapsed
     line = {
         'metric': 'gradient-steps/sec (Rainbow, batch=32, 1M-transition buffer)',
@@ -574,6 +571,11 @@ def main():
         'cpu_baseline': cpu,
         'final_mean_loss': round(loss, 5),
         'gc_disabled_in_timed_window': True,
+        # the library that ran: its recorded -D flags ("" = the product build; _lib refuses
+        # any other unless DQ_DIAGNOSTIC_BUILD=1)
+        'build': {'library': os.path.relpath(_lib.LIB_PATH, ROOT), 'flags': _lib.BUILD_FLAGS,
+                  'overrides': {k: str(v) for k, v in
+                                dict(AGENT_OVERRIDES, **CLASS_OVERRIDES).items()} or None},
         # N > 1 (or --force-dist): every data-parallel schedule timed, the headline the faster
         'schedules': schedules if pg is not None else None,
         # supplementary: BASELINE configs 2 and 5 (N = 1), same protocol, not the metric
@@ -583,7 +585,9 @@ def main():
     }
     print(json.dumps(line), flush=True)
   if pg is not None:
+    deadline.phase('destroy_process_group', DEADLINE_S)
     dist.destroy_process_group()
+    deadline.close()
 
 
 if __name__ == '__main__':

@@ -6,9 +6,10 @@ this module raises at import time -- there is no CPU fallback.
 import ctypes
 import os
 
+from dopamine_amd import _build
 from dopamine_amd._build import HEADER, LIB_PATH  # noqa: F401
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 OK = 0
 (ST_OK, ST_EMPTY_TREE, ST_MAX_ATTEMPTS, ST_TAPE_EXHAUSTED, ST_NEG_PRIORITY, ST_TOO_FEW, ST_BAD_INDEX,
  ST_BROADCAST) = range(8)
@@ -111,6 +112,7 @@ _D = ctypes.c_double
 # name -> argtypes (restype int unless noted); mirrors include/dopamine_amd.h
 SIGNATURES = {
     'dq_abi_version': [],
+    'dq_build_flags': [],
     'dq_last_error': [],
     'dq_sumtree_depth': [_I64],
     'dq_replay_create': [ctypes.POINTER(Config), ctypes.POINTER(Storage), ctypes.POINTER(_P)],
@@ -203,7 +205,7 @@ SIGNATURES = {
     'dq_comm_all_gather': [_P, _P, _I64, _P],
     'dq_comm_version': [],
 }
-RESTYPES = {'dq_last_error': ctypes.c_char_p, 'dq_cnn_workspace_floats': ctypes.c_size_t,
+RESTYPES = {'dq_last_error': ctypes.c_char_p, 'dq_build_flags': ctypes.c_char_p, 'dq_cnn_workspace_floats': ctypes.c_size_t,
             'dq_iqn_workspace_floats': ctypes.c_size_t,
             'dq_cnn_fc2_parts_offset': ctypes.c_size_t}
 
@@ -224,10 +226,20 @@ def _load():
     fn.restype = RESTYPES.get(name, ctypes.c_int)
   if lib.dq_abi_version() != ABI_VERSION:
     raise ImportError('dopamine_amd ABI mismatch: lib %d, python %d' % (lib.dq_abi_version(), ABI_VERSION))
-  return lib
+  flags = lib.dq_build_flags().decode()
+  # the product library carries no extra flags; the bf16 throughput build (bench.py's
+  # separate row) its own; anything else (a timing or stamp build) only when asked for
+  allowed = {_build.flags_string(_build.PRODUCT_FLAGS): os.path.realpath(_build.PRODUCT_LIB_PATH),
+             _build.flags_string(_build.BF16_FLAGS): os.path.realpath(_build.BF16_LIB_PATH)}
+  if (allowed.get(flags) != os.path.realpath(LIB_PATH)
+      and os.environ.get('DQ_DIAGNOSTIC_BUILD') != '1'):
+    raise ImportError('dopamine_amd: %s was built with flags %r, not a product or bf16 '
+                      'throughput build (set DQ_DIAGNOSTIC_BUILD=1 for a diagnostic run)'
+                      % (LIB_PATH, flags))
+  return lib, flags
 
 
-lib = _load()
+lib, BUILD_FLAGS = _load()
 
 
 def check(rc, what=''):

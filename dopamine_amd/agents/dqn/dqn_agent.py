@@ -467,8 +467,12 @@ class DQNAgent(object):
       at = self.rider_launches or (1, self.sample_launch, self.sample_launch + 1)
       if tuple(at) != (1, 2, 3):
         # the target conv1 (launch 5) reads the gather; write-back and sample in ONE launch
-        # run chained in one block (dq_rider_chain: the draw after the write-back)
-        assert 1 <= at[0] <= at[1] < at[2] <= 4, at
+        # run chained in one block (dq_rider_chain: the draw after the write-back).  Any
+        # other order would race (e.g. the gather beside the conv1 that reads it): an error
+        # under python -O too
+        if not (len(at) == 3 and 1 <= at[0] <= at[1] < at[2] <= 4):
+          raise ValueError('rider_launches %r: need 1 <= write-back <= sample < gather <= 4'
+                           % (tuple(at),))
         placed = [_lib.Rider() for _ in range(at[2])]
         if at[0] == at[1]:
           chained = _lib.Rider()

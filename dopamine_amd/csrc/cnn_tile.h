@@ -53,10 +53,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, kOOB, 0x00020000);
 }
 __device__ __forceinline__ float4 bload4(const float* base, int off, bool ok) {   // off in floats
-#ifdef DQ_ABLATE_LOADS   // timing experiments only: operands without memory traffic
-  const float f = ok ? (float)off * 1e-9f : 0.0f;
-  return make_float4(f, f, f, f);
-#endif
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc(base), ok ? off * 4 : kOOB, 0, 0);
   return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
@@ -425,36 +421,18 @@ struct EpiGradAdamVec {
     e.gb += r0; e.b += r0; e.mb += r0; e.vb += r0;
     return e;
   }
-#ifndef DQ_VEC_PRE
-#define DQ_VEC_PRE 1
-#endif
   // two-phase vector form (kVecPre): the next row group's parameter / moment loads are
   // issued before this group's stores (the compiler cannot tell the rows apart and would
   // otherwise serialise each group's loads behind the previous group's stores)
-  static constexpr bool kVecPre = DQ_VEC_PRE != 0;
+  static constexpr bool kVecPre = true;
   struct VPre {
     float4 w, m, v;
   };
-#ifndef DQ_ADAM_NT
-#define DQ_ADAM_NT 0   // 1: the streamed state's stores non-temporal; 2: its loads too
-#endif
-  __device__ static __forceinline__ float4 ldst(const float* p) {
-    if constexpr (DQ_ADAM_NT >= 2) {
-      typedef float f4v __attribute__((ext_vector_type(4)));
-      const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
-      return make_float4(v.x, v.y, v.z, v.w);
-    } else {
-      return ld4(p);
-    }
-  }
+  // the streamed state's loads / stores with the default cache policy (non-temporal stores,
+  // or loads and stores, measured no faster in round 4)
+  __device__ static __forceinline__ float4 ldst(const float* p) { return ld4(p); }
   __device__ static __forceinline__ void stst(float* p, float4 v) {
-    if constexpr (DQ_ADAM_NT >= 1) {
-      typedef float f4v __attribute__((ext_vector_type(4)));
-      const f4v x = {v.x, v.y, v.z, v.w};
-      __builtin_nontemporal_store(x, reinterpret_cast<f4v*>(p));
-    } else {
-      *reinterpret_cast<float4*>(p) = v;
-    }
+    *reinterpret_cast<float4*>(p) = v;
   }
   __device__ __forceinline__ VPre vpre(int m, int n) const {
     if (n >= nw) return VPre{zero4(), zero4(), zero4()};
@@ -721,17 +699,13 @@ __device__ __forceinline__ void group_coord(int g, int& rr, int& kk) {
 // accumulators are then summed through LDS by all threads, each output element
 // in wave order (deterministic), and handed to the epilogue with consecutive
 // threads on consecutive columns.
-// compile with -DDQ_SHARED_STAGING=1 for the block-shared operand staging (A/B builds)
-#ifndef DQ_SHARED_STAGING
-#define DQ_SHARED_STAGING 0
-#endif
 
 template <int WM, int WN, int WK>
 struct Tile {
   static constexpr int T = 64 * WM * WN * WK;
   static constexpr int BM = 32 * WM, BN = 32 * WN, BKT = 32 * WK;
   // one wave per k band (WM = WN = 1): each wave stages only its own band, 16 k at a time
-  static constexpr bool kPrivate = WM == 1 && WN == 1 && WK > 1 && !DQ_SHARED_STAGING;
+  static constexpr bool kPrivate = WM == 1 && WN == 1 && WK > 1;
   template <class AL, class BL>
   static constexpr int lds() {      // operand slices, or the WK > 1 reduction scratch
     const int sa = BM + (AL::kFast ? 1 : 4), sb = BN + (BL::kFast ? 1 : 4);
@@ -758,10 +732,6 @@ typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
 typedef float f32x2v __attribute__((ext_vector_type(2)));
 // two fp32 -> their hi / mid / lo bf16 pieces, each pair packed (element 0 low)
 __device__ __forceinline__ void split_x3(float a, float b, unsigned& h, unsigned& m, unsigned& l) {
-#ifdef DQ_ABLATE_X6_SPLIT   // timing experiments only: the pieces without the split's VALU work
-  h = m = l = __builtin_amdgcn_perm(__float_as_uint(b), __float_as_uint(a), 0x07060302u);
-  return;
-#endif
   const unsigned hu = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2v){a, b}, bf16x2v));
   const float ra = a - __uint_as_float(hu << 16), rb = b - __uint_as_float(hu & 0xffff0000u);
   const unsigned mu = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2v){ra, rb}, bf16x2v));
@@ -834,21 +804,6 @@ __device__ __forceinline__ f32x16 mfma_x6_lazy(const bf16x8& ah, const bf16x8& a
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
 }
-// the same with the five correction pairs in their own accumulator (its magnitude
-// ~2^-8 of the main one), the two added once at the end of the K loop
-__device__ __forceinline__ void mfma_x6_2(const bf16x8& ah, const bf16x8& am, const bf16x8& al,
-                                          const bf16x8& bh, const bf16x8& bm, const bf16x8& bl,
-                                          f32x16& acc, f32x16& cor) {
-  cor = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, cor, 0, 0, 0);
-  cor = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, cor, 0, 0, 0);
-  cor = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, cor, 0, 0, 0);
-  cor = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, cor, 0, 0, 0);
-  cor = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, cor, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
-}
-#ifndef DQ_X6_COR
-#define DQ_X6_COR 0
-#endif
 
 // The x6 staging image of one operand slice: 3 planes (hi, mid, lo) of [rows][BKT]
 // bf16, 16-byte k chunks XOR-swizzled by row so a 32x32x16 operand read (row r, 8
@@ -949,9 +904,6 @@ template <int WM, int WN, int WK, class AL, class BL, class EP, bool kLate = tru
 __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& E, int M, int N,
                                             int K, int kchunk, int bx, int by, int bz,
                                             float* smem, int tid_base = 0) {
-#ifdef DQ_ABLATE_ALL      // timing experiments only: the launch floor of these grids
-  if (M > 0) return;
-#endif
   using TL = Tile<WM, WN, WK>;
   constexpr int T = TL::T, BM = TL::BM, BN = TL::BN, BKT = TL::BKT;
   constexpr int SA = BM + (AL::kFast ? 1 : 4), SB = BN + (BL::kFast ? 1 : 4);
@@ -1011,11 +963,7 @@ __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& 
   // the epilogue's product-independent input (bias / ReLU mask) of this thread's
   // reduction elements, loaded now (clamped, never branching); see kPrefetch
   constexpr int NE = (OUT + T - 1) / T;
-#ifdef DQ_NO_PF
-  constexpr bool kPf = false;
-#else
   constexpr bool kPf = WK > 1 && HasPf<EP>::value && NE <= 2;
-#endif
   float pfv[NE];
   if constexpr (kPf) {
 #pragma unroll
@@ -1038,11 +986,6 @@ __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& 
     using IB = X6Of<BL::kFast, BN, BKT>;
     char* ia = reinterpret_cast<char*>(smem);
     char* ib = ia + IA::BYTES;
-#if DQ_X6_COR
-    f32x16 cor;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) cor[i] = 0.0f;
-#endif
     load(kbeg);
     for (int k0 = kbeg; k0 < kend; k0 += BKT) {
 #pragma unroll
@@ -1065,19 +1008,11 @@ __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& 
           bf16x8 ah, am, al, bh, bm, bl;
           IA::get(ia, wm * 32, wk * 32 + 16 * s, lane, ah, am, al);
           IB::get(ib, wn * 32, wk * 32 + 16 * s, lane, bh, bm, bl);
-#if DQ_X6_COR
-          mfma_x6_2(ah, am, al, bh, bm, bl, acc, cor);
-#else
           acc = mfma_x6(ah, am, al, bh, bm, bl, acc);
-#endif
         }
       }
       __syncthreads();
     }
-#if DQ_X6_COR
-#pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = __fadd_rn(acc[i], cor[i]);
-#endif
   } else if constexpr (TL::kPrivate) {
     // Wave-private staging: wave wk fetches its own 32-wide k band (the same
     // coalesced 128-byte row segments as the shared layout) and transposes it
@@ -1160,9 +1095,6 @@ __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& 
           float av[8], bv[8];
           operands(Aw, AL::kFast, av);
           operands(Bw, BL::kFast, bv);
-#ifdef DQ_ABLATE_MFMA    // timing experiments only: no matrix-core chain
-          for (int s = 0; s < 8; ++s) acc[s] += av[s] * bv[s];
-#else
           if constexpr (kX6) {
             // each staged element is this lane's alone (one 32 x 32 tile per wave):
             // split as read, one 16-k step of six bf16 MFMAs for the half
@@ -1174,7 +1106,6 @@ __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& 
             for (int s = 0; s < 8; ++s)
               acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc, 0, 0, 0);
           }
-#endif
         }
         if constexpr (kLate) {
           if (h == 0) fetch_h(k0, 1);
@@ -1225,39 +1156,7 @@ __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& 
     if constexpr (HasVecPre<EP>::value) {
       const int c = 4 * (lane & 7), n = n0 + wn * 32 + c;
       auto mrow = [&](int it) { return m0 + wm * 32 + 8 * it + (lane >> 3); };
-#ifndef DQ_VEC_DEPTH
-#define DQ_VEC_DEPTH 1
-#endif
-      if constexpr (DQ_VEC_DEPTH >= 3) {
-        // every row group's parameter / moment loads in flight before the first update
-        typename EP::VPre p[4];
-#pragma unroll
-        for (int it = 0; it < 4; ++it) p[it] = E.vpre(min(mrow(it), M - 1), n);
-#pragma unroll
-        for (int it = 0; it < 4; ++it) {
-          const float* q = W + (8 * it + (lane >> 3)) * 33 + c;
-          const int m = mrow(it);
-          if (m < M && n < N) E.vcommit(m, n, make_float4(q[0], q[1], q[2], q[3]), p[it]);
-        }
-        return;
-      }
-      if constexpr (DQ_VEC_DEPTH == 2) {
-        // three row groups' loads in flight, the fourth issued after the first update
-        typename EP::VPre p0 = E.vpre(min(mrow(0), M - 1), n);
-        typename EP::VPre p1 = E.vpre(min(mrow(1), M - 1), n);
-        typename EP::VPre p2 = E.vpre(min(mrow(2), M - 1), n);
-        auto commit = [&](int it, const typename EP::VPre& pp) {
-          const float* q = W + (8 * it + (lane >> 3)) * 33 + c;
-          const int m = mrow(it);
-          if (m < M && n < N) E.vcommit(m, n, make_float4(q[0], q[1], q[2], q[3]), pp);
-        };
-        commit(0, p0);
-        p0 = E.vpre(min(mrow(3), M - 1), n);
-        commit(1, p1);
-        commit(2, p2);
-        commit(3, p0);
-        return;
-      }
+      // one row group's loads ahead (all four, or three, ahead measured slower)
       typename EP::VPre p = E.vpre(min(mrow(0), M - 1), n);
 #pragma unroll
       for (int it = 0; it < 4; ++it) {
@@ -1302,16 +1201,6 @@ __device__ __forceinline__ void igemm_block(const AL& A, const BL& B, const EP& 
     }
     return;
   }
-#ifdef DQ_ABLATE_REDUCE   // timing experiments only: wave 0's partial goes straight out
-  if (wk == 0) {
-    const int n = n0 + wn * 32 + (lane & 31);
-    for (int r = 0; r < 16; ++r) {
-      const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      if (m < M && n < N) E(m, n, acc[r], bz);
-    }
-  }
-  return;
-#endif
   // partials -> LDS [wk][tile][r][lane]
   {
     float* red = smem + (wk * WM * WN + wm + WM * wn) * 1024 + lane;
@@ -1360,31 +1249,10 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_igemm(AL A, BL B, EP E, i
   constexpr int kBlkW = HasBlock<EP>::value ? 32 * WM * (32 * WN + 1) + BlockExtra<EP>::value : 0;
   constexpr int kEpi = kVecW > kBlkW ? kVecW : kBlkW;
   __shared__ __attribute__((aligned(16))) float smem[kTile > kEpi ? kTile : kEpi];
-#ifndef DQ_XCD_REMAP
-#define DQ_XCD_REMAP 0
-#endif
-#if DQ_XCD_REMAP
-  // XCD-aware tile order (a speed choice only): the dispatcher deals consecutive block ids
-  // round-robin over the 8 XCDs, so id % 8 labels the blocks that share an L2.  Give each
-  // such group a contiguous run of tiles (the bijective form for any grid size), ordered
-  // with the SHORTER of the two tile dimensions fastest, so the few tiles that read the same
-  // panel of the long operand (e.g. dW1's 4 row tiles over one column panel of x, FC1's 4
-  // column tiles over one row panel) run together on one XCD and share its L2.
-  // Measured OFF (0): IQN config 5 607-612 vs 614-620 steps/s plain, same box; no GEMM
-  // got faster in the serial timeline -- the operands already sit in the Infinity Cache
-  // and these fp32 tiles are matrix-core bound (profiles/r2_s5_xcd_remap_ab.log).
-  const unsigned nx = gridDim.x, ny = gridDim.y;
-  const unsigned nwg = nx * ny * gridDim.z;
-  const unsigned orig = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
-  const unsigned g = orig % 8, q = nwg / 8, r = nwg % 8;
-  const unsigned w = (g < r ? g * (q + 1) : r * (q + 1) + (g - r) * q) + orig / 8;
-  const unsigned z = w / (nx * ny), xy = w - z * nx * ny;
-  const unsigned bx = nx <= ny ? xy % nx : xy / ny, by = nx <= ny ? xy / nx : xy % ny;
-  igemm_block<WM, WN, WK, AL, BL, EP, true, kX6>(A, B, E, M, N, K, kchunk, bx, by, z, smem);
-#else
+  // (an XCD-aware tile order measured slower for IQN: the operands sit in the Infinity
+  // Cache and the fp32 tiles are matrix-core bound)
   igemm_block<WM, WN, WK, AL, BL, EP, true, kX6>(A, B, E, M, N, K, kchunk, blockIdx.x, blockIdx.y,
                                                 blockIdx.z, smem);
-#endif
 }
 
 // ordered split-K sum + epilogue: element i of the (M x N) result, slab loads in flight together
@@ -1393,28 +1261,17 @@ __device__ __forceinline__ void splitk_sum(const float* ws, int splits, int M, i
                                            int64_t i) {
   if (i >= (int64_t)M * N) return;
   const int64_t MN = (int64_t)M * N;
-  // a two-phase epilogue (the optimizer's parameter / moment loads) issues its loads first:
-  // they do not depend on the sum, so they share its memory round
-#ifndef DQ_SPLITK_PRE
-#define DQ_SPLITK_PRE 0     // 1: the optimizer's loads before the sum (measured slower, round 4)
-#endif
-  constexpr bool kEarly = HasPre<EP>::value && DQ_SPLITK_PRE;
-  typename std::conditional<HasPre<EP>::value, typename PreOf<EP>::type, int>::type q{};
-  if constexpr (kEarly) q = E.pre((int)(i / N), (int)(i % N));
+  // 8 slab loads in flight per memory round (16, or an optimizer epilogue's parameter /
+  // moment loads issued before the sum, measured slower in round 4)
+  constexpr int kBatch = 8;
   float s = ws[i];
-#ifndef DQ_SPLITK_BATCH
-#define DQ_SPLITK_BATCH 8   // slab loads in flight per memory round (16 measured slower, round 4)
-#endif
-  for (int z0 = 1; z0 < splits; z0 += DQ_SPLITK_BATCH) {
-    float v[DQ_SPLITK_BATCH];
+  for (int z0 = 1; z0 < splits; z0 += kBatch) {
+    float v[kBatch];
 #pragma unroll
-    for (int u = 0; u < DQ_SPLITK_BATCH; ++u) v[u] = ws[(int64_t)min(z0 + u, splits - 1) * MN + i];
+    for (int u = 0; u < kBatch; ++u) v[u] = ws[(int64_t)min(z0 + u, splits - 1) * MN + i];
 #pragma unroll
-    for (int u = 0; u < DQ_SPLITK_BATCH; ++u) s = z0 + u < splits ? __fadd_rn(s, v[u]) : s;
+    for (int u = 0; u < kBatch; ++u) s = z0 + u < splits ? __fadd_rn(s, v[u]) : s;
   }
-  if constexpr (kEarly)
-    E.commit((int)(i / N), (int)(i % N), s, q);
-  else
     E((int)(i / N), (int)(i % N), s, 0);
 }
 

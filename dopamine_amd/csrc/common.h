@@ -52,7 +52,6 @@ __device__ __forceinline__ void warm_kernargs() {
   const KPtr p = (KPtr)__builtin_amdgcn_kernarg_segment_ptr();
   constexpr int n = (kBytes + 63) / 64;
   static_assert(n <= 32, "argument block larger than the warm-up covers");
-#ifndef DQ_NO_WARM
   uint32_t v[32];
 #pragma unroll
   for (int i = 0; i < 32; ++i) v[i] = p[(i < n ? i : n - 1) * 16];   // all issued, then
@@ -61,7 +60,6 @@ __device__ __forceinline__ void warm_kernargs() {
     if (i < n)
       asm volatile("" ::"s"(v[i]), "s"(v[i + 1]), "s"(v[i + 2]), "s"(v[i + 3]), "s"(v[i + 4]),
                    "s"(v[i + 5]), "s"(v[i + 6]), "s"(v[i + 7]));
-#endif
 }
 
 // IEEE square root, correctly rounded, as TF1's CPU kernels (std::sqrt) and numpy compute

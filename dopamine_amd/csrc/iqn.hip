@@ -33,14 +33,8 @@ constexpr int H = 512;
 // h = relu(x W1^T + b1): K = 7744, 4 slabs (R/128 x 4 tiles x 4) -- two 16-wave blocks per
 // CU; 4 fills the 512 slots once at R = 4096 and 1.5 times at R = 6144, measured best
 // (config 5: 4 -> 614-616, 6 -> 609-610, 8 -> 607-608 steps/s, profiles/r2_s5_iqn_fc1_split_ab.log)
-#ifndef DQ_IQN_SPLIT_FC1            // compile-time overrides for A/B builds only
-#define DQ_IQN_SPLIT_FC1 4
-#endif
-#ifndef DQ_IQN_SPLIT_W1
-#define DQ_IQN_SPLIT_W1 2
-#endif
-constexpr int kSplitFc1 = DQ_IQN_SPLIT_FC1;
-constexpr int kSplitW1 = DQ_IQN_SPLIT_W1;  // dW1: K = R (1 / 4 measured equal, profiles/r2_s5_iqn_dw1_split_ab.log)
+constexpr int kSplitFc1 = 4;
+constexpr int kSplitW1 = 2;       // dW1: K = R (1 / 4 measured equal, profiles/r2_s5_iqn_dw1_split_ab.log)
 constexpr int kSplitWe = 8;       // dWe: K = R, 61 row tiles
 constexpr int kSplitW2 = 32;      // dW2: M = A, K = R
 
@@ -51,16 +45,12 @@ constexpr int kSplitW2 = 32;      // dW2: M = A, K = R
 // pixel that cancel to ~1/100 of their terms, and the single-accumulator split form
 // moved them from 5e-7 to 1.3e-5 of scale against float64 at B = 64, N = 64 (a bias
 // from the small correction products rounding into the large accumulator; with the
-// corrections in their own accumulator, DQ_X6_COR, they fall to 5e-7 but the 16 extra
+// corrections in their own accumulator they fall to 5e-7 but the 16 extra
 // registers cost the second 16-wave block per CU, config 5 727 vs 751 steps/s), and x6
 // bought dX no time in the two-stream step (734 with vs 751 without).
 // Measured (config 5, same box): exact f32 616, this 751 steps/s (profiles/r3_s3_x6/).
-//   -DDQ_IQN_X6=0: every GEMM exact f32; 2: dX on the split form too (A/B runs).
-#ifndef DQ_IQN_X6
-#define DQ_IQN_X6 1
-#endif
-constexpr bool kIqnX6 = DQ_IQN_X6 != 0;
-constexpr bool kDxX6 = DQ_IQN_X6 == 2;
+constexpr bool kIqnX6 = true;
+constexpr bool kDxX6 = false;
 template <int WM, int WN, int WK, class AL, class BL, class EP>
 void gemm_iqn(Ctx& c, AL a, BL b, EP e, int M, int N, int K, int splits = 1) {
   gemm_form<WM, WN, WK, kIqnX6>(c, a, b, e, M, N, K, splits);
@@ -332,12 +322,8 @@ void backward(Ctx& c, const dq_iqn_head* hp, const dq_iqn_head* hg, int B, int n
       gemm_iqn<4, 4, 1>(c, ColK{d->dh, H}, ColKOnesHad{a->emb, state, B},
                         EpiGrad{hg->fc1_w, hg->fc1_b, F}, H, F + 1, R, kSplitW1);
   };
-#ifndef DQ_IQN_DW1_FIRST
-#define DQ_IQN_DW1_FIRST 0
-#endif
-  // DQ_IQN_DW1_FIRST: dW1 (it needs only d h) before dX, so on the two-stream step the
-  // store-bound target embedding runs beside dW1's matrix work and the target FC1 beside dX
-  if (DQ_IQN_DW1_FIRST) dw1();
+  // dX before dW1 (dW1 first, so the store-bound target embedding would run beside dW1's
+  // matrix work on the two-stream step, measured 1% slower)
   if (fuse_tile) {
     if (!c.dry)
       hipLaunchKernelGGL((k_igemm<4, 4, 1, RowKQ, ColK, EpiDxQ, kDxX6>), dim3((R + 127) / 128, (F + 127) / 128),
@@ -348,7 +334,7 @@ void backward(Ctx& c, const dq_iqn_head* hp, const dq_iqn_head* hg, int B, int n
     gemm_form<4, 4, 1, kDxX6>(c, RowK{d->dh, H}, ColK{hp->fc1_w, F},
                               EpiDx{d->dtl, d->dpre, a->emb, state, B}, R, F, H, 1);
   }
-  if (!DQ_IQN_DW1_FIRST) dw1();
+  dw1();
   if (we_narrow) {           // dWe over the E cosine columns, dbe from the row-tile partials
     gemm_iqn<4, 2, 2>(c, ColK{d->dpre, F}, ColK{a->cos, E}, EpiGrad{hg->emb_w, hg->emb_b, E}, F, E, R,
                   kSplitWe);

@@ -69,9 +69,8 @@ __device__ long long g_c51_w0[256][16];
 // when the bit is set): no kernel-argument test is left in the chain, so the compiler loads
 // the arguments in one batch instead of one dependent scalar round per branch.
 constexpr int kC51Probs = 1, kC51W2 = 2, kC51LogitsOut = 4;
-#ifndef DQ_C51_SPLIT
-#define DQ_C51_SPLIT 4
-#endif
+// the fused path's d h: 4 blocks per sample (8 or 2 measured a tie)
+constexpr int kC51Split = 4;
 
 // LDS floats of k_c51's head (before the fused path's W2 rows), 4-float aligned
 __host__ __device__ constexpr int c51_head_floats(int A, int N, int nw) {
@@ -773,7 +772,7 @@ int dq_c51_loss_fused(const float* online_parts, const float* online_bias,
   DQ_CHECK_ARG(num_actions <= 64, "num_actions must be <= 64");
   const int waves = num_actions < 16 ? num_actions : 16;
   // d h split over S blocks per sample when the column slices stay whole 16-B chunks
-  const int S = fc2_w && hidden % (4 * DQ_C51_SPLIT) == 0 ? DQ_C51_SPLIT : 1;
+  const int S = fc2_w && hidden % (4 * kC51Split) == 0 ? kC51Split : 1;
   const size_t shm = c51_lds(num_actions, num_atoms, fc2_w ? hidden / S : 0, waves);
   DQ_CHECK_ARG(shm <= 160 * 1024, "num_atoms * hidden exceeds the LDS");
   static void (*const kerns[8])(C51Args, LogitsParts, LogitsParts, C51Extra) = {
@@ -891,10 +890,8 @@ int dq_adam_tf1_part(float* var, const float* grad, float* m, float* v, float* s
   DQ_CHECK_ARG(var && grad && m && v && state && n >= 0 && (slot == 0 || slot == 1), "bad arguments");
   DQ_CHECK_ARG(((uintptr_t)var | (uintptr_t)grad | (uintptr_t)m | (uintptr_t)v) % 16 == 0,
                "adam buffers must be 16-byte aligned");
-#ifndef DQ_ADAM_PART_MAXB
-#define DQ_ADAM_PART_MAXB 256   // N > 1's fc update beside the main queue: a cap leaves it CUs
-#endif
-  hipLaunchKernelGGL(k_adam_part, dim3(std::min(elementwise_grid(n), DQ_ADAM_PART_MAXB)), dim3(256), 0,
+  constexpr int kMaxBlocks = 256;   // N > 1's fc update beside the main queue: a cap leaves it CUs
+  hipLaunchKernelGGL(k_adam_part, dim3(std::min(elementwise_grid(n), kMaxBlocks)), dim3(256), 0,
                      (hipStream_t)stream,
                      var, grad, m, v, state, slot, n, lr, beta1, beta2, eps, bump);
   DQ_CHECK_LAUNCH("k_adam_part");

@@ -41,9 +41,6 @@ namespace cnn {
 // each op owns a contiguous range of blockIdx.x.  All ops of a group run with
 // the same block size kGroupT, and the block's LDS is the largest op's.
 constexpr int kGroupT = 1024;
-#ifndef DQ_ADAM_U
-#define DQ_ADAM_U 1
-#endif
 
 template <int WM, int WN, int WK, class AL, class BL, class EP, bool kLate = true>
 struct GemmOp {
@@ -55,17 +52,6 @@ struct GemmOp {
   EP e;
   int M, N, K, kchunk, gx, gy, gz;
   __device__ __forceinline__ void run(int blk, float* smem, int tid_base = 0) const {
-#ifndef DQ_GROUP_XCD
-#define DQ_GROUP_XCD 0
-#endif
-    if (DQ_GROUP_XCD && gz > 1) {
-      // split-K ops (a speed choice only): the dispatcher deals consecutive block ids round-
-      // robin over the 8 XCDs, so blocks with the same id mod 8 share an L2.  Give each such
-      // class a contiguous run of tiles, k slab slowest, so the tiles of one slab (which
-      // read the same k range of the shared operand) run on one XCD (bijective for any G)
-      const int G = gx * gy * gz, x = blk & 7, q = blk >> 3, per = G >> 3, rem = G & 7;
-      blk = (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + q;
-    }
     const int bx = blk % gx, by = (blk / gx) % gy, bz = blk / (gx * gy);
     igemm_block<WM, WN, WK, AL, BL, EP, kLate, cnn_x6<WM, WN, WK, AL>()>(a, b, e, M, N, K, kchunk,
                                                                       bx, by, bz, smem, tid_base);
@@ -89,13 +75,6 @@ struct PairOp {
   }
   int blocks() const { return (op.blocks() + 1) / 2; }
 };
-template <class T>
-struct IsPairOp : std::false_type {};
-template <class O>
-struct IsPairOp<PairOp<O>> : std::true_type {};
-#ifndef DQ_SP_PAIR
-#define DQ_SP_PAIR 1   // round 4 session 2: +0.7% with the riders in launches 2-4
-#endif
 
 template <class EP, int T = kGroupT>
 struct ReduceOp {                 // ordered split-K sum of nz slabs + epilogue
@@ -137,12 +116,8 @@ struct FcHeadOp {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int nt = 4 * g + wave;
     const int r = lane & 31, hh = lane >> 5, n = 32 * nt + r;
-#ifndef DQ_FCHEAD_EARLY_W2
-#define DQ_FCHEAD_EARLY_W2 0   // 1 measured slower with the 16-slab batch (round 4)
-#endif
-    // B operand: lane r's 8 k of each half, straight from W2's row n (k contiguous) --
-    // independent of the slab sums, so (DQ_FCHEAD_EARLY_W2) issued before them: one
-    // dependent memory round fewer
+    // B operand: lane r's 8 k of each half, straight from W2's row n (k contiguous), loaded
+    // after the slab sums (issuing it before them measured slower)
     float bv[2][8];
     auto load_w2 = [&]() {
 #pragma unroll
@@ -157,46 +132,25 @@ struct FcHeadOp {
         bv[hf][6] = ok ? x1.z : 0.0f; bv[hf][7] = ok ? x1.w : 0.0f;
       }
     };
-    if (DQ_FCHEAD_EARLY_W2) load_w2();
     {
       const int r = tid >> 3, c = 4 * (tid & 7);
       const int m = min(m0 + r, B - 1);
       const int64_t i = (int64_t)m * kHidden + 32 * j + c, MN = (int64_t)B * kHidden;
       const float4 bb = *reinterpret_cast<const float4*>(b1 + 32 * j + c);
       float4 s = *reinterpret_cast<const float4*>(ws + i);
-#ifndef DQ_FCHEAD_SLAB_BATCH
-#define DQ_FCHEAD_SLAB_BATCH 0
-#endif
-      if (DQ_FCHEAD_SLAB_BATCH && nz <= 16) {
-        // all (up to 16) slabs' loads in flight together, then the sum in slab order: one
-        // memory round instead of one per 8 slabs (a runtime loop splits the batches)
-        float4 v[15];
+      for (int z0 = 1; z0 < nz; z0 += 8) {   // 8 slab loads in flight, summed in slab order
+        float4 v[8];
 #pragma unroll
-        for (int u = 0; u < 15; ++u)
-          v[u] = *reinterpret_cast<const float4*>(ws + (int64_t)min(1 + u, nz - 1) * MN + i);
+        for (int u = 0; u < 8; ++u)
+          v[u] = *reinterpret_cast<const float4*>(ws + (int64_t)min(z0 + u, nz - 1) * MN + i);
 #pragma unroll
-        for (int u = 0; u < 15; ++u)
-          if (1 + u < nz) {
+        for (int u = 0; u < 8; ++u)
+          if (z0 + u < nz) {
             s.x = __fadd_rn(s.x, v[u].x);
             s.y = __fadd_rn(s.y, v[u].y);
             s.z = __fadd_rn(s.z, v[u].z);
             s.w = __fadd_rn(s.w, v[u].w);
           }
-      } else {
-        for (int z0 = 1; z0 < nz; z0 += 8) {
-          float4 v[8];
-#pragma unroll
-          for (int u = 0; u < 8; ++u)
-            v[u] = *reinterpret_cast<const float4*>(ws + (int64_t)min(z0 + u, nz - 1) * MN + i);
-#pragma unroll
-          for (int u = 0; u < 8; ++u)
-            if (z0 + u < nz) {
-              s.x = __fadd_rn(s.x, v[u].x);
-              s.y = __fadd_rn(s.y, v[u].y);
-              s.z = __fadd_rn(s.z, v[u].z);
-              s.w = __fadd_rn(s.w, v[u].w);
-            }
-        }
       }
       s.x = fmaxf(__fadd_rn(s.x, bb.x), 0.0f);
       s.y = fmaxf(__fadd_rn(s.y, bb.y), 0.0f);
@@ -211,7 +165,7 @@ struct FcHeadOp {
     }
     __syncthreads();
     if (32 * nt >= NO) return;
-    if (!DQ_FCHEAD_EARLY_W2) load_w2();
+    load_w2();
     f32x16 acc;
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[e] = 0.0f;
@@ -243,9 +197,9 @@ struct AdamOp {
   int64_t n;
   AdamDev o;
   int nb;
-  // kU float4 per array per thread with all 4 kU loads issued before the first
-  // update: more bytes in flight per CU, so the rider holds a CU for less time
-  static constexpr int kU = DQ_ADAM_U;
+  // kU float4 per array per thread, all 4 kU loads issued before the first update
+  // (kU = 2 / 4 measured no faster: the rider's cost is its CU slots and bytes)
+  static constexpr int kU = 1;
   __device__ __forceinline__ void run(int blk, float*) const {
     const float alpha = adam_alpha_of(o.state, o.slot, o.lr);
     const float omb1 = __fsub_rn(1.0f, o.b1), omb2 = __fsub_rn(1.0f, o.b2);
@@ -293,7 +247,7 @@ struct RmsOp {
   int64_t n;
   RmsDev o;
   int nb;
-  static constexpr int kU = DQ_ADAM_U;
+  static constexpr int kU = 1;
   __device__ __forceinline__ void run(int blk, float*) const {
     const bool c = o.centered != 0;
     const int64_t n4 = n >> 2, stride = (int64_t)nb * kT * kU;
@@ -361,7 +315,7 @@ struct OptPart<2> {
   }
 };
 
-// fc1's weight gradient + its optimizer in the vector epilogue (DQ_FC1_EPI_OPT): TF1 Adam
+// fc1's weight gradient + its optimizer in the vector epilogue: TF1 Adam
 // or centered RMSProp over fc1_w and fc1_b, the riders' arithmetic.  RMSProp's four state
 // arrays made the epilogue the longer path at first (config 2: 8,060 vs 8,143 steps/s with
 // riders); with the next row group's loads issued before this group's stores (kVecPre) it
@@ -380,14 +334,14 @@ struct Fc1EpiOpt<1> {
 };
 
 template <>
-struct Fc1EpiOpt<2> {       // centered RMSProp (DQN, config 2): DQ_FC1_EPI_RMS
+struct Fc1EpiOpt<2> {       // centered RMSProp (DQN, config 2)
   static EpiGradRmsVec make(const dq_cnn_params* p, const dq_cnn_params* g, const dq_adam_args* o) {
     return EpiGradRmsVec{GradEpi<2>::make(g->fc1_w, g->fc1_b, kFlat, p->fc1_w, p->fc1_b,
                                           AdamHost{o}, 0)};
   }
 };
 
-// the same for fc2 (DQ_FC2_EPI): fc2's weight gradient + optimizer in one vector epilogue
+// the same for fc2: fc2's weight gradient + optimizer in one vector epilogue
 template <int kOpt>
 struct Fc2EpiOpt;
 template <>
@@ -406,17 +360,6 @@ struct Fc2EpiOpt<2> {
     return EpiGradRmsVec{GradEpi<2>::make(g->fc2_w, g->fc2_b, kHidden, p->fc2_w, p->fc2_b,
                                           AdamHost{o}, 0)};
   }
-};
-#ifndef DQ_FC2_EPI
-#define DQ_FC2_EPI 1   // round 4 session 2: +0.8% with the riders in launches 2-4
-#endif
-#ifndef DQ_FC1_EPI_RMS
-#define DQ_FC1_EPI_RMS 1
-#endif
-
-// timing experiments only (DQ_ABL_*): the GEMM's result is dropped
-struct EpiNone {
-  __device__ __forceinline__ void operator()(int, int, float, int) const {}
 };
 
 // A recorded replay operation (replay_dev.h) riding in a grouped launch: its
@@ -466,18 +409,9 @@ struct GroupArgs {
   int nblocks[sizeof...(Ops)];
 };
 
-#ifndef DQ_GROUP_WPE
-#define DQ_GROUP_WPE 8
-#endif
-#ifndef DQ_B1_LATE
-#define DQ_B1_LATE false   // B1 is one round of blocks: early fetch (+1.5%)
-#endif
-#ifndef DQ_F4_LATE
-#define DQ_F4_LATE true
-#endif
-#ifndef DQ_B6_LATE
-#define DQ_B6_LATE true
-#endif
+constexpr bool kB1Late = false;   // backward launch 1 is one round of blocks: early fetch (+1.5%)
+constexpr bool kF4Late = true;
+constexpr bool kB6Late = true;
 // 8 waves per SIMD (<= 64 VGPRs: two 16-wave blocks per CU) unless a tile op of the
 // group fetches early (single-round launches, where the registers buy more)
 template <class Op, class = void>
@@ -490,7 +424,7 @@ struct LateOk<Op, decltype((void)Op::kLateFetch)> {
 };
 template <class... Ops>
 constexpr int group_wpe() {
-  return (LateOk<Ops>::value && ...) ? DQ_GROUP_WPE : 1;
+  return (LateOk<Ops>::value && ...) ? 8 : 1;
 }
 template <int T, class... Ops>
 __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(group_wpe<Ops...>())))
@@ -539,13 +473,9 @@ void group_r(Ctx& c, const RiderDesc* r, Ops... ops) {
 // Tile shapes: WM = WN = 1 with WK k-bands sized so K takes one or two slices
 // (BKT = 32 * WK); split-K only where the grid would otherwise leave most of the
 // 256 CUs idle (weight streaming of fc1, the pixel-deep weight gradients).
-#ifndef DQ_SPLIT_CONVW
-#define DQ_SPLIT_CONVW 8     // conv2 / conv3 weight gradients: split-K slabs over B * 121
-#endif
-#ifndef DQ_SPLIT_CONV1W
-#define DQ_SPLIT_CONV1W 28   // conv1's over B * 441
-#endif
-constexpr int kSplitFc1 = 16, kSplitConvW = DQ_SPLIT_CONVW, kSplitConv1W = DQ_SPLIT_CONV1W;
+// conv2 / conv3 weight gradients: 8 split-K slabs over B * 121; conv1's 28 over B * 441
+// (4 / 14 measured slower)
+constexpr int kSplitFc1 = 16, kSplitConvW = 8, kSplitConv1W = 28;
 
 void forward(Ctx& c, const dq_cnn_params* p, int B, const float* x, dq_cnn_acts* a) {
   // conv1 / conv2 / conv3 + bias + ReLU  (implicit GEMM: M = pixels, N = out channels)
@@ -628,37 +558,25 @@ void forward_fused(Ctx& c0, Ctx& c1, const FwdOps& f0, const FwdOps& f1, bool fc
   c1.need = n1 > c1.need ? n1 : c1.need;
   if (c0.dry) return;
   if (convs) {
-// net 1's conv3 (head_from = 5) rides in net 0's conv3 launch (DQ_T3_AT 3): measured
-// +1.1% over the conv1 launch and +2.2% over the conv2 launch
-#ifndef DQ_T3_AT
-#define DQ_T3_AT 3
-#endif
-#ifndef DQ_F1_LATE
-#define DQ_F1_LATE false
-#endif
-#ifndef DQ_F2_LATE       // the conv2 launch with the target's conv2: late fetch, +0.9%
-#define DQ_F2_LATE true
-#endif
+    // single-round launches fetch early; the conv2 launch with the target's conv2 late
+    // (+0.9%); net 1's conv3 (head_from = 5) rides in net 0's conv3 launch (+1.1% over the
+    // conv1 launch, +2.2% over the conv2 launch)
     if (conv1_1)                     // net 1's conv1 (head_from = 7) beside net 0's conv1
-      group(c0, f0.conv1<DQ_F1_LATE>(), f1.conv1());
-    else if (conv3_1 && DQ_T3_AT == 1)
-      group(c0, f0.conv1<DQ_F1_LATE>(), f1.conv3());
+      group(c0, f0.conv1<false>(), f1.conv1());
     else
-      group(c0, f0.conv1<false>());  // single-round launches: fetch early
+      group(c0, f0.conv1<false>());
     if (conv2_1)                     // net 1's conv2 (head_from = 6) beside net 0's conv2
-      group(c0, f0.conv2<DQ_F2_LATE>(), f1.conv2());
-    else if (conv3_1 && DQ_T3_AT == 2)
-      group(c0, f0.conv2<DQ_F1_LATE>(), f1.conv3());
+      group(c0, f0.conv2<true>(), f1.conv2());
     else
       group(c0, f0.conv2<false>());
-    if (conv3_1 && DQ_T3_AT == 3)
-      group(c0, f0.conv3<DQ_F1_LATE>(), f1.conv3());
+    if (conv3_1)
+      group(c0, f0.conv3<false>(), f1.conv3());
     else
       group(c0, f0.conv3<false>());
   }
   if (!fcs) return;
   if (fc1_1)
-    group(c0, f0.fc1<DQ_F4_LATE>(), f1.fc1<DQ_F4_LATE>());
+    group(c0, f0.fc1<kF4Late>(), f1.fc1<kF4Late>());
   else
     group(c0, f0.fc1());
   group(c0, f0.fchead(), f1.fchead());
@@ -687,12 +605,12 @@ void forward_fused_c51(Ctx& c0, Ctx& c1, const FwdOps& f0, const FwdOps& f1, con
   c1.need = n1 > c1.need ? n1 : c1.need;
   if (c0.dry) return;
   if (convs) {
-    group(c0, f0.conv1<DQ_F1_LATE>(), f1.conv2());
-    group(c0, f0.conv2<DQ_F2_LATE>(), f1.conv3());
-    group(c0, f0.conv3<DQ_F1_LATE>(), f1.fc1());
+    group(c0, f0.conv1<false>(), f1.conv2());
+    group(c0, f0.conv2<true>(), f1.conv3());
+    group(c0, f0.conv3<false>(), f1.fc1());
   }
   if (!fcs) return;
-  group(c0, f0.fc1<DQ_F4_LATE>(), f1.fchead());
+  group(c0, f0.fc1<kF4Late>(), f1.fchead());
   group(c0, f0.fchead(), TgtC51Op{t});
 }
 
@@ -740,13 +658,10 @@ void forward_head(Ctx& c, const FwdOps& f) {
 
 // conv2's input gradient as its 4 sub-pixel classes (SubPix): da1 straight from da2,
 // masked by a1 > 0, in one grouped launch of 8-wave tiles (K = 2 x 2 taps x 64 = 256)
-#ifndef DQ_SP_LATE
-#define DQ_SP_LATE true
-#endif
 template <int PY, int PX>
 auto subpix_op(const dq_cnn_params* p, const dq_cnn_acts* a, dq_cnn_acts* d, int B) {
   using SP = SubPix<Conv2, PY, PX>;
-  return gemm_op<1, 1, 8, DQ_SP_LATE>(SubPixDy<Conv2, PY, PX>{d->a2}, SubPixW<Conv2, PY, PX>{p->conv2_w},
+  return gemm_op<1, 1, 8, true>(SubPixDy<Conv2, PY, PX>{d->a2}, SubPixW<Conv2, PY, PX>{p->conv2_w},
                           EpiMaskPix<SP, Conv2::CI>{d->a1, a->a1}, B * SP::NY * SP::NX, Conv2::CI,
                           SP::K, SP::K);
 }
@@ -836,18 +751,11 @@ void backward_torso_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params*
                                  EpiPartial{ws + o1, 32, Conv1::K + 1}, 32, Conv1::K + 1, K1, ch1);
   auto sum_c1 = ReduceOp<EpiGrad>{ws + o1, nz1, 32, Conv1::K + 1,
                                   EpiGrad{g->conv1_w, g->conv1_b, Conv1::K}};
-#ifndef DQ_SP_PAIR_TORSO
-#define DQ_SP_PAIR_TORSO 0
-#endif
-  // DQ_SP_PAIR_TORSO: two of the 8-wave sub-pixel tiles per 16-wave block here too
-  auto tsp = [](auto op) {
-    if constexpr (DQ_SP_PAIR_TORSO != 0) return PairOp<decltype(op)>{op};
-    else return op;
-  };
+  // (the sub-pixel tiles unpaired here: two per block measured a tie for IQN)
   if constexpr (kOpt == 0) {
     group(c, dW_c3, dX_c3);
-    group(c, dW_c2, tsp(subpix_op<0, 0>(p, a, d, B)), tsp(subpix_op<0, 1>(p, a, d, B)),
-          tsp(subpix_op<1, 0>(p, a, d, B)), tsp(subpix_op<1, 1>(p, a, d, B)), sum_c3);
+    group(c, dW_c2, subpix_op<0, 0>(p, a, d, B), subpix_op<0, 1>(p, a, d, B),
+          subpix_op<1, 0>(p, a, d, B), subpix_op<1, 1>(p, a, d, B), sum_c3);
     group(c, dW_c1, sum_c2);
     group(c, sum_c1);
   } else {
@@ -861,8 +769,8 @@ void backward_torso_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params*
         ws + o1, nz1, 32, Conv1::K + 1,
         GE::make(g->conv1_w, g->conv1_b, Conv1::K, p->conv1_w, p->conv1_b, opt, 1)};
     group(c, dW_c3, dX_c3, part(head_begin, hm));
-    group(c, dW_c2, tsp(subpix_op<0, 0>(p, a, d, B)), tsp(subpix_op<0, 1>(p, a, d, B)),
-          tsp(subpix_op<1, 0>(p, a, d, B)), tsp(subpix_op<1, 1>(p, a, d, B)), sum_c3,
+    group(c, dW_c2, subpix_op<0, 0>(p, a, d, B), subpix_op<0, 1>(p, a, d, B),
+          subpix_op<1, 0>(p, a, d, B), subpix_op<1, 1>(p, a, d, B), sum_c3,
           part(hm, head_end));
     group(c, dW_c1, sum_c2o, part(p->conv3_w, head_begin));
     group(c, sum_c1o);
@@ -916,7 +824,7 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
   auto dW_fc2 = gemm_op<4, 4, 1>(ColKScalar{dout, NO}, ColKOnes{a->h, kHidden},
                                  EpiGrad{g->fc2_w, g->fc2_b, kHidden},
                                  NO, kHidden + 1, B, B);
-  auto dX_fc1 = gemm_op<1, 1, 16, DQ_B1_LATE>(RowK{d->h, kHidden}, ColK{p->fc1_w, kFlat},
+  auto dX_fc1 = gemm_op<1, 1, 16, kB1Late>(RowK{d->h, kHidden}, ColK{p->fc1_w, kFlat},
                                   EpiMask{d->a3, a->a3, kFlat}, B, kFlat, kHidden, kHidden);
   auto dW_fc1 = gemm_op<4, 4, 1>(ColK{d->h, kHidden}, ColKOnes{a->a3, kFlat},
                                  EpiGrad{g->fc1_w, g->fc1_b, kFlat},
@@ -925,11 +833,8 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
                                  EpiMask{d->a2, a->a2, 64}, K3, 64, Conv3::K, Conv3::K);
   auto dW_c3 = gemm_op<1, 1, 16>(DyT<64>{d->a3}, Im2colT<Conv3>{a->a2},
                                  EpiPartial{ws + o3, 64, Conv3::K + 1}, 64, Conv3::K + 1, K3, ch3);
-  // DQ_SP_PAIR: two of the 8-wave sub-pixel tiles per 16-wave block of the grouped launch
-  auto sp_op = [](auto op) {
-    if constexpr (DQ_SP_PAIR != 0) return PairOp<decltype(op)>{op};
-    else return op;
-  };
+  // two of the 8-wave sub-pixel tiles per 16-wave block of the grouped launch (+0.7%)
+  auto sp_op = [](auto op) { return PairOp<decltype(op)>{op}; };
   auto sp00 = sp_op(subpix_op<0, 0>(p, a, d, B));
   auto sp01 = sp_op(subpix_op<0, 1>(p, a, d, B));
   auto sp10 = sp_op(subpix_op<1, 0>(p, a, d, B));
@@ -945,171 +850,52 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
   auto sum_c1 = ReduceOp<decltype(GE::make(0, 0, 0, 0, 0, opt, 0))>{
       ws + o1, nz1, 32, Conv1::K + 1,
       GE::make(g->conv1_w, g->conv1_b, Conv1::K, p->conv1_w, p->conv1_b, opt, 1)};
-#ifndef DQ_T1_PAIR
-#define DQ_T1_PAIR 0
-#endif
-  // the target head's conv1 (8-wave tiles) riding in a 16-wave launch: DQ_T1_PAIR puts two
-  // of its tiles in each block (PairOp) instead of leaving half of every block's waves idle
-  auto t1 = [&]() {
-    if constexpr (DQ_T1_PAIR != 0) return PairOp<decltype(head->conv1())>{head->conv1()};
-    else return head->conv1();
-  };
   auto in = [&](int i) { return first <= i && i < last; };
   auto rd = [&](int i) {   // rider of launch i
     return i >= first && i - first < n_riders ? riders + (i - first) : nullptr;
   };
   if constexpr (kOpt != 0) {
     {
-      // The optimizer spread over the launches after each gradient is final (fc2 after
-      // launch 2, fc1 after launch 3) and each weight's last read: fc2 rides in launch 3,
-      // fc1 in thirds in launches 4-6, conv2..conv3 with conv1's epilogue in launch 7.
+      // The optimizer spread over the launches after each gradient is final and each
+      // weight's last read.
       auto part = [&](float* w0, float* w1) { return OptPart<kOpt>::make(p, g, opt.a, w0, w1); };
       float* f0 = p->fc1_w;
       float* f3 = p->fc2_w;                          // fc1_w .. fc1_b (+ pad)
-#ifndef DQ_FC1_A      // fc1's Adam split points, in 24ths of the range
-#define DQ_FC1_A 8
-#endif
-#ifndef DQ_FC1_B
-#define DQ_FC1_B 16
-#endif
-      float* f1 = f0 + (((f3 - f0) * DQ_FC1_A / 24) & ~(int64_t)3);
-      float* f2 = f0 + (((f3 - f0) * DQ_FC1_B / 24) & ~(int64_t)3);
-#ifndef DQ_FC1_EPI_OPT
-#define DQ_FC1_EPI_OPT 1
-#endif
-      // TF1 Adam on fc1 in its weight-gradient GEMM's (vector) epilogue, launch 2, instead of
-      // Adam riders over fc1 in launches 3-5 reading the stored gradient back (+0.6-1.2%
-      // config 1: 7,600-7,644 vs 7,555-7,559 steps/s)
-      if constexpr (kHeadFrom >= 5 && (kOpt == 1 || (kOpt == 2 && DQ_FC1_EPI_RMS)) &&
-                    DQ_FC1_EPI_OPT) {
+      // fc1's range op split points (kHeadFrom < 5), in 24ths of the range: thirds
+      float* f1 = f0 + (((f3 - f0) * 8 / 24) & ~(int64_t)3);
+      float* f2 = f0 + (((f3 - f0) * 16 / 24) & ~(int64_t)3);
+      if constexpr (kHeadFrom >= 5) {
+        // fc1 and fc2: TF1 Adam / RMSProp in their weight-gradient GEMMs' vector epilogues,
+        // launch 2 (fc1's instead of range ops over fc1 in launches 3-5 reading the stored
+        // gradient back: +0.6-1.2%; fc2's moved there from launch 1 so launch 1 keeps only
+        // dX fc1 (+ rider), one round of blocks: +0.8%).  conv2 and conv1 in
+        // their split-K sums' epilogues, conv3 as a range op in the last launch.
         auto dW_fc1a = gemm_op<4, 4, 1>(ColK{d->h, kHidden}, ColKOnes{a->a3, kFlat},
                                         Fc1EpiOpt<kOpt>::make(p, g, opt.a), kHidden, kFlat + 1,
                                         B, B);
-#ifndef DQ_FC1_SPLIT_L
-#define DQ_FC1_SPLIT_L 0
-#endif
-        // DQ_FC1_SPLIT_L = L > 2 (kHeadFrom 6): fc1's weight gradient + update for its rows
-        // [256, 512) in launch L instead of 2 (the gradient needs only d h and a3; fc1_w's
-        // last read is dX fc1 in launch 1)
-        constexpr int kFc1Lo = DQ_FC1_SPLIT_L > 2 ? kHidden / 2 : kHidden;
-        auto dW_fc1lo = gemm_op<4, 4, 1>(ColK{d->h, kHidden}, ColKOnes{a->a3, kFlat},
-                                         Fc1EpiOpt<kOpt>::make(p, g, opt.a), kFc1Lo, kFlat + 1,
-                                         B, B);
-        auto dW_fc1hi = gemm_op<4, 4, 1>(ColK{d->h + kFc1Lo, kHidden}, ColKOnes{a->a3, kFlat},
-                                         Fc1EpiOpt<kOpt>::make(p, g, opt.a).rows_from(kFc1Lo),
-                                         kHidden - kFc1Lo, kFlat + 1, B, B);
+        auto dW_fc2a = gemm_op<4, 4, 1>(ColKScalar{dout, NO}, ColKOnes{a->h, kHidden},
+                                        Fc2EpiOpt<kOpt>::make(p, g, opt.a), NO, kHidden + 1, B, B);
         auto sum_c2a = ReduceOp<decltype(GE::make(0, 0, 0, 0, 0, opt, 0))>{
             ws + o2, nz3, 64, Conv2::K + 1,
             GE::make(g->conv2_w, g->conv2_b, Conv2::K, p->conv2_w, p->conv2_b, opt, 0)};
-        // DQ_FC2_EPI: fc2's weight gradient moves from launch 1 to 2 with its optimizer in the
-        // GEMM's vector epilogue (instead of a float4 range op in launch 2): launch 1 keeps
-        // only dX fc1 (+ rider), one round of blocks at one 16-wave block per CU
-        auto dW_fc2a = gemm_op<4, 4, 1>(ColKScalar{dout, NO}, ColKOnes{a->h, kHidden},
-                                        Fc2EpiOpt<kOpt>::make(p, g, opt.a), NO, kHidden + 1, B, B);
-#ifndef DQ_ABL_B2
-#define DQ_ABL_B2 0
-#endif
-#ifndef DQ_FC2_OPT_LAUNCH
-#define DQ_FC2_OPT_LAUNCH 2
-#endif
-        constexpr bool kFc2Epi = DQ_FC2_EPI && DQ_ABL_B2 == 0 && DQ_FC1_SPLIT_L == 0 &&
-                                 DQ_FC2_OPT_LAUNCH == 2;
         if (in(0)) group_r(c, rd(0), dX_fc2);
-        // DQ_FC2_EPI == 2: fc2's gradient + optimizer epilogue in launch 1 beside dX fc1
-        if (in(1)) {
-          if constexpr (kFc2Epi && DQ_FC2_EPI == 2)
-            group_r(c, rd(1), dX_fc1, dW_fc2a);
-          else if constexpr (kFc2Epi)
-            group_r(c, rd(1), dX_fc1);
-          else
-            group_r(c, rd(1), dW_fc2, dX_fc1);
-        }
-        // DQ_ABL_B2 (timing experiments only, tools/build_variant.py; results are wrong):
-        // launch 2 without  1: its rider  2: fc1's Adam epilogue (the GEMM, no stores)
-        // 4: dX conv3  8: fc2's Adam part
-        if constexpr (DQ_ABL_B2 != 0) {
-          if (in(2)) {
-            auto dW_none = gemm_op<4, 4, 1>(ColK{d->h, kHidden}, ColKOnes{a->a3, kFlat},
-                                            EpiNone{}, kHidden, kFlat + 1, B, B);
-            const RiderDesc* r2 = (DQ_ABL_B2 & 1) ? nullptr : rd(2);
-            auto fc2p = part(p->fc2_w, (DQ_ABL_B2 & 8) ? p->fc2_w + 4 : p->fc2_b + NO);
-            auto x3 = dX_c3;
-            if (DQ_ABL_B2 & 4) x3.gx = x3.gy = x3.gz = 0;
-            if (DQ_ABL_B2 & 2) {
-              group_r(c, r2, dW_none, x3, fc2p);
-            } else {
-              group_r(c, r2, dW_fc1a, x3, fc2p);
-            }
-          }
-        } else if (in(2)) {
-          // fc2's optimizer part: launch 2 (its gradient is final after launch 1), or 4
-          // (launch 2 holds the fc1 update's stream; nothing reads fc2_w before the next C)
-          if constexpr (kFc2Epi && DQ_FC2_EPI == 2)
-            group_r(c, rd(2), dW_fc1a, dX_c3);
-          else if constexpr (kFc2Epi)
-            group_r(c, rd(2), dW_fc1a, dX_c3, dW_fc2a);
-          else if (DQ_FC1_SPLIT_L > 2 && kHeadFrom == 6)
-            group_r(c, rd(2), dW_fc1lo, dX_c3, part(p->fc2_w, p->fc2_b + NO));
-          else if (DQ_FC2_OPT_LAUNCH == 2 || kHeadFrom != 6)
-            group_r(c, rd(2), dW_fc1a, dX_c3, part(p->fc2_w, p->fc2_b + NO));
-          else
-            group_r(c, rd(2), dW_fc1a, dX_c3);
-        }
+        if (in(1)) group_r(c, rd(1), dX_fc1);
+        if (in(2)) group_r(c, rd(2), dW_fc1a, dX_c3, dW_fc2a);
         if (kHeadFrom == 6) {
-          if (in(3)) {
-#ifndef DQ_ABL_B3
-#define DQ_ABL_B3 0
-#endif
-            // DQ_ABL_B3 (timing experiments only, results wrong): launch 3 without
-            // 1: its rider (the gather)  2: dW conv3's slabs  4: the sub-pixel GEMMs
-            // 8: dW conv2's slabs
-            if constexpr (DQ_ABL_B3 != 0) {
-              auto w3 = dW_c3;
-              auto w2 = dW_c2;
-              auto s0 = sp00;
-              auto s1 = sp01;
-              auto s2 = sp10;
-              auto s3 = sp11;
-              auto none = [](auto& o) {       // an op with no blocks (a GemmOp, or a PairOp's)
-                if constexpr (IsPairOp<std::decay_t<decltype(o)>>::value)
-                  o.op.gx = o.op.gy = o.op.gz = 0;
-                else
-                  o.gx = o.gy = o.gz = 0;
-              };
-              if (DQ_ABL_B3 & 2) none(w3);
-              if (DQ_ABL_B3 & 8) none(w2);
-              if (DQ_ABL_B3 & 4) {
-                none(s0); none(s1); none(s2); none(s3);
-              }
-              group_r(c, (DQ_ABL_B3 & 1) ? nullptr : rd(3), w3, s0, s1, s2, s3, w2);
-            } else if (DQ_FC1_SPLIT_L == 3) {
-              group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11, dW_c2, dW_fc1hi);
-            } else {
-              group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11, dW_c2);
-            }
-          }
-          if (in(4)) {
-            if (DQ_FC1_SPLIT_L == 4)
-              group_r(c, rd(4), sum_c3, dW_c1, dW_fc1hi);
-            else if (DQ_FC2_OPT_LAUNCH == 4)
-              group_r(c, rd(4), sum_c3, dW_c1, part(p->fc2_w, p->fc2_b + NO));
-            else
-              group_r(c, rd(4), sum_c3, dW_c1);
-          }
+          // conv2's weight-gradient slabs (they need only da2) beside conv3's in launch 3
+          // (+0.9%), the head's conv1 in launch 5, its conv2 and conv3 in the next forward
+          if (in(3)) group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11, dW_c2);
+          if (in(4)) group_r(c, rd(4), sum_c3, dW_c1);
           if (in(5)) {
-            if (DQ_FC1_SPLIT_L == 5) {
-              if (head)
-                group_r(c, rd(5), sum_c2a, sum_c1, part(p->conv3_w, p->fc1_w), t1(), dW_fc1hi);
-              else
-                group_r(c, rd(5), sum_c2a, sum_c1, part(p->conv3_w, p->fc1_w), dW_fc1hi);
-            } else if (head) {
-              group_r(c, rd(5), sum_c2a, sum_c1, part(p->conv3_w, p->fc1_w), t1());
-            } else {
+            if (head)
+              group_r(c, rd(5), sum_c2a, sum_c1, part(p->conv3_w, p->fc1_w), head->conv1());
+            else
               group_r(c, rd(5), sum_c2a, sum_c1, part(p->conv3_w, p->fc1_w));
-            }
           }
           return;
         }
+        // five launches: conv2's input gradient by sub-pixel class needs only da2, so conv1's
+        // weight-gradient slabs join launch 4 and the split-K sums end the backward in launch 5
         if (in(3)) group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11);
         if (head) {
           if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, dW_c1, head->conv1());
@@ -1121,43 +907,6 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
         }
         return;
       }
-      if constexpr (kHeadFrom >= 5) {
-        // five launches: conv2's input gradient by sub-pixel class needs only da2, so
-        // conv1's weight-gradient slabs join launch 4 and the three split-K sums end
-        // the backward in launch 5, conv2 and conv1 applying Adam in their epilogues
-        auto sum_c2a = ReduceOp<decltype(GE::make(0, 0, 0, 0, 0, opt, 0))>{
-            ws + o2, nz3, 64, Conv2::K + 1,
-            GE::make(g->conv2_w, g->conv2_b, Conv2::K, p->conv2_w, p->conv2_b, opt, 0)};
-        if (in(0)) group_r(c, rd(0), dX_fc2);
-        if (in(1)) group_r(c, rd(1), dW_fc2, dX_fc1);
-        if (in(2)) group_r(c, rd(2), dW_fc1, dX_c3, part(p->fc2_w, p->fc2_b + NO));
-        if (kHeadFrom == 6) {
-          // 6: conv2's weight-gradient slabs (they need only da2) beside conv3's in
-          // launch 3 (+0.9%), the head's conv1 in launch 5, its conv2 and conv3 in the
-          // next forward
-          if (in(3)) group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11, dW_c2, part(f0, f1));
-          if (in(4)) group_r(c, rd(4), sum_c3, dW_c1, part(f1, f2));
-          if (in(5)) {
-            if (head)
-              group_r(c, rd(5), sum_c2a, sum_c1, part(f2, f3), part(p->conv3_w, p->fc1_w),
-                      head->conv1());
-            else
-              group_r(c, rd(5), sum_c2a, sum_c1, part(f2, f3), part(p->conv3_w, p->fc1_w));
-          }
-          return;
-        }
-        if (in(3)) group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11, part(f0, f1));
-        if (head) {
-          if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, dW_c1, part(f1, f2), head->conv1());
-          if (in(5))
-            group_r(c, rd(5), sum_c2a, sum_c1, part(f2, f3), part(p->conv3_w, p->fc1_w),
-                    head->conv2());
-        } else {
-          if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, dW_c1, part(f1, f2));
-          if (in(5)) group_r(c, rd(5), sum_c2a, sum_c1, part(f2, f3), part(p->conv3_w, p->fc1_w));
-        }
-        return;
-      }
       if (in(0)) group_r(c, rd(0), dX_fc2);
       if (in(1)) group_r(c, rd(1), dW_fc2, dX_fc1);
       if (in(2)) group_r(c, rd(2), dW_fc1, dX_c3, part(p->fc2_w, p->fc2_b + NO));
@@ -1166,7 +915,7 @@ if constexpr (kHeadFrom == 4) {
           if (in(3)) group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11, part(f0, f1));
           if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, part(f1, f2), head->conv1());
           if (in(5)) group_r(c, rd(5), sum_c2, dW_c1, part(f2, f3), head->conv2());
-          if (in(6)) group_r(c, rd(6), sum_c1, part(p->conv2_w, p->fc1_w), head->conv3<DQ_B6_LATE>());
+          if (in(6)) group_r(c, rd(6), sum_c1, part(p->conv2_w, p->fc1_w), head->conv3<kB6Late>());
         } else {
           if (in(3)) group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11, part(f0, f1), head->conv1());
           if (in(4)) group_r(c, rd(4), sum_c3, dW_c2, part(f1, f2), head->conv2());
@@ -1191,7 +940,7 @@ if constexpr (kHeadFrom == 4) {
       if (in(4)) group_r(c, rd(4), sum_c3, dW_c1);
       if (in(5)) {
         if (head)
-          group_r(c, rd(5), sum_c2, sum_c1, t1());
+          group_r(c, rd(5), sum_c2, sum_c1, head->conv1());
         else
           group_r(c, rd(5), sum_c2, sum_c1);
       }
@@ -1471,17 +1220,7 @@ int dq_cnn_backward_torso(const dq_cnn_params* p, const dq_cnn_params* g, int32_
   DQ_CHECK_ARG(p && g && a && d && x && ws && batch >= 1, "null argument");
   DQ_CHECK_ARG(p->in_channels == 4, "the Nature CNN takes 84x84x4 NHWC input");
   Ctx c{(hipStream_t)stream, ws, false, 0};
-#ifndef DQ_TORSO_GROUPED
-#define DQ_TORSO_GROUPED 1
-#endif
-  if (DQ_TORSO_GROUPED) {
-    backward_torso_grouped(c, p, g, batch, x, a, d);
-  } else {
-    for (int layer = 2; layer <= 4; ++layer) {        // conv3, conv2, conv1 (same tiles as
-      backward_layer(c, p, g, batch, x, a, nullptr, d, layer, 1);   // the full backward)
-      if (layer < 4) backward_layer(c, p, g, batch, x, a, nullptr, d, layer, 0);
-    }
-  }
+  backward_torso_grouped(c, p, g, batch, x, a, d);
   DQ_CHECK_LAUNCH("dq_cnn_backward_torso");
   return DQ_OK;
 }

@@ -194,15 +194,76 @@ __global__ __launch_bounds__(256) void k_gather_f32(ReplayView v, GatherOut g) {
 // the scalar chain.
 template <int R>
 __global__ __launch_bounds__(256) void k_gather_nhwc4(ReplayView v, GatherOut g) {
+#ifdef DQ_GATHER_PROF
+  unsigned long long gp[4] = {__builtin_amdgcn_s_memrealtime(), 0, 0, 0};
+  unsigned long long* gpp = gp;
+#else
+  unsigned long long* gpp = nullptr;
+#endif
   warm_kernargs<sizeof(ReplayView) + sizeof(GatherOut)>();
   const int slot = blockIdx.y;
   if (blockIdx.x == gridDim.x - 1) {
     if ((slot & 1) == 0 && threadIdx.x < kWave)
       write_scalars_wave(v, g, slot >> 1, pymod((int64_t)g.indices[slot >> 1], v.C));
-    return;
+  } else {
+    gather_nhwc4_body<R, kScalNone, true>(v, g, blockIdx.x, slot, threadIdx.x, gpp);
   }
-  gather_nhwc4_body<R, kScalNone, true>(v, g, blockIdx.x, slot, threadIdx.x);
+#ifdef DQ_GATHER_PROF
+  GP_STAMP(gp, 3);
+  if ((threadIdx.x & 63) == 0) {
+    const unsigned launch = *(volatile unsigned*)&g_gp_count;
+    const unsigned waves = gridDim.x * gridDim.y * (blockDim.x / 64);
+    const unsigned wid = (blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6);
+    const bool frame = blockIdx.x != gridDim.x - 1;
+    if (launch < (unsigned)kGpLaunches) {
+      unsigned long long* L = g_gp_launch[launch];
+      atomicMin(&L[0], gp[0]);
+      atomicMax(&L[1], gp[0]);
+      if (frame && gp[1]) {
+        atomicMax(&L[2], gp[1]);
+        atomicMin(&L[3], gp[2]);
+        atomicMax(&L[4], gp[2]);
+      }
+      atomicMax(&L[5], gp[3]);
+      if (!frame) atomicMax(&L[6], gp[3]);      // the scalar column's end
+    }
+    if (launch == *(volatile unsigned*)&g_gp_target && wid < (unsigned)kGpWaves) {
+      g_gp_wave[wid][0] = gp[0];
+      g_gp_wave[wid][1] = gp[1];
+      g_gp_wave[wid][2] = gp[2];
+      g_gp_wave[wid][3] = gp[3];
+    }
+    __threadfence();
+    if (atomicAdd(&g_gp_done, 1u) == waves - 1) {   // the launch's last wave
+      g_gp_done = 0;
+      __threadfence();
+      atomicAdd(&g_gp_count, 1u);
+    }
+  }
+#endif
 }
+
+#ifdef DQ_GATHER_PROF
+// reset (launch counter 0, per-launch mins at +inf, maxes at 0; per-wave stamps of launch
+// `target`) and read back: tools/gather_stamps.py
+extern "C" int dq_debug_gather_reset(int32_t target) {
+  static unsigned long long init[kGpLaunches][8];
+  for (int i = 0; i < kGpLaunches; ++i)
+    for (int k = 0; k < 8; ++k) init[i][k] = (k == 0 || k == 3) ? ~0ull : 0ull;
+  const unsigned zero = 0, t = (unsigned)target;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_gp_launch), init, sizeof(init)) != hipSuccess) return -1;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_gp_count), &zero, 4) != hipSuccess) return -1;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_gp_done), &zero, 4) != hipSuccess) return -1;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_gp_target), &t, 4) == hipSuccess ? 0 : -1;
+}
+extern "C" int dq_debug_gather_read(unsigned long long* launches, unsigned long long* waves,
+                                    unsigned int* count) {
+  if (hipMemcpyFromSymbol(launches, HIP_SYMBOL(g_gp_launch), sizeof(g_gp_launch)) != hipSuccess)
+    return -1;
+  if (hipMemcpyFromSymbol(waves, HIP_SYMBOL(g_gp_wave), sizeof(g_gp_wave)) != hipSuccess) return -1;
+  return hipMemcpyFromSymbol(count, HIP_SYMBOL(g_gp_count), 4) == hipSuccess ? 0 : -1;
+}
+#endif
 
 __device__ __forceinline__ int64_t frame_of(const ReplayView& v, const GatherOut& g, int slot,
                                             int* b_out, int* which_out, int* k_out) {
@@ -401,6 +462,14 @@ using namespace dq;
 extern "C" {
 
 int dq_abi_version(void) { return DQ_ABI_VERSION; }
+
+// the extra -D flags every translation unit was compiled with (dopamine_amd/_build.py
+// passes them as DQ_BUILD_FLAGS): "" for the product library
+#ifdef DQ_BUILD_FLAGS
+const char* dq_build_flags(void) { return DQ_BUILD_FLAGS; }
+#else
+const char* dq_build_flags(void) { return "(unrecorded: not built by dopamine_amd/_build.py)"; }
+#endif
 const char* dq_last_error(void) { return g_err.c_str(); }
 
 int dq_sumtree_depth(int64_t capacity) {

@@ -507,9 +507,32 @@ __device__ __forceinline__ float4 u8x4_to_f32_255(uint32_t w) {
 // kNt: non-temporal float4 stores (the line stays in L2; 5.58 -> 5.42 us alone).
 enum { kScalEarly = 0, kScalLate = 1, kScalNone = 2 };
 
+#ifdef DQ_GATHER_PROF
+// Stamp build of the standalone gather (tools/gather_stamps.py; never the product: the
+// waits below serialise what the product overlaps only where a stamp is taken).  Each wave
+// takes s_memrealtime (100 MHz) at its start, once its index is in, once its frames are in,
+// and once its stores are acknowledged; per launch (a counter the launch's last wave
+// advances) the first / last of each go to g_gp_launch, every wave's of one launch to
+// g_gp_wave.  Stamp words only ever go to these buffers.
+constexpr int kGpLaunches = 1024, kGpWaves = 4096;
+__device__ unsigned long long g_gp_launch[kGpLaunches][8];
+__device__ unsigned long long g_gp_wave[kGpWaves][4];
+__device__ unsigned int g_gp_count;
+__device__ unsigned int g_gp_done;
+__device__ unsigned int g_gp_target;
+#define GP_STAMP(gp, k)                                      \
+  do {                                                       \
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");         \
+    (gp)[k] = __builtin_amdgcn_s_memrealtime();              \
+  } while (0)
+#else
+#define GP_STAMP(gp, k) do { } while (0)
+#endif
+
 template <int R, int kScalars = kScalEarly, bool kNt = false>
 __device__ __forceinline__ void gather_nhwc4_body(const ReplayView& v, const GatherOut& g, int bx,
-                                                  int slot, int tid) {
+                                                  int slot, int tid,
+                                                  unsigned long long* gp = nullptr) {
   constexpr bool kLateScalars = kScalars == kScalLate;
   const int b = slot >> 1, which = slot & 1;
   const bool scal = kScalars != kScalNone && bx == 0 && which == 0 && tid < 64;
@@ -528,6 +551,7 @@ __device__ __forceinline__ void gather_nhwc4_body(const ReplayView& v, const Gat
   // terminal bytes and re-loaded only when a terminal makes L < n (wave-uniform
   // branch), so frames wait on the index alone: two dependent cold loads, not three.
   const int64_t idx = pymod((int64_t)g.indices[b], v.C);
+  if (gp) GP_STAMP(gp, 1);
   uint32_t w[R][4];
   auto load = [&](int64_t base) {
     const uint32_t* fr[4];
@@ -551,6 +575,7 @@ __device__ __forceinline__ void gather_nhwc4_body(const ReplayView& v, const Gat
     load(idx);
     if (kLateScalars && scal) write_scalars_wave(v, g, b, idx);
   }
+  if (gp) GP_STAMP(gp, 2);
   // store j of chunk r: lane l writes pixel 64j + l of the chunk (its 4 channels =
   // 16 B), so every store instruction covers 1 KiB contiguous; the bytes come from
   // lane 16j + l/4.

@@ -152,11 +152,34 @@ class Runner(object):
     self._checkpoint_dir = os.path.join(self._base_dir, 'checkpoints')
     self._logger = logger.Logger(os.path.join(self._base_dir, 'logs'))
 
+  def _runner_checkpoint_dir(self):
+    """Where the runner's own ``ckpt.N`` / sentinel files go: the agent's directory for this
+    learner (``_rank_dir``: ``checkpoints`` for a single replica as the reference,
+    ``checkpoints/rank<r>`` for data-parallel learners, whose runner states -- the agent's
+    ``state``, its step counters -- differ per rank).  A learner with a process group (even
+    of one rank) therefore resumes only from a rank-directory checkpoint, not from a
+    single-process one."""
+    if self._process_group() is None:
+      return self._checkpoint_dir
+    return self._agent._rank_dir(self._checkpoint_dir)
+
+  def _process_group(self):
+    """The agent's torch.distributed process group (data-parallel learners), or None."""
+    import torch.distributed as dist
+    pg = getattr(self._agent, '_pg', None)
+    return pg if isinstance(pg, dist.ProcessGroup) else None
+
   def _initialize_checkpointer_and_maybe_resume(self, checkpoint_file_prefix):
-    """Resume after the newest checkpoint that the agent accepts (run_experiment.py:210-249)."""
-    self._checkpointer = checkpointer.Checkpointer(self._checkpoint_dir, checkpoint_file_prefix)
+    """Resume after the newest checkpoint that the agent accepts (run_experiment.py:210-249).
+    Data-parallel learners agree on the iteration: the newest one EVERY rank completed."""
+    self._checkpointer = checkpointer.Checkpointer(self._runner_checkpoint_dir(),
+                                                   checkpoint_file_prefix)
     self._start_iteration = 0
-    newest = checkpointer.get_latest_checkpoint_number(self._checkpoint_dir)
+    newest = checkpointer.get_latest_checkpoint_number(self._runner_checkpoint_dir())
+    pg = self._process_group()
+    if pg is not None:
+      from dopamine_amd import parallel
+      newest = parallel.agree_min(newest, pg)
     if newest < 0:
       return
     runner_state = self._checkpointer.load_checkpoint(newest)
@@ -243,6 +266,13 @@ class Runner(object):
 
   def _log_experiment(self, iteration, statistics):
     self._logger['iteration_{:d}'.format(iteration)] = statistics
+    # data-parallel learners: group rank 0 writes the shared log files (every rank keeps its
+    # statistics in its own runner checkpoint)
+    pg = self._process_group()
+    if pg is not None:
+      import torch.distributed as dist
+      if dist.get_rank(pg) != 0:
+        return
     if iteration % self._log_every_n == 0:
       self._logger.log_to_file(self._logging_file_prefix, iteration)
 

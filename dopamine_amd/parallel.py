@@ -11,6 +11,9 @@ ranks' single-GPU gradients, not a single B*N batch.
 """
 import ctypes
 import os
+import sys
+import threading
+import time
 
 import torch
 import torch.distributed as dist
@@ -167,6 +170,68 @@ def native_comm_available(group, device):
   t = torch.tensor([ok], device=device if dist.get_backend(group) == 'nccl' else 'cpu')
   dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
   return bool(t.item() == 1.0)
+
+
+def agree_min(value, group):
+  """The smallest of an integer every rank of ``group`` holds (e.g. the newest checkpoint
+  iteration every rank completed)."""
+  dev = torch.device('cuda', torch.cuda.current_device()) if dist.get_backend(group) == 'nccl' \
+      else 'cpu'
+  t = torch.tensor([int(value)], dtype=torch.int64, device=dev)
+  dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+  return int(t.item())
+
+
+# exit status of a process whose deadline expired (Deadline)
+DEADLINE_EXIT = 3
+
+
+class Deadline(object):
+  """Host-side deadline for the blocking phases of an N > 1 run (rendezvous, the barriers
+  around the timed window, the window's captured collectives, the final exchanges).
+
+  ``phase(label, seconds)`` names what the process is about to wait for and arms the
+  deadline; ``done()`` disarms it.  A watcher thread that finds an armed deadline expired
+  prints ``rank R: <label> did not complete within S s`` to stderr and ends the process with
+  DEADLINE_EXIT (os._exit: no in-process retry, nothing after it runs; the launcher sees a
+  non-zero status instead of a hang).  A peer that died or withheld a collective leaves the
+  other ranks blocked inside RCCL / gloo, where no Python exception can reach them -- the
+  watcher is what bounds it."""
+
+  def __init__(self, rank=None, out=None, poll=0.2):
+    self.rank = int(os.environ.get('RANK', '0')) if rank is None else rank
+    self._out = out
+    self._poll = poll
+    self._lock = threading.Lock()
+    self._label, self._expires, self._seconds = None, None, None
+    self._stop = threading.Event()
+    self._thread = threading.Thread(target=self._watch, name='dq-deadline', daemon=True)
+    self._thread.start()
+
+  def phase(self, label, seconds):
+    with self._lock:
+      self._label, self._seconds = label, float(seconds)
+      self._expires = time.monotonic() + float(seconds)
+
+  def done(self):
+    with self._lock:
+      self._label = self._expires = None
+
+  def close(self):
+    self.done()
+    self._stop.set()
+
+  def _watch(self):
+    while not self._stop.wait(self._poll):
+      with self._lock:
+        expired = self._expires is not None and time.monotonic() > self._expires
+        label, seconds = self._label, self._seconds
+      if expired:
+        out = self._out or sys.stderr
+        out.write('dopamine_amd deadline: rank %d: %s did not complete within %.0f s; '
+                  'exiting with status %d\n' % (self.rank, label, seconds, DEADLINE_EXIT))
+        out.flush()
+        os._exit(DEADLINE_EXIT)
 
 
 def replicas_in_sync(flat_params, group=None):

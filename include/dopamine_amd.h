@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define DQ_ABI_VERSION 6
+#define DQ_ABI_VERSION 7
 
 /* host-side return codes */
 #define DQ_OK 0
@@ -94,6 +94,10 @@ typedef struct dq_replay_storage {   /* all device pointers, caller-owned */
 typedef struct dq_replay dq_replay;
 
 int dq_abi_version(void);
+/* the extra -D flags the library was compiled with: "" for the product build, the bf16
+   throughput build's flags for libdopamine_amd_bf16.so (dopamine_amd/_lib.py refuses any
+   other build unless DQ_DIAGNOSTIC_BUILD=1 is set, e.g. by a tools/ stamp run) */
+const char* dq_build_flags(void);
 const char* dq_last_error(void);
 /* depth of the sum tree for a capacity: ceil(log2(capacity)) (sum_tree.py:80) */
 int dq_sumtree_depth(int64_t capacity);

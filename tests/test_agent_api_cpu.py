@@ -125,6 +125,7 @@ def test_per_rider_placement_lists():
   assert tags(place(_PlaceStub(True, (1, 2, 3)), [wb, smp, gat])) == [11, 12, 13]
   assert tags(place(_PlaceStub(True, None), [wb, smp, gat])) == [11, 12, 13]
   assert tags(place(_PlaceStub(False, (2, 3, 4)), [wb, smp, gat])) == [11, 12, 13]
-  with pytest.raises(AssertionError):
-    place(_PlaceStub(True, (2, 3, 5)), [wb, smp, gat])
+  for bad in ((2, 3, 5), (3, 2, 4), (2, 4, 4), (0, 1, 2), (2, 3)):
+    with pytest.raises(ValueError, match='rider_launches'):   # also under python -O
+      place(_PlaceStub(True, bad), [wb, smp, gat])
   assert dqn_agent.DQNAgent.rider_launches == (2, 3, 4)

@@ -109,3 +109,65 @@ print('ok')
     pytest.skip('no rccl.h')
   out = subprocess.run(['python', '-c', code], cwd=ROOT, capture_output=True, text=True)
   assert out.returncode == 0 and out.stdout.strip().endswith('ok'), out.stderr[-2000:]
+
+
+def test_loaded_library_is_the_product_build():
+  """The library the package loads records the flags it was built with (dq_build_flags): the
+  product build has none (no experiment or ablation build may pass as it)."""
+  from dopamine_amd import _build, _lib
+  if os.environ.get('DOPAMINE_AMD_LIB'):
+    pytest.skip('an alternate build was asked for')
+  assert os.path.realpath(_lib.LIB_PATH) == os.path.realpath(_build.PRODUCT_LIB_PATH)
+  assert _lib.BUILD_FLAGS == '' == _build.flags_string(_build.PRODUCT_FLAGS)
+  assert _lib.lib.dq_build_flags().decode() == ''
+
+
+def _load_in_child(env_lib, diagnostic=False):
+  env = dict(os.environ, DOPAMINE_AMD_LIB=env_lib)
+  env.pop('DQ_DIAGNOSTIC_BUILD', None)
+  if diagnostic:
+    env['DQ_DIAGNOSTIC_BUILD'] = '1'
+  code = 'from dopamine_amd import _lib; print(repr(_lib.BUILD_FLAGS))'
+  return subprocess.run(['python', '-c', code], cwd=ROOT, env=env, capture_output=True, text=True)
+
+
+def test_non_product_builds_are_refused():
+  """A library whose recorded flags do not belong to its path (here the bf16 build under
+  another name) loads only with DQ_DIAGNOSTIC_BUILD=1; a library outside the tree never."""
+  import shutil
+  from dopamine_amd import _build
+  if not os.path.exists(_build.BF16_LIB_PATH):
+    pytest.skip('bf16 build absent')
+  ok = _load_in_child(_build.BF16_LIB_PATH)
+  assert ok.returncode == 0 and ok.stdout.strip() == repr(' '.join(_build.BF16_FLAGS)), ok.stderr[-800:]
+  d = os.path.join(ROOT, 'dopamine_amd', 'build')
+  os.makedirs(d, exist_ok=True)
+  copy = os.path.join(d, 'test_copy_of_bf16.so')
+  shutil.copyfile(_build.BF16_LIB_PATH, copy)
+  try:
+    bad = _load_in_child(copy)
+    assert bad.returncode != 0 and 'not a product or bf16 throughput build' in bad.stderr
+    diag = _load_in_child(copy, diagnostic=True)
+    assert diag.returncode == 0, diag.stderr[-800:]
+  finally:
+    os.remove(copy)
+  with tempfile.TemporaryDirectory() as t:
+    out = os.path.join(t, 'libdopamine_amd.so')
+    shutil.copyfile(_build.PRODUCT_LIB_PATH, out)
+    far = _load_in_child(out, diagnostic=True)
+    assert far.returncode != 0 and 'only in-tree builds' in far.stderr
+
+
+def test_product_sources_carry_only_the_bf16_build_switches():
+  """the rejected A/B knobs and the result-dropping ablations are gone from
+  the product sources; the compile-time switches left are the bf16 throughput build's two
+  (dopamine_amd/_build.py BF16_FLAGS).  #ifdef DQ_C51_PROF / DQ_GATHER_PROF are stamp
+  builds (they write timing words to buffers of their own, never results)."""
+  csrc = os.path.join(ROOT, 'dopamine_amd', 'csrc')
+  knobs, ifdefs = set(), set()
+  for f in os.listdir(csrc):
+    src = open(os.path.join(csrc, f)).read()
+    knobs |= set(re.findall(r'^#ifndef (DQ_\w+)', src, re.M))
+    ifdefs |= set(re.findall(r'^#if(?:def)?\s+(DQ_\w+)', src, re.M))
+  assert knobs == {'DQ_CNN_X6', 'DQ_X6_PAIRS'}, knobs
+  assert ifdefs <= {'DQ_C51_PROF', 'DQ_GATHER_PROF', 'DQ_BUILD_FLAGS'}, ifdefs

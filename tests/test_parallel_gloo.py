@@ -199,3 +199,153 @@ def test_data_parallel_checkpoints_go_to_rank_directories():
     assert p.exitcode == 0
   for r in range(world):
     assert res[r] == (os.path.join('/ck', 'rank%d' % r), '/ck')
+
+
+# ---------------------------------------------------------------- N > 1 deadline
+def _deadline_worker(rank, world, port, path, withhold):
+  os.environ['MASTER_ADDR'] = '127.0.0.1'
+  os.environ['MASTER_PORT'] = str(port)
+  dist.init_process_group('gloo', rank=rank, world_size=world)
+  from dopamine_amd import parallel
+  import time
+  if rank == withhold:            # this rank never enters the collective
+    time.sleep(30)
+    os._exit(0)
+  dl = parallel.Deadline(rank, out=open(path % rank, 'w'))
+  dl.phase('the fc bucket all_reduce of step 7', 3)
+  t = torch.ones(4)
+  dist.all_reduce(t)              # blocks: the peer withholds it; the deadline ends us
+  os._exit(0)                     # not reached
+
+
+@pytest.mark.timeout(120)
+def test_deadline_reports_rank_and_collective_and_exits(tmp_path):
+  """parallel.Deadline (bench.py's N > 1 phases): a rank blocked in a collective that a
+  peer withholds reports which rank and which phase, and exits with DEADLINE_EXIT instead
+  of hanging."""
+  from dopamine_amd import parallel
+  ctx = mp.get_context('spawn')
+  port = _free_port()
+  path = str(tmp_path / 'dl_%d.txt')
+  procs = [ctx.Process(target=_deadline_worker, args=(r, 2, port, path, 1)) for r in range(2)]
+  for p in procs:
+    p.start()
+  procs[0].join(timeout=90)
+  assert procs[0].exitcode == parallel.DEADLINE_EXIT
+  msg = open(path % 0).read()
+  assert 'rank 0: the fc bucket all_reduce of step 7 did not complete within 3 s' in msg, msg
+  procs[1].kill()
+  procs[1].join(timeout=30)
+
+
+def test_deadline_disarmed_never_fires():
+  import time
+  from dopamine_amd import parallel
+  dl = parallel.Deadline(0, poll=0.01)
+  dl.phase('short phase', 0.05)
+  dl.done()
+  time.sleep(0.2)                 # would have expired had it stayed armed
+  dl.close()
+
+
+# ------------------------------------------------- rank-aware Runner checkpoints
+class _StubAgent(object):
+  """The agent interface the Runner uses (bundle / unbundle / step), with a process group:
+  per-rank state, files under checkpoint_dir/rank<r> as DQNAgent._rank_dir."""
+
+  def __init__(self, pg):
+    self._pg = pg
+    self.eval_mode = False
+    self.state = np.zeros(1)
+    self.training_steps = 0
+
+  def _rank_dir(self, d):
+    return os.path.join(d, 'rank%d' % dist.get_rank(self._pg))
+
+  def begin_episode(self, obs):
+    return 0
+
+  def step(self, r, obs):
+    self.training_steps += 1 + dist.get_rank(self._pg)    # ranks diverge
+    return 0
+
+  def end_episode(self, r):
+    pass
+
+  def bundle_and_checkpoint(self, d, it):
+    os.makedirs(self._rank_dir(d), exist_ok=True)
+    return {'training_steps': self.training_steps}
+
+  def unbundle(self, d, it, bundle):
+    if bundle is None:
+      return False
+    self.training_steps = bundle['training_steps']
+    return True
+
+
+class _Env(object):
+  game_over = False
+
+  class action_space(object):
+    n = 2
+
+  def reset(self):
+    return np.zeros(4)
+
+  def step(self, a):
+    return np.zeros(4), 1.0, False, {}
+
+
+def _runner_worker(rank, world, port, base, q, iters, drop_last_on):
+  os.environ['MASTER_ADDR'] = '127.0.0.1'
+  os.environ['MASTER_PORT'] = str(port)
+  dist.init_process_group('gloo', rank=rank, world_size=world)
+  from dopamine_amd.discrete_domains import run_experiment
+  pg = dist.group.WORLD
+  mk = lambda sess, env, summary_writer=None: _StubAgent(pg)
+  r = run_experiment.Runner(base, mk, _Env, num_iterations=iters, training_steps=5,
+                            evaluation_steps=0, max_steps_per_episode=5)
+  start = r._start_iteration
+  r.run_experiment()
+  ck = os.path.join(base, 'checkpoints', 'rank%d' % rank)
+  if rank == drop_last_on:          # this rank "crashed" before its last sentinel landed
+    os.remove(os.path.join(ck, 'sentinel_checkpoint_complete.%d' % (iters - 1)))
+  q.put((rank, start, r._agent.training_steps, sorted(os.listdir(ck)),
+         sorted(os.listdir(os.path.join(base, 'checkpoints')))))
+  dist.barrier()
+  dist.destroy_process_group()
+
+
+def _runner_round(base, iters, drop_last_on=-1):
+  ctx = mp.get_context('spawn')
+  q = ctx.Queue()
+  port = _free_port()
+  procs = [ctx.Process(target=_runner_worker, args=(r, 2, port, base, q, iters, drop_last_on))
+           for r in range(2)]
+  for p in procs:
+    p.start()
+  res = dict((r, rest) for r, *rest in (q.get(timeout=120) for _ in range(2)))
+  for p in procs:
+    p.join(timeout=60)
+    assert p.exitcode == 0
+  return res
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_runner_checkpoints_are_per_rank_and_resume_together(tmp_path):
+  """Runner with data-parallel learners: each rank's ckpt.N and sentinel go to
+  checkpoints/rank<r> (its own runner state), logs only from rank 0, and on resume the
+  ranks agree on the newest iteration EVERY rank completed."""
+  base = str(tmp_path / 'run')
+  res = _runner_round(base, 3, drop_last_on=1)
+  for r in (0, 1):
+    start, steps, files, top = res[r]
+    assert start == 0 and top == ['rank0', 'rank1']
+    assert 'ckpt.2' in files
+  assert res[0][1] != res[1][1]                       # per-rank states differ
+  assert 'sentinel_checkpoint_complete.2' not in res[1][2]
+  # resume: rank 1 lacks iteration 2's sentinel, so both ranks restart after iteration 1
+  res2 = _runner_round(base, 4)
+  assert res2[0][0] == 2 and res2[1][0] == 2
+  logs = sorted(os.listdir(os.path.join(base, 'logs')))
+  assert logs and all(f.startswith('log_') for f in logs)

@@ -2,7 +2,7 @@
 flags into ab/<name>/, link them with the in-tree objects of the others.
   python tools/build_variant.py <name> <tu[,tu..]> [-DFLAG ...]
 e.g.  python tools/build_variant.py c51prof learner -DDQ_C51_PROF
-The variant loads through DOPAMINE_AMD_LIB=ab/<name>/libdopamine_amd.so."""
+The variant loads through DQ_DIAGNOSTIC_BUILD=1 DOPAMINE_AMD_LIB=ab/<name>/libdopamine_amd.so."""
 import os
 import subprocess
 import sys
@@ -19,8 +19,14 @@ def main():
   out_dir = os.path.join(ROOT, 'ab', name)
   os.makedirs(out_dir, exist_ok=True)
   bdir = os.path.join(ROOT, 'dopamine_amd', 'build')
+  # the variant records what it is (dq_build_flags); replay.hip, which exports it, is always
+  # recompiled, so a variant never reports the product's empty flags.  It loads only with
+  # DQ_DIAGNOSTIC_BUILD=1 (dopamine_amd/_lib.py).
+  tus.setdefault('replay', None)
+  note = 'variant %s: %s %s' % (name, ','.join(sorted(tus)), ' '.join(extra))
   flags = ['--offload-arch=' + _build.ARCH, '-O3', '-fPIC', '-std=c++17', '-ffp-contract=off',
-           '-I', os.path.join(ROOT, 'dopamine_amd', 'csrc')] + extra
+           '-I', os.path.join(ROOT, 'dopamine_amd', 'csrc')] + extra + [
+               '-DDQ_BUILD_FLAGS="%s"' % note.replace('"', "'")]
   objs, procs = [], []
   for src in _build.SOURCES:
     tu = os.path.splitext(os.path.basename(src))[0]

@@ -4,7 +4,9 @@
 # step timeline of each (DQ_NOAB=1: the timelines only).
 #   gpurun -- 'DQ_TESTS="tests/test_gpu_cnn.py ..." CFG=rainbow DQ_TIMELINE=1 \
 #     bash tools/gpu_ab.sh <out-name> ab/X/libdopamine_amd.so "args:--split-c51 1" ...'
-# (the environment is set inside the gpurun command: gpurun does not forward it)
+# (the environment is set inside the gpurun command: gpurun does not forward it).  "args:"
+# flags are tools/bench_ab.py's schedule experiments; variant builds load with
+# DQ_DIAGNOSTIC_BUILD=1 (their recorded flags are not the product's).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -18,7 +20,7 @@ if [ -n "$DQ_TESTS" ]; then
     lib=$spec
     case "$spec" in args:*) continue;; *"|"*) lib=${spec%%|*};; esac
     n=$(basename $(dirname $lib))
-    DOPAMINE_AMD_LIB=$lib timeout -k 10 600 python -u -m pytest $DQ_TESTS -m gpu -v \
+    DQ_DIAGNOSTIC_BUILD=1 DOPAMINE_AMD_LIB=$lib timeout -k 10 600 python -u -m pytest $DQ_TESTS -m gpu -v \
       --timeout 300 --timeout-method thread > $OUT/tests_$n.log 2>&1
     rc=$?; echo "[$n] tests rc=$rc"; tail -1 $OUT/tests_$n.log; grep FAILED $OUT/tests_$n.log | head
     if [ $rc -ne 0 ]; then exit $rc; fi
@@ -31,10 +33,10 @@ for rep in $([ -z "$DQ_NOAB" ] && echo 1 2); do
     lib=$spec; extra=
     case "$spec" in args:*) lib=; extra=${spec#args:};; *"|"*) lib=${spec%%|*}; extra=${spec#*|};; esac
     if [ "${CFG:-rainbow}" = rainbow ]; then
-      line=$(DOPAMINE_AMD_LIB=$lib timeout -k 10 240 python bench.py --steps ${STEPS:-2000} --skip-cpu-baseline --skip-bf16 --skip-configs --gather-iters 20 $extra 2>>$OUT/err.log | tail -1) || exit 1
+      line=$(DQ_DIAGNOSTIC_BUILD=1 DOPAMINE_AMD_LIB=$lib timeout -k 10 240 python tools/bench_ab.py $extra -- --steps ${STEPS:-2000} --skip-cpu-baseline --skip-bf16 --skip-configs --gather-iters 20 2>>$OUT/err.log | tail -1) || exit 1
       v=$(echo "$line" | python3 -c 'import sys,json; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')
     else
-      v=$(DOPAMINE_AMD_LIB=$lib timeout -k 10 240 python tools/bench_configs.py ${STEPS:-300} $CFG $extra 2>>$OUT/err.log | tail -1) || exit 1
+      v=$(DQ_DIAGNOSTIC_BUILD=1 DOPAMINE_AMD_LIB=$lib timeout -k 10 240 python tools/bench_configs.py ${STEPS:-300} $CFG $extra 2>>$OUT/err.log | tail -1) || exit 1
     fi
     echo "[${spec:-in-tree}] $v" | tee -a $OUT/ab.log
   done
@@ -46,7 +48,7 @@ if [ -n "$DQ_TIMELINE" ]; then
     lib=$spec; extra=
     case "$spec" in args:*) lib=; extra=${spec#args:};; *"|"*) lib=${spec%%|*}; extra=${spec#*|};; esac
     n=t$i
-    DOPAMINE_AMD_LIB=$lib timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/r_$n -o run -- python3 bench.py --skip-cpu-baseline --skip-bf16 --skip-configs --gather-iters 20 $extra > $OUT/prof_$n.log 2>&1 || exit 1
+    DQ_DIAGNOSTIC_BUILD=1 DOPAMINE_AMD_LIB=$lib timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/r_$n -o run -- python3 tools/bench_ab.py $extra -- --skip-cpu-baseline --skip-bf16 --skip-configs --gather-iters 20 > $OUT/prof_$n.log 2>&1 || exit 1
     echo "== [$n] ${spec:-in-tree}" >> $OUT/timelines.txt
     python3 tools/step_timeline_db.py /tmp/r_$n/run_results.db k_c51 30 > $OUT/timeline_$n.txt
     cat $OUT/timeline_$n.txt >> $OUT/timelines.txt

@@ -1,0 +1,71 @@
+"""Where a short timed window's time goes (the driver's 20-step window read
+2-3% below 300-step windows of the same build).  After bench.py's priming, times windows of
+K steps exactly as bench.timed_steps does (synchronize, perf_counter, train_gradient_steps,
+synchronize) and splits each into: host time before the first chunk graph is handed to the
+GPU, host submission time of the whole window, and the GPU's time from an event recorded at
+the window start to one recorded at its end.
+
+    python tools/window_probe.py [K ...]
+"""
+import gc
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def main():
+  import bench
+  ks = [int(x) for x in sys.argv[1:]] or [20, 300]
+  dev = torch.device('cuda', 0)
+  torch.cuda.set_device(0)
+  agent = bench.build_agent(9, 1_000_000, 32, dev)
+  import random
+  random.seed(0)
+  bench.fill_synthetic(agent._replay.memory, 9, seed=1)
+  torch.cuda.synchronize()
+  bench.timed_steps(agent, 20, 5)          # bench's priming (graphs captured, clocks up)
+  first = {}
+
+  def wrap(g):
+    orig = g.replay
+
+    def replay():
+      if 't' not in first:
+        first['t'] = time.perf_counter()
+      orig()
+    g.replay = replay
+  for key, g in agent._graph_sets.items():
+    if isinstance(key, tuple) and key[0] == 'chunk':
+      wrap(g)
+  stream = torch.cuda.current_stream()
+  rows = {k: [] for k in ks}
+  gc.disable()
+  for rep in range(6):
+    for k in ks:
+      first.clear()
+      e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+      torch.cuda.synchronize()
+      t0 = time.perf_counter()
+      e0.record(stream)
+      agent.train_gradient_steps(k)
+      ts = time.perf_counter()
+      e1.record(stream)
+      torch.cuda.synchronize()
+      t1 = time.perf_counter()
+      rows[k].append((first.get('t', ts) - t0, ts - t0, e0.elapsed_time(e1) * 1e-3, t1 - t0))
+  gc.enable()
+  print('K   pre-first-replay us   host submit us   GPU e0->e1 us   wall us   steps/s wall   '
+        'steps/s GPU   (medians of 6)')
+  for k in ks:
+    a = np.median(np.array(rows[k]), axis=0) * 1e6
+    print('%4d %12.1f %16.1f %15.1f %10.1f %12.1f %14.1f' % (k, a[0], a[1], a[2], a[3],
+                                                             k / a[3] * 1e6, k / a[2] * 1e6))
+
+
+if __name__ == '__main__':
+  main()
