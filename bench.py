@@ -48,11 +48,13 @@ def parse(argv=None):
                   help='drive the agent by update_period _train_step() calls per gradient '
                        'step (one graph replay per step) instead of train_gradient_steps')
   ap.add_argument('--gather-iters', type=int, default=400)
-  ap.add_argument('--zero', type=int, default=None,
-                  help='N > 1: time only the replicated all-reduce schedule (0) or only ZeRO-1 '
-                       'for the fc bucket (1: DQNAgent shard_optimizer -- reduce-scatter, TF1 '
-                       'Adam on the rank\'s slice, all-gather); default: both, headline from the '
-                       'faster')
+  ap.add_argument('--schedules', default=None,
+                  help='N > 1 (or --force-dist): comma-separated data-parallel schedules to time, '
+                       'one after the other on fresh agents, the headline from the fastest -- '
+                       'peer (the exchange over peer memory inside the backward, one stream: '
+                       'DQNAgent exchange=\'peer\'), allreduce (the gradient buckets\' '
+                       'all-reduce on a second stream), zero1 (its reduce-scatter / slice Adam / '
+                       'all-gather form); default peer,allreduce')
   ap.add_argument('--comm', choices=('native', 'torch'), default='native',
                   help='N > 1 over RCCL: the learner\'s own communicators (parallel.RcclComm) '
                        'or torch.distributed\'s collectives')
@@ -471,22 +473,26 @@ def main(argv=None):
     os.environ.setdefault('MASTER_PORT', '29533')
     dist.init_process_group('nccl', rank=0, world_size=1, device_id=dev)
     pg = dist.group.WORLD
-  # N > 1: the replicated all-reduce schedule and ZeRO-1 are both timed, one
-  # after the other on fresh agents, and the headline is the faster (both are reported)
-  zeros = [0, 1] if (pg is not None and args.zero is None) else [int(args.zero or 0)]
+  # N > 1: the data-parallel schedules are timed one after the other on fresh
+  # agents, and the headline is the fastest (every one is reported)
+  names = ['single'] if pg is None else (args.schedules or 'peer,allreduce').split(',')
+  kwargs_of = {'single': {}, 'peer': {'exchange': 'peer'}, 'allreduce': {},
+               'zero1': {'shard_optimizer': True}}
+  assert all(n in kwargs_of for n in names), names
   schedules = {}
   agent = None
-  for zero in zeros:
+  for name in names:
     if agent is not None:
       agent.close()                   # its RCCL communicators (N > 1) before the next pair
       del agent
       gc.collect()
       torch.cuda.empty_cache()
     if deadline is not None:
-      deadline.phase('building the learner (RCCL communicators, rank-0 broadcast)', DEADLINE_S)
+      deadline.phase('building the %s learner (RCCL communicators or peer mappings, rank-0 '
+                     'broadcast)' % name, DEADLINE_S)
     agent = build_agent(args.actions, args.capacity, args.batch, dev, pg=pg,
                         use_hip_graph=not args.no_graph, native_comm=args.comm == 'native',
-                        **AGENT_OVERRIDES, **({'shard_optimizer': True} if zero else {}))
+                        **AGENT_OVERRIDES, **kwargs_of[name])
     import random
     random.seed(0 + rank)
     fill_synthetic(agent._replay.memory, args.actions, seed=1 + rank)
@@ -505,11 +511,12 @@ def main(argv=None):
     agent._replay.memory.sync_rng()   # raises if the device latched a sampling error
     loss = agent.mean_loss()
     assert np.isfinite(loss), 'non-finite loss'
-    schedules['zero1' if zero else 'allreduce'] = {
+    schedules[name] = {
         'value': round(world * args.steps / elapsed, 2), 'ms_per_step': round(1e3 * elapsed / args.steps, 4),
         'per_rank_ms_per_step': [round(1e3 * e / args.steps, 4) for e in per_rank],
         'prime_steps': prime, 'final_mean_loss': round(loss, 5), '_elapsed': elapsed,
-        'comm': (args.comm if agent._rccl is not None or args.comm == 'torch' else 'torch')
+        'comm': ('peer memory (one stream)' if agent._peer is not None else
+                 args.comm if agent._rccl is not None or args.comm == 'torch' else 'torch')
         if pg is not None else None}
   best = min(schedules, key=lambda k: schedules[k]['_elapsed'])
   elapsed, prime, loss = (schedules[best]['_elapsed'], schedules[best]['prime_steps'],
@@ -556,7 +563,9 @@ def main(argv=None):
                    'replay_capacity': args.capacity,
                    'parallelism': 'dp%d' % world + (' (one-rank RCCL group, --force-dist)'
                                                     if args.force_dist and world == 1 else '')
-                                  + (', ZeRO-1 fc bucket' if best == 'zero1' else ''),
+                                  + {'zero1': ', ZeRO-1 fc bucket over RCCL',
+                                     'allreduce': ', all-reduce over RCCL',
+                                     'peer': ', peer-memory exchange on one stream'}.get(best, ''),
                    'hip_graph': not args.no_graph},
         'roofline': {'kernel': gname + ' (frame-stack gather + /255, state+next_state)',
                      'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,

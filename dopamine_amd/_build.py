@@ -20,7 +20,7 @@ def _lib_path():
 
 
 LIB_PATH = _lib_path()
-SOURCES = [os.path.join(_HERE, 'csrc', f) for f in ('replay.hip', 'learner.hip', 'nature_cnn.hip', 'iqn.hip', 'comm.hip')]
+SOURCES = [os.path.join(_HERE, 'csrc', f) for f in ('replay.hip', 'learner.hip', 'nature_cnn.hip', 'iqn.hip', 'comm.hip', 'peer.hip')]
 HEADER = os.path.join(os.path.dirname(_HERE), 'include', 'dopamine_amd.h')
 ARCH = os.environ.get('DQ_OFFLOAD_ARCH', 'gfx950')
 

@@ -9,7 +9,7 @@ import os
 from dopamine_amd import _build
 from dopamine_amd._build import HEADER, LIB_PATH  # noqa: F401
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 OK = 0
 (ST_OK, ST_EMPTY_TREE, ST_MAX_ATTEMPTS, ST_TAPE_EXHAUSTED, ST_NEG_PRIORITY, ST_TOO_FEW, ST_BAD_INDEX,
  ST_BROADCAST) = range(8)
@@ -101,6 +101,23 @@ class IqnGrads(ctypes.Structure):
 class Rider(ctypes.Structure):
   """dq_rider: a recorded replay operation (opaque)."""
   _fields_ = [('words', ctypes.c_int64 * 40)]
+
+
+PEER_MAX = 8            # DQ_PEER_MAX
+PEER_FLAG_WORDS = 8     # DQ_PEER_FLAG_WORDS
+(PEER_STEP, PEER_GRAD, PEER_PARAM, PEER_CONV, PEER_ERR, PEER_TICKET) = range(6)
+
+
+class IpcHandle(ctypes.Structure):
+  _fields_ = [('handle', ctypes.c_uint8 * 64), ('offset', ctypes.c_int64)]
+
+
+class Peer(ctypes.Structure):
+  """dq_peer: the data-parallel exchange over peer memory."""
+  _fields_ = [('world', ctypes.c_int32), ('rank', ctypes.c_int32), ('lo', ctypes.c_int64),
+              ('n', ctypes.c_int64), ('grad', ctypes.c_void_p * PEER_MAX),
+              ('param', ctypes.c_void_p * PEER_MAX), ('flags', ctypes.c_void_p * PEER_MAX),
+              ('max_polls', ctypes.c_int64)]
 
 
 _P = ctypes.c_void_p
@@ -204,6 +221,15 @@ SIGNATURES = {
     'dq_comm_reduce_scatter_mean': [_P, _P, _I64, _P],
     'dq_comm_all_gather': [_P, _P, _I64, _P],
     'dq_comm_version': [],
+    'dq_peer_ipc_get': [_P, ctypes.POINTER(IpcHandle)],
+    'dq_peer_ipc_open': [ctypes.POINTER(IpcHandle), ctypes.POINTER(ctypes.c_void_p),
+                         ctypes.POINTER(ctypes.c_void_p)],
+    'dq_peer_ipc_close': [_P],
+    'dq_peer_can_access': [_I32, _I32],
+    'dq_cnn_backward_peer': [ctypes.POINTER(CnnParams), ctypes.POINTER(CnnParams), _I32, _P,
+                             ctypes.POINTER(CnnActs), _P, ctypes.POINTER(CnnActs), _P,
+                             ctypes.POINTER(Rider), _I32, ctypes.POINTER(AdamArgs),
+                             ctypes.POINTER(CnnNet), ctypes.POINTER(Peer), _P],
 }
 RESTYPES = {'dq_last_error': ctypes.c_char_p, 'dq_build_flags': ctypes.c_char_p, 'dq_cnn_workspace_floats': ctypes.c_size_t,
             'dq_iqn_workspace_floats': ctypes.c_size_t,

@@ -93,7 +93,8 @@ class DQNAgent(object):
                seed=0,
                process_group=None,
                shard_optimizer=False,
-               native_comm=True):
+               native_comm=True,
+               exchange='collective'):
     assert num_actions is not None
     assert isinstance(observation_shape, tuple)      # abstract_agent.py:34
     self.num_actions = num_actions
@@ -130,6 +131,14 @@ class DQNAgent(object):
     # (parallel.RcclComm, issued on the stream each bucket runs on) instead of
     # torch.distributed's collectives (each forked onto the process group's own stream)
     self.native_comm = bool(native_comm)
+    # N > 1: 'collective' -- the gradient buckets' all-reduce (RCCL / gloo) on a second stream
+    # beside the backward (_split_step); 'peer' -- the exchange over peer memory inside the
+    # backward's own launches on ONE stream (parallel.PeerExchange): one node,
+    # the HIP Nature CNN with the fused Rainbow schedule and TF1 Adam
+    if exchange not in ('collective', 'peer'):
+      raise ValueError("exchange must be 'collective' or 'peer'")
+    self.exchange = exchange
+    self._peer = None
     self._rccl = None
     self._pg_conv = None           # a second communicator for the conv bucket (see _split_step)
     self._fc_pending = None        # event: the previous step's fc all-reduce + update are done
@@ -177,6 +186,8 @@ class DQNAgent(object):
       self._comm_opt = torch.cuda.Stream(self._device)    # ... and the Adam parts behind them
       if self._pg is not None:
         self._broadcast_replica()
+        if self.exchange == 'peer':
+          self._peer = self._make_peer_exchange()
         self._rccl = self._make_native_comms()
     self._observation = None
     self._last_observation = None
@@ -199,13 +210,39 @@ class DQNAgent(object):
       return None        # every rank agreed: torch.distributed's collectives instead
     return (parallel.RcclComm(self._pg, self._device), parallel.RcclComm(self._pg, self._device))
 
+  def _make_peer_exchange(self):
+    """The peer-memory exchange (exchange='peer').  Collective: every rank constructs its
+    agent.  Raises if the learner's schedule or placement cannot run it."""
+    if not (self._hip is not None and isinstance(self._opt, ops.TF1Adam) and self._fused()
+            and self._head_from() == 6 and self.fuse_optimizer):
+      raise ValueError("exchange='peer' needs the HIP Nature CNN's fused schedule (ride_replay, "
+                       "fused_head, fuse_optimizer) and TF1 Adam")
+    if not parallel.PeerExchange.available(self._pg, self._device):
+      raise RuntimeError("exchange='peer': the learners are not on one node with peer access "
+                         "between their devices")
+    lo, n = self._shard_bounds()
+    return parallel.PeerExchange(self._pg, self._device, self.online_convnet.fp.grad,
+                                 self.online_convnet.fp.flat, lo, n)
+
+  def _collective(self):
+    """N > 1 with the gradient exchange outside the backward (collectives between graphs or
+    on a second stream); False for a single replica and for the peer exchange, whose
+    learners run the single-replica schedule on one stream."""
+    return self._pg is not None and self._peer is None
+
   def close(self):
     """Releases the learner's RCCL communicators (each holds proxy threads and device
-    buffers until destroyed): waits for the device, drops the HIP graphs that captured
-    their collectives, then destroys them.  The agent cannot train afterwards.  A no-op
-    for a single replica."""
+    buffers until destroyed) or peer mappings: waits for the device, drops the HIP graphs
+    that captured their collectives, then destroys them.  The agent cannot train
+    afterwards.  A no-op for a single replica."""
     self._join_fc()
     torch.cuda.synchronize(self._device)
+    if self._peer is not None:
+      self._graph_sets = {}
+      self._graph_pool = None
+      self._peer.close()
+      self._peer = None
+      self._closed = True
     if self._rccl is not None:
       self._graph_sets = {}
       self._graph_pool = None
@@ -358,7 +395,7 @@ class DQNAgent(object):
     k_adam / k_rmsprop step and 3.5% faster on MI355X for Adam (5,500 vs 5,315
     steps/s).  (Earlier forms were slower: the whole update in the last launch -1.5%;
     Adam in every gradient epilogue -12%, scalar RMW of 4M fc1 parameters.)"""
-    return (self.fuse_optimizer and self._hip is not None and self._pg is None and
+    return (self.fuse_optimizer and self._hip is not None and not self._collective() and
             isinstance(self._opt, (ops.TF1Adam, ops.TF1RMSProp)))
 
   def _store_grads(self):
@@ -369,6 +406,9 @@ class DQNAgent(object):
     return bool(self.keep_gradients or self._trace is not None)
 
   def _backward(self, y, g, k=0):
+    if self._peer is not None:      # the exchange inside the backward (non-pipelined steps too)
+      self._hip['online'].backward_peer(g, self._opt, k, self._peer.desc)
+      return
     if self._hip is not None:       # all gradients stored into the flat buffer
       groups = (1, 7) if self._fused() else None    # fused: d h came with the loss
       if self._fused_opt():
@@ -574,6 +614,11 @@ class DQNAgent(object):
         self._post_loss(self._pbuf[c])
         self._prefetch(1 - c)
       riders = self._place_riders(riders)
+      if self._peer is not None:      # the exchange inside the backward's launches (one stream)
+        self._hip['online'].backward_peer(g, self._opt, k, self._peer.desc, riders=riders,
+                                          head=self._head)
+        self._head = None
+        return
       adam = self._opt if self._fused_opt() else None
       f = self._bwd_first()
       self._hip['online'].store_grads = self._store_grads()
@@ -603,7 +648,7 @@ class DQNAgent(object):
   _SPLIT = 3
 
   def _split_allreduce(self):
-    return self._pg is not None and self._hip is not None and not self._fused_opt()
+    return self._collective() and self._hip is not None and not self._fused_opt()
 
   def _head_splits(self):
     """The N > 1 head graph splits before fc1's forward (fused Rainbow path), so the
@@ -699,6 +744,8 @@ class DQNAgent(object):
 
   def _sharded(self):
     """shard_optimizer in effect: N > 1 (or forced collectives) with TF1 Adam."""
+    if self._peer is not None:      # each learner keeps its own slice's moments
+      return True
     return (self.shard_optimizer and self._pg is not None and isinstance(self._opt, ops.TF1Adam)
             and (self._world() > 1 or parallel.FORCE_COLLECTIVES))
 
@@ -863,7 +910,7 @@ class DQNAgent(object):
       self._opt.step_multi([prm.grad for prm in self.online_convnet.parameters()], slot=k)
 
   def _allreduce_grads(self):
-    if self._pg is None:
+    if not self._collective():
       return
     parallel.allreduce_mean_(self.online_convnet.fp.grad, self._pg)
 
@@ -885,7 +932,7 @@ class DQNAgent(object):
   chunk_gather = True
 
   def _chunk_gathers(self):
-    return (self.chunk_gather and self._fused() and self._pg is None and
+    return (self.chunk_gather and self._fused() and not self._collective() and
             not self._replay.memory._prioritized)
 
   def _cb_sets(self):
@@ -945,8 +992,7 @@ class DQNAgent(object):
       finally:
         self._gather_plan = None
         self._pbuf[:] = saved
-    for _ in range(K):
-      mem.reserve_rng(self._batch_size)
+    mem.reserve_rng(self._batch_size, steps=K)
     self._graph_sets[key].replay()
     self._opt_steps += K
     last = self._cbv[p][K - 2]          # the batch the chunk's last step trained on
@@ -1002,7 +1048,7 @@ class DQNAgent(object):
         self._eager_steps[pipe] += 1
     elif graphs is not None:
       graphs[0][k].replay()
-      if self._pg is not None:
+      if self._collective():
         self._allreduce_grads()
         graphs[1][k].replay()
     else:
@@ -1063,12 +1109,12 @@ class DQNAgent(object):
       g = torch.cuda.CUDAGraph()
       with torch.cuda.graph(g, pool=pool, capture_error_mode='thread_local'):
         self._grad_step(c, k, pipe)
-        if self._pg is None:
+        if not self._collective():
           self._device_opt_step(k)
           self._trace_step(self._UNROLL + k, c)
       pool = g.pool()
       graphs.append(g)
-      if self._pg is not None:
+      if self._collective():
         go = torch.cuda.CUDAGraph()
         with torch.cuda.graph(go, pool=pool, capture_error_mode='thread_local'):
           self._device_opt_step(k)
@@ -1255,7 +1301,7 @@ class DQNAgent(object):
     """N > 1 over the learner's own RCCL communicators with the split fused-head schedule:
     the gradient all-reduces are captured inside the learner loop's chunk graphs (gloo's
     host-side collectives cannot be, torch.distributed's are not)."""
-    if self._pg is None:
+    if not self._collective():
       return False
     import torch.distributed as dist
     # (torch.distributed's own collectives are never captured: parallel.collectives_capturable)
@@ -1267,7 +1313,7 @@ class DQNAgent(object):
 
   def _chunks_apply(self):
     return (self._hip is not None and self.pipeline and
-            (self._pg is None or self._captures_collectives()))
+            (not self._collective() or self._captures_collectives()))
 
   def _chunk_ok(self):
     K, U = self._UNROLL, self.update_period
@@ -1297,7 +1343,7 @@ class DQNAgent(object):
       self._join_fc()                 # nothing outside the capture may be pending
       torch.cuda.synchronize(self._device)
       g = torch.cuda.CUDAGraph()
-      if self._pg is None:
+      if not self._collective():
         with torch.cuda.graph(g, pool=self._graph_pool):
           for j in range(K):
             k = (k0 + j) % 2
@@ -1322,8 +1368,7 @@ class DQNAgent(object):
       self._graph_sets[key] = g
     else:
       self._join_fc()
-    for _ in range(K):
-      mem.reserve_rng(self._batch_size)
+    mem.reserve_rng(self._batch_size, steps=K)
     g.replay()
     self._opt_steps += K
     c = (k0 + K - 1) % 2
@@ -1353,7 +1398,10 @@ class DQNAgent(object):
 
   def mean_loss(self):
     """Mean loss of the last gradient step (the summary scalar, dqn:318-321); the fused
-    head's loss kernel leaves the mean to this call (it is not on the gradient path)."""
+    head's loss kernel leaves the mean to this call (it is not on the gradient path).
+    With the peer exchange it also raises if a wait of it timed out (a latched error)."""
+    if self._peer is not None:
+      self._peer.check()
     if self._fused():
       return float(self._loss_out['loss'].double().mean().item())
     return float(self._loss_out['mean_loss'].item())

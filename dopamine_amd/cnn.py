@@ -112,6 +112,29 @@ class HipNatureCNN(object):
                          state=adam.state.data_ptr(), slot=int(slot), lr=adam.lr,
                          beta1=adam.b1, beta2=adam.b2, epsilon=adam.eps, no_grad_store=ngs)
 
+  def backward_peer(self, dout, adam, slot, peer, riders=None, head=None):
+    """The fused Rainbow schedule's backward (head_from 6, from launch 1) with the data-
+    parallel exchange over peer memory (dq_cnn_backward_peer; ``peer``: a _lib.Peer) in
+    place of the fused optimizer's updates: the gradients are stored, this rank's slice of
+    the fc bucket is reduce-scattered and updated inside launches 3-4, the conv bucket and
+    the all-gather in launch 6.  Rider i rides in launch 1 + i."""
+    dout = dout.reshape(self.B, self.n_out)
+    assert dout.is_contiguous() and self._x is not None
+    args = self._adam_args(adam, slot)
+    args.no_grad_store = 0
+    riders = riders or []
+    arr = (_lib.Rider * max(1, len(riders)))(*riders)
+    hn = None
+    if head is not None:
+      assert head[0] is not self
+      hn = ctypes.byref(head[0].cnn_net(head[1]))
+    _lib.check(_lib.lib.dq_cnn_backward_peer(
+        ctypes.byref(self._p), ctypes.byref(self._g), self.B, self._x.data_ptr(),
+        ctypes.byref(self._a), dout.data_ptr(), ctypes.byref(self._d), self.ws.data_ptr(),
+        arr, len(riders), ctypes.byref(args), hn, ctypes.byref(peer), self._stream(dout)),
+        'dq_cnn_backward_peer')
+    return self.net.fp.grad
+
   def backward(self, dout, parallel=False, adam=None, slot=0, groups=None, riders=None, head=None,
                head_from=3):
     """dout: (B, n_out).  Writes all parameter gradients into net.fp.grad.

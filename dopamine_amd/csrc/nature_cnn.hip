@@ -235,6 +235,220 @@ struct AdamOp {
   int blocks() const { return nb; }
 };
 
+// ------------------------------------------------- data-parallel exchange over peer memory
+// (dq_peer, include/dopamine_amd.h).  Every rank's flat gradient, parameter and
+// flag buffers are mapped into every learner; the exchange runs as ops of the backward's
+// grouped launches.  Flag words per rank: [0] step counter e (local; the exchange launch's
+// last block advances it), [1] fc-bucket gradient of step e final (= e + 1), [2] this rank's
+// slice of the parameters updated, [3] conv bucket gradient final, [4] error latch (1 + the
+// flag a wait timed out on), [5] the exchange launch's block ticket.
+// Loads of another rank's (and, uniformly, one's own) exchanged words are system-coherent
+// (sc0 sc1: no stale line of a previous step in this GPU's caches); a flag is a system-scope
+// store behind a system release (s_waitcnt after it: the guide's compiler-hazard rule).
+enum { kPeerStep = 0, kPeerGrad = 1, kPeerParam = 2, kPeerConv = 3, kPeerErr = 4, kPeerTicket = 5 };
+
+__device__ __forceinline__ uint64_t peer_load(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void peer_store(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// 16 bytes at base[4 i4 ..] with the system-coherent cache policy (cpol sc0 | sc1 = 1 | 16);
+// the resource is the (wave-uniform) base, the lane's offset a VGPR (buffers < 2 GB)
+__device__ __forceinline__ float4 peer_load4(const float* base, int64_t i4) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, 0x7fffffff, 0x00020000),
+      (int)(i4 * 16), 0, 17);
+  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
+                     __uint_as_float(v.w));
+}
+// the step counter, read once per block (a previous launch wrote it)
+__device__ __forceinline__ uint64_t peer_step(const dq_peer& P) {
+  return __hip_atomic_load(&P.flags[P.rank][kPeerStep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// publish flag `which` of step e: everything this rank stored before this launch is final
+__device__ __forceinline__ void peer_publish(const dq_peer& P, int which) {
+  const uint64_t e = peer_step(P);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  peer_store(&P.flags[P.rank][which], e + 1);
+}
+// the whole block waits until every rank's flag `which` passed step e (lane q of wave 0
+// polls rank q; bounded: a timeout latches the error word and every waiter gives up).
+// Returns false on a timeout or a latched error.
+__device__ __forceinline__ bool peer_wait(const dq_peer& P, int which, uint64_t e, float* smem) {
+  int* ok = reinterpret_cast<int*>(smem);
+  if (threadIdx.x < 64) {
+    const int q = threadIdx.x;
+    uint64_t* err = &P.flags[P.rank][kPeerErr];
+    bool done = q >= P.world;
+    int bad = 0;
+    int64_t polls = 0;
+    while (true) {                      // every exit condition is wave-uniform
+      if (!done) done = peer_load(&P.flags[q][which]) > e;
+      if (__all(done ? 1 : 0)) break;
+      if (++polls > P.max_polls) {
+        if (q == 0) peer_store(err, (uint64_t)(1 + which));
+        bad = 1;
+        break;
+      }
+      if ((polls & 63) == 0) {          // another waiter of this rank gave up: so do we
+        bad = __shfl(q == 0 ? (peer_load(err) != 0 ? 1 : 0) : 0, 0);
+        if (bad) break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (q == 0) *ok = bad ? 0 : 1;
+  }
+  __syncthreads();
+  const bool r = *ok != 0;
+  __syncthreads();
+  return r;
+}
+// the exchange launch's last block (ticket) advances the step counter: every block of the
+// launch has read it by then
+__device__ __forceinline__ void peer_ticket(const dq_peer& P, int total_blocks, uint64_t e) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t* t = &P.flags[P.rank][kPeerTicket];
+    if (atomicAdd((unsigned long long*)t, 1ull) == (unsigned long long)(total_blocks - 1)) {
+      __hip_atomic_store(t, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&P.flags[P.rank][kPeerStep], e + 1, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// one block: publish flag `which` (kPeerGrad / kPeerParam; kPeerConv is PeerConvOp's block 0)
+struct PeerPubOp {
+  static constexpr int kT = 64;
+  static constexpr int kLds = 0;
+  dq_peer P;
+  int which;
+  __device__ __forceinline__ void run(int, float*) const {
+    if (threadIdx.x == 0) peer_publish(P, which);
+  }
+  int blocks() const { return 1; }
+};
+
+// float4 i of the rank-ordered mean over the ranks' gradients, ApplyAdam'd into var / m / v
+// (the loads of kU elements issued before the first update)
+template <int kU>
+__device__ __forceinline__ void peer_mean_adam(const dq_peer& P, float* var, float* m, float* v,
+                                               const int64_t (&idx)[kU], int64_t end4, float alpha,
+                                               float omb1, float omb2, float eps, float inv) {
+  float4 g[kU], p[kU], mm[kU], vv[kU];
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    const int64_t i = min(idx[u], end4 - 1);          // clamped: the loads never branch
+    g[u] = peer_load4(P.grad[0], i);
+#pragma unroll
+    for (int q = 1; q < DQ_PEER_MAX; ++q)
+      if (q < P.world) {
+        const float4 x = peer_load4(P.grad[q], i);
+        g[u].x = __fadd_rn(g[u].x, x.x);
+        g[u].y = __fadd_rn(g[u].y, x.y);
+        g[u].z = __fadd_rn(g[u].z, x.z);
+        g[u].w = __fadd_rn(g[u].w, x.w);
+      }
+    p[u] = reinterpret_cast<float4*>(var)[i];
+    mm[u] = reinterpret_cast<float4*>(m)[i];
+    vv[u] = reinterpret_cast<float4*>(v)[i];
+  }
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    if (idx[u] >= end4) break;
+    const int64_t i = idx[u];
+    const float4 gm = make_float4(__fmul_rn(g[u].x, inv), __fmul_rn(g[u].y, inv),
+                                  __fmul_rn(g[u].z, inv), __fmul_rn(g[u].w, inv));
+    adam1(p[u].x, gm.x, mm[u].x, vv[u].x, alpha, omb1, omb2, eps);
+    adam1(p[u].y, gm.y, mm[u].y, vv[u].y, alpha, omb1, omb2, eps);
+    adam1(p[u].z, gm.z, mm[u].z, vv[u].z, alpha, omb1, omb2, eps);
+    adam1(p[u].w, gm.w, mm[u].w, vv[u].w, alpha, omb1, omb2, eps);
+    reinterpret_cast<float4*>(var)[i] = p[u];
+    reinterpret_cast<float4*>(m)[i] = mm[u];
+    reinterpret_cast<float4*>(v)[i] = vv[u];
+  }
+}
+
+// The ops below hold at most kPeerMaxBlocks blocks each (grid-stride): blocks that wait for
+// other learners hold CU slots, and learners sharing a GPU (the one-GPU tests) must leave
+// the others room to reach the flags being waited for.
+constexpr int kPeerMaxBlocks = 128;
+
+// reduce-scatter + TF1 Adam of floats [b0, b1) of this rank's slice: wait for every rank's
+// fc gradient, their sum in rank order times 1 / world, ApplyAdam (this rank keeps the
+// slice's moments).  grid-stride over float4 pairs, nb blocks.
+struct PeerRsAdamOp {
+  static constexpr int kT = kGroupT;
+  static constexpr int kLds = 1;
+  dq_peer P;
+  AdamDev o;
+  float* var;          // own flat parameters (= P.param[P.rank])
+  float* m;
+  float* v;
+  int64_t b0, b1;      // float offsets in the flat buffers, multiples of 4
+  int nb;
+  __device__ __forceinline__ void run(int blk, float* smem) const {
+    const uint64_t e = peer_step(P);
+    if (!peer_wait(P, kPeerGrad, e, smem)) return;
+    const float alpha = adam_alpha_of(o.state, o.slot, o.lr);
+    const float omb1 = __fsub_rn(1.0f, o.b1), omb2 = __fsub_rn(1.0f, o.b2);
+    const float inv = __fdiv_rn(1.0f, (float)P.world);
+    const int64_t e4 = b1 >> 2, st = (int64_t)nb * kT;
+    for (int64_t i = (b0 >> 2) + (int64_t)blk * kT + threadIdx.x; i < e4; i += 2 * st) {
+      const int64_t idx[2] = {i, i + st};
+      peer_mean_adam<2>(P, var, m, v, idx, e4, alpha, omb1, omb2, o.eps, inv);
+    }
+  }
+  int blocks() const { return nb; }
+};
+
+// the exchange launch: block 0 publishes the conv bucket; blocks [0, nc) wait for every
+// rank's, take the rank-ordered mean of [0, lo) and apply TF1 Adam (replicated; block 0 also
+// advances the beta powers); blocks [nc, nc + na) all-gather: every other rank's updated
+// slice of [lo, n) once its kPeerParam flag passed e.  Every block takes a ticket; the last
+// advances the step counter.
+struct PeerExchOp {
+  static constexpr int kT = kGroupT;
+  static constexpr int kLds = 1;
+  dq_peer P;
+  AdamDev o;
+  float* var;
+  float* m;
+  float* v;
+  int nc, na;
+  __device__ __forceinline__ void run(int blk, float* smem) const {
+    const uint64_t e = peer_step(P);
+    if (blk < nc) {
+      if (blk == 0 && threadIdx.x == 0) peer_publish(P, kPeerConv);
+      if (peer_wait(P, kPeerConv, e, smem)) {
+        const float alpha = adam_alpha_of(o.state, o.slot, o.lr);
+        const float omb1 = __fsub_rn(1.0f, o.b1), omb2 = __fsub_rn(1.0f, o.b2);
+        const float inv = __fdiv_rn(1.0f, (float)P.world);
+        const int64_t e4 = P.lo >> 2, st = (int64_t)nc * kT;
+        for (int64_t i = (int64_t)blk * kT + threadIdx.x; i < e4; i += 2 * st) {
+          const int64_t idx[2] = {i, i + st};
+          peer_mean_adam<2>(P, var, m, v, idx, e4, alpha, omb1, omb2, o.eps, inv);
+        }
+        if (blk == 0 && threadIdx.x == 0) adam_bump(o.state, o.slot, o.b1, o.b2);
+      }
+    } else if (peer_wait(P, kPeerParam, e, smem)) {
+      const int64_t S4 = ((P.n - P.lo) / P.world) >> 2;       // float4 per slice
+      const int64_t tot = S4 * P.world;
+      for (int64_t j = (int64_t)(blk - nc) * kT + threadIdx.x; j < tot; j += (int64_t)na * kT) {
+        const int q = (int)(j / S4);
+        if (q == P.rank) continue;
+        const int64_t i = (P.lo >> 2) + j;
+        reinterpret_cast<float4*>(var)[i] = peer_load4(P.param[q], i);
+      }
+    }
+    peer_ticket(P, nc + na, e);
+  }
+  int blocks() const { return nc + na; }
+};
+
 // TF1 RMSProp (the arithmetic of dq_rmsprop_tf1) over a contiguous range, as AdamOp
 struct RmsOp {
   static constexpr int kT = kGroupT;
@@ -976,6 +1190,77 @@ if constexpr (kHeadFrom == 4) {
   if (in(6)) group_r(c, rd(6), sum_c1);
 }
 
+// The fused Rainbow schedule's backward (backward_grouped<1, 6>, first 1) with the data-
+// parallel exchange over peer memory (dq_peer) in place of the fused optimizer's fc and conv
+// updates -- the gradients are stored, the reduce-scatter + Adam of this rank's slice rides
+// in launches 3 and 4, the parameter publication in launch 5, and one launch more (6) holds
+// the conv bucket's exchange + Adam and the all-gather.  Same tiles and summation orders as
+// backward_grouped: with world 1 the parameters, moments and gradients are bitwise those of
+// the single learner's fused step.
+void backward_peer(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int B, const float* x,
+                   const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d, const dq_adam_args* oa,
+                   const RiderDesc* riders, int n_riders, const FwdOps* head, const dq_peer& P) {
+  const int NO = p->n_out;
+  using W16 = Tile<1, 1, 16>;
+  const int K3 = B * 121, K1 = B * 441;
+  const int ch3 = split_chunk(K3, kSplitConvW, W16::BKT), nz3 = (K3 + ch3 - 1) / ch3;
+  const int ch1 = split_chunk(K1, kSplitConv1W, W16::BKT), nz1 = (K1 + ch1 - 1) / ch1;
+  const size_t o3 = c.take((size_t)nz3 * 64 * (Conv3::K + 1));
+  const size_t o2 = c.take((size_t)nz3 * 64 * (Conv2::K + 1));
+  const size_t o1 = c.take((size_t)nz1 * 32 * (Conv1::K + 1));
+  float* ws = c.ws;
+  if (c.dry) return;
+  auto dX_fc1 = gemm_op<1, 1, 16, kB1Late>(RowK{d->h, kHidden}, ColK{p->fc1_w, kFlat},
+                                           EpiMask{d->a3, a->a3, kFlat}, B, kFlat, kHidden, kHidden);
+  auto dW_fc1 = gemm_op<4, 4, 1>(ColK{d->h, kHidden}, ColKOnes{a->a3, kFlat},
+                                 EpiGrad{g->fc1_w, g->fc1_b, kFlat}, kHidden, kFlat + 1, B, B);
+  auto dW_fc2 = gemm_op<4, 4, 1>(ColKScalar{dout, NO}, ColKOnes{a->h, kHidden},
+                                 EpiGrad{g->fc2_w, g->fc2_b, kHidden}, NO, kHidden + 1, B, B);
+  auto dX_c3 = gemm_op<1, 1, 16>(Col2im<Conv3>{d->a3}, WeightT<Conv3>{p->conv3_w},
+                                 EpiMask{d->a2, a->a2, 64}, K3, 64, Conv3::K, Conv3::K);
+  auto dW_c3 = gemm_op<1, 1, 16>(DyT<64>{d->a3}, Im2colT<Conv3>{a->a2},
+                                 EpiPartial{ws + o3, 64, Conv3::K + 1}, 64, Conv3::K + 1, K3, ch3);
+  auto sp_op = [](auto op) { return PairOp<decltype(op)>{op}; };
+  auto sp00 = sp_op(subpix_op<0, 0>(p, a, d, B));
+  auto sp01 = sp_op(subpix_op<0, 1>(p, a, d, B));
+  auto sp10 = sp_op(subpix_op<1, 0>(p, a, d, B));
+  auto sp11 = sp_op(subpix_op<1, 1>(p, a, d, B));
+  auto sum_c3 = ReduceOp<EpiGrad>{ws + o3, nz3, 64, Conv3::K + 1,
+                                  EpiGrad{g->conv3_w, g->conv3_b, Conv3::K}};
+  auto dW_c2 = gemm_op<1, 1, 16>(DyT<64>{d->a2}, Im2colT<Conv2>{a->a1},
+                                 EpiPartial{ws + o2, 64, Conv2::K + 1}, 64, Conv2::K + 1, K3, ch3);
+  auto sum_c2 = ReduceOp<EpiGrad>{ws + o2, nz3, 64, Conv2::K + 1,
+                                  EpiGrad{g->conv2_w, g->conv2_b, Conv2::K}};
+  auto dW_c1 = gemm_op<1, 1, 16>(DyT<32>{d->a1}, Im2colT<Conv1>{x},
+                                 EpiPartial{ws + o1, 32, Conv1::K + 1}, 32, Conv1::K + 1, K1, ch1);
+  auto sum_c1 = ReduceOp<EpiGrad>{ws + o1, nz1, 32, Conv1::K + 1,
+                                  EpiGrad{g->conv1_w, g->conv1_b, Conv1::K}};
+  const AdamDev od{oa->state, oa->slot, oa->lr, oa->beta1, oa->beta2, oa->epsilon, 1};
+  // this rank's slice of [lo, n), halves in launches 3 and 4; one float4 per thread
+  const int64_t S = (P.n - P.lo) / P.world;
+  const int64_t s0 = P.lo + (int64_t)P.rank * S, sm = s0 + ((S / 2) & ~(int64_t)3), s1 = s0 + S;
+  auto blocks_for = [](int64_t floats, int per_thread) {
+    return (int)std::min<int64_t>(kPeerMaxBlocks,
+                                  std::max<int64_t>(1, (floats / 4 + per_thread * kGroupT - 1) /
+                                                           (per_thread * kGroupT)));
+  };
+  auto rs = [&](int64_t b0, int64_t b1) {
+    return PeerRsAdamOp{P, od, oa->var, oa->m, oa->v, b0, b1, blocks_for(b1 - b0, 2)};
+  };
+  const int nc = blocks_for(P.lo, 2);
+  const int na = P.world > 1 ? blocks_for((P.n - P.lo) * (P.world - 1) / P.world, 4) : 0;
+  auto rd = [&](int i) { return i >= 1 && i - 1 < n_riders ? riders + (i - 1) : nullptr; };
+  group_r(c, rd(1), dX_fc1);
+  group_r(c, rd(2), dW_fc1, dX_c3, dW_fc2);
+  group_r(c, rd(3), PeerPubOp{P, kPeerGrad}, dW_c3, sp00, sp01, sp10, sp11, dW_c2, rs(s0, sm));
+  group_r(c, rd(4), sum_c3, dW_c1, rs(sm, s1));
+  if (head)
+    group_r(c, rd(5), PeerPubOp{P, kPeerParam}, sum_c2, sum_c1, head->conv1());
+  else
+    group_r(c, rd(5), PeerPubOp{P, kPeerParam}, sum_c2, sum_c1);
+  group(c, PeerExchOp{P, od, oa->var, oa->m, oa->v, nc, na});
+}
+
 // backward_grouped with the runtime head_from (7: the whole target head runs in the next
 // forward, so the five-launch schedule carries none of it)
 template <int kOpt>
@@ -1198,6 +1483,50 @@ int dq_cnn_backward_riders(const dq_cnn_params* p, const dq_cnn_params* g, int32
                           n_riders, hp, head_from);
   }
   DQ_CHECK_LAUNCH("dq_cnn_backward_riders");
+  return DQ_OK;
+}
+
+int dq_cnn_backward_peer(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch,
+                         const float* x, const dq_cnn_acts* a, const float* dout,
+                         dq_cnn_acts* d, float* ws, const dq_rider* riders, int32_t n_riders,
+                         const dq_adam_args* opt, const dq_cnn_net* head, const dq_peer* peer,
+                         void* stream) {
+  DQ_CHECK_ARG(p && g && a && d && x && dout && ws && opt && peer && batch >= 1, "null argument");
+  DQ_CHECK_ARG(p->in_channels == 4 && p->n_out >= 1, "the Nature CNN takes 84x84x4 NHWC input");
+  DQ_CHECK_ARG(opt->kind == DQ_OPT_ADAM, "the peer exchange applies TF1 Adam");
+  DQ_CHECK_ARG(0 <= n_riders && n_riders <= 5 && (riders || n_riders == 0),
+               "at most one rider per grouped launch 1..5");
+  const int rc = check_adam(p, g, opt);
+  if (rc != DQ_OK) return rc;
+  const dq_peer& P = *peer;
+  DQ_CHECK_ARG(P.world >= 1 && P.world <= DQ_PEER_MAX && P.rank >= 0 && P.rank < P.world,
+               "peer: 1 <= world <= DQ_PEER_MAX, 0 <= rank < world");
+  DQ_CHECK_ARG(P.lo >= 0 && P.lo % 4 == 0 && P.n > P.lo && (P.n - P.lo) % (4 * P.world) == 0,
+               "peer: lo % 4 == 0 and (n - lo) % (4 world) == 0");
+  DQ_CHECK_ARG(P.n >= (int64_t)(p->fc2_b + p->n_out - opt->var),
+               "peer: [lo, n) must reach the end of the flat parameter buffer");
+  DQ_CHECK_ARG(P.lo >= (int64_t)(p->fc1_w - opt->var),
+               "peer: the sharded range lies in the fc bucket (its gradient final after launch 2)");
+  DQ_CHECK_ARG(P.param[P.rank] == opt->var && P.grad[P.rank] == g->conv1_w - (p->conv1_w - opt->var),
+               "peer: this rank's buffers must be opt->var and the gradient of its layout");
+  for (int q = 0; q < P.world; ++q)
+    DQ_CHECK_ARG(P.grad[q] && P.param[q] && P.flags[q], "peer: null rank buffer");
+  DQ_CHECK_ARG(P.max_polls > 0, "peer: max_polls must be positive");
+  RiderDesc r[5];
+  for (int i = 0; i < n_riders; ++i) {
+    memcpy(&r[i], &riders[i], sizeof(RiderDesc));
+    DQ_CHECK_ARG(r[i].kind >= kRiderNone && r[i].kind <= kRiderSetSample, "corrupt rider");
+  }
+  FwdOps hf{};
+  if (head) {
+    DQ_CHECK_ARG(head->p && head->x && head->a && head->ws, "null head network field");
+    DQ_CHECK_ARG(head->p->in_channels == 4, "the Nature CNN takes 84x84x4 NHWC input");
+    DQ_CHECK_ARG(head->ws != ws, "the head network needs its own workspace");
+    hf = FwdOps{head->p, head->x, head->a, head->ws, batch};
+  }
+  Ctx c{(hipStream_t)stream, ws, false, 0};
+  backward_peer(c, p, g, batch, x, a, dout, d, opt, r, n_riders, head ? &hf : nullptr, P);
+  DQ_CHECK_LAUNCH("dq_cnn_backward_peer");
   return DQ_OK;
 }
 

@@ -197,6 +197,8 @@ __global__ __launch_bounds__(256) void k_gather_nhwc4(ReplayView v, GatherOut g)
 #ifdef DQ_GATHER_PROF
   unsigned long long gp[4] = {__builtin_amdgcn_s_memrealtime(), 0, 0, 0};
   unsigned long long* gpp = gp;
+  const unsigned gp_wid = (blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6);
+  const unsigned gp_seq = gp_wid < (unsigned)kGpWaves ? g_gp_seq[gp_wid] : 0u;   // issued first
 #else
   unsigned long long* gpp = nullptr;
 #endif
@@ -210,58 +212,30 @@ __global__ __launch_bounds__(256) void k_gather_nhwc4(ReplayView v, GatherOut g)
   }
 #ifdef DQ_GATHER_PROF
   GP_STAMP(gp, 3);
-  if ((threadIdx.x & 63) == 0) {
-    const unsigned launch = *(volatile unsigned*)&g_gp_count;
-    const unsigned waves = gridDim.x * gridDim.y * (blockDim.x / 64);
-    const unsigned wid = (blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6);
-    const bool frame = blockIdx.x != gridDim.x - 1;
-    if (launch < (unsigned)kGpLaunches) {
-      unsigned long long* L = g_gp_launch[launch];
-      atomicMin(&L[0], gp[0]);
-      atomicMax(&L[1], gp[0]);
-      if (frame && gp[1]) {
-        atomicMax(&L[2], gp[1]);
-        atomicMin(&L[3], gp[2]);
-        atomicMax(&L[4], gp[2]);
-      }
-      atomicMax(&L[5], gp[3]);
-      if (!frame) atomicMax(&L[6], gp[3]);      // the scalar column's end
-    }
-    if (launch == *(volatile unsigned*)&g_gp_target && wid < (unsigned)kGpWaves) {
-      g_gp_wave[wid][0] = gp[0];
-      g_gp_wave[wid][1] = gp[1];
-      g_gp_wave[wid][2] = gp[2];
-      g_gp_wave[wid][3] = gp[3];
-    }
-    __threadfence();
-    if (atomicAdd(&g_gp_done, 1u) == waves - 1) {   // the launch's last wave
-      g_gp_done = 0;
-      __threadfence();
-      atomicAdd(&g_gp_count, 1u);
-    }
+  if ((threadIdx.x & 63) == 0 && gp_wid < (unsigned)kGpWaves) {
+    unsigned long long* d = g_gp_wave[gp_seq % kGpRing][gp_wid];
+    d[0] = gp[0];
+    d[1] = gp[1];
+    d[2] = gp[2];
+    d[3] = gp[3];
+    g_gp_seq[gp_wid] = gp_seq + 1;
   }
 #endif
 }
 
 #ifdef DQ_GATHER_PROF
-// reset (launch counter 0, per-launch mins at +inf, maxes at 0; per-wave stamps of launch
-// `target`) and read back: tools/gather_stamps.py
-extern "C" int dq_debug_gather_reset(int32_t target) {
-  static unsigned long long init[kGpLaunches][8];
-  for (int i = 0; i < kGpLaunches; ++i)
-    for (int k = 0; k < 8; ++k) init[i][k] = (k == 0 || k == 3) ? ~0ull : 0ull;
-  const unsigned zero = 0, t = (unsigned)target;
-  if (hipMemcpyToSymbol(HIP_SYMBOL(g_gp_launch), init, sizeof(init)) != hipSuccess) return -1;
-  if (hipMemcpyToSymbol(HIP_SYMBOL(g_gp_count), &zero, 4) != hipSuccess) return -1;
-  if (hipMemcpyToSymbol(HIP_SYMBOL(g_gp_done), &zero, 4) != hipSuccess) return -1;
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_gp_target), &t, 4) == hipSuccess ? 0 : -1;
+// tools/gather_stamps.py: zero the ring and the per-wave counters; read them back
+extern "C" int dq_debug_gather_reset(int32_t) {
+  static unsigned long long zw[kGpRing][kGpWaves][4];
+  static unsigned zs[kGpWaves];
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_gp_wave), zw, sizeof(zw)) != hipSuccess) return -1;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_gp_seq), zs, sizeof(zs)) == hipSuccess ? 0 : -1;
 }
-extern "C" int dq_debug_gather_read(unsigned long long* launches, unsigned long long* waves,
-                                    unsigned int* count) {
-  if (hipMemcpyFromSymbol(launches, HIP_SYMBOL(g_gp_launch), sizeof(g_gp_launch)) != hipSuccess)
-    return -1;
-  if (hipMemcpyFromSymbol(waves, HIP_SYMBOL(g_gp_wave), sizeof(g_gp_wave)) != hipSuccess) return -1;
-  return hipMemcpyFromSymbol(count, HIP_SYMBOL(g_gp_count), 4) == hipSuccess ? 0 : -1;
+extern "C" int dq_debug_gather_read(unsigned long long* ring, unsigned* seq, unsigned* dims) {
+  dims[0] = kGpRing;
+  dims[1] = kGpWaves;
+  if (hipMemcpyFromSymbol(ring, HIP_SYMBOL(g_gp_wave), sizeof(g_gp_wave)) != hipSuccess) return -1;
+  return hipMemcpyFromSymbol(seq, HIP_SYMBOL(g_gp_seq), sizeof(g_gp_seq)) == hipSuccess ? 0 : -1;
 }
 #endif
 

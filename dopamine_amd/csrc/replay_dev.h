@@ -511,15 +511,12 @@ enum { kScalEarly = 0, kScalLate = 1, kScalNone = 2 };
 // Stamp build of the standalone gather (tools/gather_stamps.py; never the product: the
 // waits below serialise what the product overlaps only where a stamp is taken).  Each wave
 // takes s_memrealtime (100 MHz) at its start, once its index is in, once its frames are in,
-// and once its stores are acknowledged; per launch (a counter the launch's last wave
-// advances) the first / last of each go to g_gp_launch, every wave's of one launch to
-// g_gp_wave.  Stamp words only ever go to these buffers.
-constexpr int kGpLaunches = 1024, kGpWaves = 4096;
-__device__ unsigned long long g_gp_launch[kGpLaunches][8];
-__device__ unsigned long long g_gp_wave[kGpWaves][4];
-__device__ unsigned int g_gp_count;
-__device__ unsigned int g_gp_done;
-__device__ unsigned int g_gp_target;
+// and once its stores are acknowledged, and writes the four to its own slot of a ring of
+// kGpRing launches (the slot from a counter only that wave position reads and advances: no
+// atomics, no shared words).  Stamp words only ever go to these buffers.
+constexpr int kGpRing = 64, kGpWaves = 2048;
+__device__ unsigned long long g_gp_wave[kGpRing][kGpWaves][4];
+__device__ unsigned int g_gp_seq[kGpWaves];
 #define GP_STAMP(gp, k)                                      \
   do {                                                       \
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");         \

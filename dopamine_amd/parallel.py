@@ -182,6 +182,92 @@ def agree_min(value, group):
   return int(t.item())
 
 
+class PeerExchange(object):
+  """The data-parallel exchange over peer memory (include/dopamine_amd.h dq_peer; DESIGN.md
+  6): every learner maps every other learner's flat gradient, parameter and flag buffers
+  (IPC handles exchanged over ``group``, a host-side collective), and the backward's grouped
+  launches run the reduce-scatter + slice Adam, the conv bucket's mean + Adam and the all-
+  gather as extra blocks on the learner's ONE stream (cnn.HipNatureCNN.backward_peer).
+
+  ``[lo, n)``: the sharded range of the flat buffers (the fc bucket, minus a head of < 4N
+  floats that joins the conv bucket); every rank keeps the Adam moments of its own slice
+  only (ZeRO-1: DQNAgent._gather_opt_state gathers them for a checkpoint).  group None: one
+  learner running the same protocol with itself (world 1).  Requires every learner on one
+  node with peer access between their devices (``available``)."""
+
+  MAX_POLLS = 4_000_000      # per wait (~1-2 us per poll): a dead peer latches an error in seconds
+
+  def __init__(self, group, device, grad, params, lo, n, max_polls=None):
+    from dopamine_amd import _lib
+    self._lib = _lib
+    self.group = group
+    self.world = 1 if group is None else dist.get_world_size(group)
+    self.rank = 0 if group is None else dist.get_rank(group)
+    assert self.world <= _lib.PEER_MAX, 'the peer exchange holds at most %d ranks' % _lib.PEER_MAX
+    assert lo % 4 == 0 and (n - lo) % (4 * self.world) == 0
+    self.lo, self.n = int(lo), int(n)
+    self.flags = torch.zeros(_lib.PEER_FLAG_WORDS, dtype=torch.int64, device=device)
+    self._opened = []
+    bufs = (grad, params, self.flags)
+    ptrs = [[0] * 3 for _ in range(self.world)]
+    ptrs[self.rank] = [b.data_ptr() for b in bufs]
+    if self.world > 1:
+      mine = []
+      for b in bufs:
+        h = _lib.IpcHandle()
+        _lib.call('dq_peer_ipc_get', ctypes.c_void_p(b.data_ptr()), ctypes.byref(h))
+        mine.append(bytes(ctypes.string_at(ctypes.addressof(h), ctypes.sizeof(h))))
+      allh = [None] * self.world
+      dist.all_gather_object(allh, mine, group=group)
+      torch.cuda.synchronize(device)
+      for q in range(self.world):
+        if q == self.rank:
+          continue
+        for k in range(3):
+          h = _lib.IpcHandle.from_buffer_copy(allh[q][k])
+          ptr, base = ctypes.c_void_p(), ctypes.c_void_p()
+          _lib.call('dq_peer_ipc_open', ctypes.byref(h), ctypes.byref(ptr), ctypes.byref(base))
+          self._opened.append(base.value)
+          ptrs[q][k] = ptr.value
+    d = _lib.Peer(world=self.world, rank=self.rank, lo=self.lo, n=self.n,
+                  max_polls=int(max_polls or self.MAX_POLLS))
+    for q in range(self.world):
+      d.grad[q], d.param[q], d.flags[q] = ptrs[q]
+    self.desc = d
+
+  @staticmethod
+  def available(group, device):
+    """Whether every learner of ``group`` can run the exchange: one host, peer access
+    between every pair of their devices.  Collective; every rank gets the same answer."""
+    import socket
+    from dopamine_amd import _lib
+    me = (socket.gethostname(), torch.device(device).index)
+    allm = [None] * dist.get_world_size(group)
+    dist.all_gather_object(allm, me, group=group)
+    ok = all(h == me[0] for h, _ in allm) and dist.get_world_size(group) <= _lib.PEER_MAX
+    ok = ok and all(int(_lib.lib.dq_peer_can_access(me[1], dv)) == 1 for _, dv in allm)
+    flags = [None] * dist.get_world_size(group)
+    dist.all_gather_object(flags, bool(ok), group=group)
+    return all(flags)
+
+  def error(self):
+    """0, or 1 + the flag a wait of this learner timed out on (a synchronising read)."""
+    return int(self.flags[self._lib.PEER_ERR].item())
+
+  def check(self):
+    e = self.error()
+    if e:
+      names = {1 + self._lib.PEER_GRAD: 'gradients', 1 + self._lib.PEER_PARAM: 'parameters',
+               1 + self._lib.PEER_CONV: 'conv gradients'}
+      raise RuntimeError('peer exchange: rank %d timed out waiting for the other learners\' %s '
+                         '(a learner stopped or fell out of step)' % (self.rank, names.get(e, e)))
+
+  def close(self):
+    for base in self._opened:
+      self._lib.call('dq_peer_ipc_close', ctypes.c_void_p(base))
+    self._opened = []
+
+
 # exit status of a process whose deadline expired (Deadline)
 DEADLINE_EXIT = 3
 

@@ -639,13 +639,14 @@ class OutOfGraphReplayBuffer(object):
     return out
 
   # ------------------------------------------------------- device fast path
-  def reserve_rng(self, batch_size=None):
-    """Host-side tape bookkeeping for one upcoming device sample (call outside
-    graph capture; may synchronise and refill the tape)."""
+  def reserve_rng(self, batch_size=None, steps=1):
+    """Host-side tape bookkeeping for ``steps`` upcoming device samples of ``batch_size``
+    (call outside graph capture; may synchronise and refill the tape): the same budget as
+    ``steps`` calls of one, in one call (a learner-loop chunk's reservation)."""
     B = self._batch_size if batch_size is None else batch_size
     if not self._prioritized:
       self._precheck()
-    return self._rng.reserve(self._words_worst_case(B), self._stream)
+    return self._rng.reserve(steps * self._words_worst_case(B), self._stream)
 
   def sample_device(self, batch_size=None, layout=_lib.LAYOUT_F32_NORM, out=None, indices=None,
                     reserve=True, groups=1):

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define DQ_ABI_VERSION 7
+#define DQ_ABI_VERSION 8
 
 /* host-side return codes */
 #define DQ_OK 0
@@ -583,6 +583,55 @@ int dq_comm_reduce_scatter_mean(dq_comm* c, float* buf, int64_t n_per_rank, void
 int dq_comm_all_gather(dq_comm* c, float* buf, int64_t n_per_rank, void* stream);
 /* RCCL's version code, or -1 if it cannot be opened */
 int dq_comm_version(void);
+
+/* ---------------- the same exchange over peer memory, on ONE queue --------------------
+ * ("one-queue exchange").  Learners on one node map each other's flat
+ * gradient, parameter and flag buffers (IPC handles, exchanged by the host) and the exchange
+ * runs as extra blocks ("riders") of the backward's grouped launches plus one short launch:
+ *   launch 3: publish "my fc-bucket gradient of step e is final" (flags[1] = e + 1); the
+ *             reduce-scatter + TF1 Adam of this rank's slice of [lo, n): wait until every
+ *             rank's flags[1] > e, sum the slice over the ranks IN RANK ORDER, times 1 / N
+ *             (the gloo reference's order, parallel.allreduce_mean_), ApplyAdam on the slice;
+ *   launch 4: the second half of that slice;
+ *   launch 5: publish "my slice's parameters of step e are updated" (flags[2] = e + 1);
+ *   launch 6: publish the conv bucket [0, lo) (flags[3]), wait for every rank's, its rank-
+ *             ordered mean and ApplyAdam (replicated; this one advances the beta powers);
+ *             all-gather: every other rank's slice of the parameters once its flags[2] > e;
+ *             the step counter flags[0] += 1 by the launch's last block.
+ * No collective library, no second queue, no graph fork or join.  Remote loads are
+ * system-coherent (sc0 sc1), the flags system-scope stores behind a system release; every
+ * wait is bounded (max_polls) and a timeout latches flags[4] (dq_peer_flags_words words
+ * per rank, zero-initialised; flags[0] = the step counter, equal on every rank). */
+#define DQ_PEER_MAX 8
+#define DQ_PEER_FLAG_WORDS 8
+typedef struct dq_ipc_handle {
+  uint8_t handle[64];             /* hipIpcMemHandle_t of the allocation holding the pointer */
+  int64_t offset;                 /* the pointer's byte offset in that allocation */
+} dq_ipc_handle;
+int dq_peer_ipc_get(const void* ptr, dq_ipc_handle* out);
+/* maps another process's allocation: *ptr_out = its base + offset; close with the base */
+int dq_peer_ipc_open(const dq_ipc_handle* h, void** ptr_out, void** base_out);
+int dq_peer_ipc_close(void* base);
+/* hipDeviceCanAccessPeer: 1 if `device` can map `peer`'s memory (always 1 for itself) */
+int dq_peer_can_access(int32_t device, int32_t peer);
+typedef struct dq_peer {
+  int32_t world, rank;
+  int64_t lo, n;                  /* the sharded range [lo, n) of the flat buffers (floats);
+                                     (n - lo) % (4 world) == 0, lo % 4 == 0 */
+  float* grad[DQ_PEER_MAX];       /* rank q's flat gradient, mapped here ([rank]: own) */
+  float* param[DQ_PEER_MAX];      /* rank q's flat parameters */
+  uint64_t* flags[DQ_PEER_MAX];   /* rank q's DQ_PEER_FLAG_WORDS flag words */
+  int64_t max_polls;              /* per wait; then flags[4] := 1 + which flag timed out */
+} dq_peer;
+/* dq_cnn_backward_riders of the fused Rainbow schedule (head_from 6, first 1, last 7, TF1
+   Adam) with the exchange above in place of the fused optimizer's fc / conv updates: the
+   gradients are stored (keep them in g), launches 1-5 as there plus the exchange riders,
+   then launch 6.  world = 1 runs the same protocol with itself. */
+int dq_cnn_backward_peer(const dq_cnn_params* p, const dq_cnn_params* g, int32_t batch,
+                         const float* x, const dq_cnn_acts* a, const float* dout,
+                         dq_cnn_acts* d, float* ws, const dq_rider* riders, int32_t n_riders,
+                         const dq_adam_args* opt, const dq_cnn_net* head, const dq_peer* peer,
+                         void* stream);
 
 #ifdef __cplusplus
 }

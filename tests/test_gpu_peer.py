@@ -1,0 +1,138 @@
+"""The data-parallel exchange over peer memory on ONE stream (exchange='peer',
+parallel.PeerExchange, dq_cnn_backward_peer), on one GPU:
+
+* world 1 (a one-rank group, the protocol run with itself): parameters, Adam moments and beta
+  powers bitwise those of the single learner's fused schedule, per call and in the learner
+  loop's captured chunks;
+* two ranks sharing cuda:0 (two processes, each mapping the other's buffers through IPC
+  handles), different buffers and network seeds: parameters and (gathered) moments bitwise
+  those of one process applying TF1 Adam to the rank-ordered mean of the two gradients
+  (test_gpu_multirank._mean_gradient_reference);
+* a rank that never trains: the other's bounded waits time out, latch the error word and the
+  learner raises -- no hang."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from tests.test_gpu_multirank import STEPS, _agent, _free_port, _mean_gradient_reference, _run
+
+pytestmark = pytest.mark.gpu
+
+
+def _peer_worker(rank, world, port, q, loop, same_seed=False, idle_rank=-1, max_polls=None):
+  import sys
+  sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+  import torch.distributed as dist
+  os.environ['MASTER_ADDR'] = '127.0.0.1'
+  os.environ['MASTER_PORT'] = str(port)
+  torch.cuda.set_device(0)
+  dist.init_process_group('gloo', rank=rank, world_size=world)
+  from dopamine_amd import parallel
+  if max_polls is not None:
+    parallel.PeerExchange.MAX_POLLS = max_polls
+  agent = _agent(dist.group.WORLD, 0 if same_seed else rank,
+                 net_seed=0 if same_seed else 1000 * rank, exchange='peer')
+  assert agent._peer is not None and agent._sharded() and not agent._collective()
+  if rank == idle_rank:
+    q.put((rank, 'idle'))
+    dist.barrier()
+    dist.destroy_process_group()
+    return
+  try:
+    flat = _run(agent, loop)
+    err = None
+    agent.mean_loss()
+  except RuntimeError as e:
+    q.put((rank, 'error', str(e)))
+    if idle_rank >= 0:
+      dist.barrier()
+      dist.destroy_process_group()
+      return
+    raise
+  assert agent._graph_sets.get(True) is not None    # the later steps replayed captured graphs
+  assert not loop or any(isinstance(k, tuple) and k[0] == 'chunk' for k in agent._graph_sets)
+  ok = parallel.replicas_in_sync(agent.online_convnet.fp.flat)
+  ok = ok and parallel.replicas_in_sync(agent.target_convnet.fp.flat)
+  agent._gather_opt_state()         # every slice's moments, as a checkpoint sees them
+  ok = ok and parallel.replicas_in_sync(agent._opt.m) and parallel.replicas_in_sync(agent._opt.v)
+  st = agent._opt.state.cpu().numpy()
+  if rank == 0:
+    q.put((rank, ok, flat.numpy(), agent._opt.m.cpu().numpy(), agent._opt.v.cpu().numpy(), st,
+           int(agent._peer.flags[0].item()), err))
+  agent.close()
+  dist.barrier()
+  dist.destroy_process_group()
+
+
+def _spawn(world, loop, **kw):
+  ctx = mp.get_context('spawn')
+  q = ctx.Queue()
+  port = _free_port()
+  procs = [ctx.Process(target=_peer_worker, args=(r, world, port, q, loop), kwargs=kw)
+           for r in range(world)]
+  for p in procs:
+    p.start()
+  res = []
+  import queue
+  import time
+  try:
+    want = world if kw.get('idle_rank', -1) >= 0 else 1
+    t0 = time.time()
+    while len(res) < want and time.time() - t0 < 400:
+      try:
+        res.append(q.get(timeout=5))
+      except queue.Empty:          # a worker that died (its traceback is on stderr) ends the wait
+        assert not any(p.exitcode not in (None, 0) for p in procs), [p.exitcode for p in procs]
+    assert len(res) == want, 'workers did not report'
+  finally:
+    for p in procs:
+      p.join(timeout=120)
+      if p.exitcode is None:
+        p.kill()
+  return res, [p.exitcode for p in procs]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize('loop', [False, True])
+def test_peer_world1_equals_single_learner_bitwise(loop):
+  """World 1: the exchange's reduce-scatter, slice Adam, conv bucket and (empty) all-gather
+  run against the learner itself -- bitwise the single learner (parameters, moments, beta
+  powers), and the step counter counts the gradient steps."""
+  res, codes = _spawn(1, loop)
+  _, ok, flat, m, v, st, steps, _ = res[0]
+  assert codes == [0] and ok
+  single = _agent(None, 0)
+  sflat = _run(single, loop).numpy()
+  assert np.array_equal(flat, sflat)
+  assert np.array_equal(m, single._opt.m.cpu().numpy())
+  assert np.array_equal(v, single._opt.v.cpu().numpy())
+  assert np.array_equal(st, single._opt.state.cpu().numpy())
+  assert steps == single._opt_steps == STEPS
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize('loop', [False, True])
+def test_peer_two_ranks_equal_mean_gradient_reference(loop):
+  """Two processes on cuda:0, different buffers and network seeds (rank 0's broadcast at
+  construction): parameters and gathered moments bitwise the rank-ordered mean-gradient
+  TF1 Adam reference; the replicas stay bit-identical."""
+  res, codes = _spawn(2, loop)
+  _, ok, flat, m, v, st, steps, _ = res[0]
+  assert codes == [0, 0] and ok and steps == STEPS
+  ref, rm, rv = _mean_gradient_reference(loop, moments=True)
+  assert np.array_equal(flat, ref)
+  assert np.array_equal(m, rm) and np.array_equal(v, rv)
+
+
+@pytest.mark.timeout(600)
+def test_peer_wait_times_out_instead_of_hanging():
+  """Rank 1 builds its learner (the handles are exchanged) but never trains: rank 0's waits
+  for its gradients give up after max_polls, latch the error word, and mean_loss raises."""
+  res, codes = _spawn(2, False, idle_rank=1, max_polls=20000)
+  by_rank = {r[0]: r for r in res}
+  assert by_rank[1][1] == 'idle'
+  assert by_rank[0][1] == 'error' and 'timed out' in by_rank[0][2], by_rank[0]
+  assert codes == [0, 0]

@@ -22,12 +22,13 @@ _Orig = torch.cuda.CUDAGraph
 
 
 class _DbgGraph(_Orig):
-  made = []
+  """Every graph kept after instantiation (keep_graph), so HIP can print it."""
 
-  def __init__(self, *a, **k):
-    super().__init__(*a, **k)
-    self.enable_debug_mode()
-    _DbgGraph.made.append(self)
+  def __new__(cls, keep_graph=False):
+    return super().__new__(cls, True)
+
+  def __init__(self, keep_graph=False):
+    super().__init__(True)
 
 
 def parse_dot(path):

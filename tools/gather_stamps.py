@@ -4,9 +4,10 @@ build:
     DQ_DIAGNOSTIC_BUILD=1 DOPAMINE_AMD_LIB=ab/gprof/libdopamine_amd.so python tools/gather_stamps.py
 The launches are the bench's (bench.time_gather): ITERS back-to-back graph launches, each on
 a fresh random index batch of a 1M-transition buffer.  Every wave stamps s_memrealtime
-(100 MHz) at its start, with its index in, with its four frames in, and with its stores
-acknowledged; per launch the first / last of each are kept.  Times in us from the launch's
-first wave start; 'boundary' = this launch's first wave start - the previous one's last store."""
+(100 MHz, 10 ns) at its start, with its index in, with its four frames in and with its
+stores acknowledged, into its own slot of a ring of the last 64 launches.  Per launch, times
+in us from its first wave start; 'boundary' = a launch's first wave start - the previous
+launch's last store acknowledgement."""
 import ctypes
 import os
 import sys
@@ -17,6 +18,11 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 ITERS = int(os.environ.get('GP_ITERS', '400'))
+
+
+def pct(v):
+  return '%7.2f %7.2f %7.2f %7.2f' % (np.percentile(v, 10), np.median(v), np.percentile(v, 90),
+                                      v.max())
 
 
 def main():
@@ -32,52 +38,48 @@ def main():
   L = _lib.lib
   L.dq_debug_gather_reset.argtypes = [ctypes.c_int32]
   L.dq_debug_gather_read.argtypes = [ctypes.c_void_p] * 3
-  nl, nw = 1024, 4096
-  target = ITERS // 2
-  # warm-up / event timing exactly as the bench line's (the stamps add their waits)
+  assert L.dq_debug_gather_reset(0) == 0
   us, algo, name = bench.time_gather(agent, ITERS)
-  assert L.dq_debug_gather_reset(target) == 0
-  us2, _, _ = bench.time_gather(agent, ITERS)
   torch.cuda.synchronize()
-  launches = np.zeros((nl, 8), np.uint64)
-  waves = np.zeros((nw, 4), np.uint64)
-  count = np.zeros(1, np.uint32)
-  assert L.dq_debug_gather_read(launches.ctypes.data, waves.ctypes.data, count.ctypes.data) == 0
-  n = int(count[0])
-  print('stamp build %r; launches stamped %d; event-timed avg launch %.3f us (%.3f with the '
-        'stamps reset between, same build)' % (_lib.BUILD_FLAGS, n, us, us2))
-  # time_gather runs 10 eager launches, then the graph replayed twice: the last ITERS
-  # launches are the timed replay
-  Lr = launches[:min(n, nl)].astype(np.float64)
-  tl = Lr[-ITERS:] if n >= ITERS else Lr
-  t0 = tl[:, 0]
-  rel = (tl - t0[:, None]) / 100.0
-  cols = [('last wave start (dispatch ramp)', 1), ('last index in', 2), ('first frames in', 3),
-          ('last frames in', 4), ('last store acked (launch end)', 5), ('scalar column end', 6)]
-  print('%-34s %8s %8s %8s' % ('per launch, us from first wave start', 'p10', 'median', 'p90'))
-  for lab, k in cols:
-    v = rel[:, k]
-    print('%-34s %8.2f %8.2f %8.2f' % (lab, np.percentile(v, 10), np.median(v), np.percentile(v, 90)))
-  b = (tl[1:, 0] - tl[:-1, 5]) / 100.0
-  print('%-34s %8.2f %8.2f %8.2f' % ('boundary (prev end -> this start)', np.percentile(b, 10),
-                                     np.median(b), np.percentile(b, 90)))
-  per = (tl[1:, 0] - tl[:-1, 0]) / 100.0
-  print('%-34s %8.2f %8.2f %8.2f' % ('start-to-start period', np.percentile(per, 10),
-                                     np.median(per), np.percentile(per, 90)))
-  # the target launch (launch index `target` of the run: in the first replay)
-  w = waves.astype(np.float64)
-  live = w[:, 0] > 0
-  w = w[live]
-  s0 = w[:, 0].min()
-  fr = w[:, 1] > 0
-  print('target launch %d: %d waves (%d frame waves)' % (target, len(w), int(fr.sum())))
-  for lab, v in (('wave start', (w[:, 0] - s0) / 100.0),
-                 ('index latency (start -> index in)', (w[fr, 1] - w[fr, 0]) / 100.0),
-                 ('frame latency (index in -> frames in)', (w[fr, 2] - w[fr, 1]) / 100.0),
-                 ('store phase (frames in -> stores acked)', (w[fr, 3] - w[fr, 2]) / 100.0),
-                 ('wave end', (w[:, 3] - s0) / 100.0)):
-    print('  %-42s p10 %6.2f  median %6.2f  p90 %6.2f  max %6.2f' % (
-        lab, np.percentile(v, 10), np.median(v), np.percentile(v, 90), v.max()))
+  dims = np.zeros(2, np.uint32)
+  ring = np.zeros((64, 2048, 4), np.uint64)
+  seq = np.zeros(2048, np.uint32)
+  assert L.dq_debug_gather_read(ring.ctypes.data, seq.ctypes.data, dims.ctypes.data) == 0
+  R, W = int(dims[0]), int(dims[1])
+  n = int(seq.max())
+  assert (seq == n).all(), 'waves saw different launch counts'
+  print('stamp build %r; %s; launches %d; event-timed avg launch %.3f us (stamp build)' % (
+      _lib.BUILD_FLAGS, name, n, us))
+  order = [(l % R) for l in range(n - R, n)]          # the last R launches, in order
+  st = ring[order].astype(np.float64) / 100.0          # (R, W, 4) us
+  frame = st[:, :, 1] > 0                              # the frame waves (not the scalar column)
+  t0 = st[:, :, 0].min(axis=1)
+  rows = []
+  for i in range(R):
+    f = frame[i]
+    s = st[i]
+    rows.append([s[:, 0].max() - t0[i], s[f, 1].max() - t0[i], s[f, 2].min() - t0[i],
+                 s[f, 2].max() - t0[i], s[:, 3].max() - t0[i], s[~f, 3].max() - t0[i],
+                 np.median(s[f, 1] - s[f, 0]), np.median(s[f, 2] - s[f, 1]),
+                 np.median(s[f, 3] - s[f, 2])])
+  rows = np.array(rows)
+  labs = ['last wave start (dispatch ramp)', 'last index in', 'first frames in', 'last frames in',
+          'last store acked (launch end)', 'scalar column end', 'wave: index latency (median)',
+          'wave: frame latency (median)', 'wave: store phase (median)']
+  print('%-36s %7s %7s %7s %7s' % ('per launch (us from first wave start)', 'p10', 'median', 'p90',
+                                   'max'))
+  for k, lab in enumerate(labs):
+    print('%-36s %s' % (lab, pct(rows[:, k])))
+  end = t0 + rows[:, 4]
+  b = t0[1:] - end[:-1]
+  print('%-36s %s' % ('boundary (prev end -> this start)', pct(b)))
+  print('%-36s %s' % ('start-to-start period', pct(np.diff(t0))))
+  # one launch in detail: waves by start time
+  i = R // 2
+  s, f = st[i], frame[i]
+  for lab, v in (('wave start', s[:, 0] - t0[i]), ('index in', s[f, 1] - t0[i]),
+                 ('frames in', s[f, 2] - t0[i]), ('stores acked', s[:, 3] - t0[i])):
+    print('  launch %d %-14s %s' % (i, lab, pct(v)))
 
 
 if __name__ == '__main__':
