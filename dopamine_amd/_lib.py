@@ -277,6 +277,17 @@ def call(name, *args):
   check(getattr(lib, name)(*args), name)
 
 
+def stream_of(device):
+  """The current HIP stream of ``device`` (a torch.device or index) as a void* for the C ABI:
+  torch's raw getter, without building a torch.cuda.Stream object per call (the learner loop
+  calls this on its host path several times per step)."""
+  import torch
+  idx = device if isinstance(device, int) else device.index
+  if idx is None:
+    idx = torch.cuda.current_device()
+  return ctypes.c_void_p(torch._C._cuda_getCurrentRawStream(idx))
+
+
 def ptr(t):
   """Raw device pointer of a torch tensor (or None)."""
   return None if t is None else ctypes.c_void_p(t.data_ptr())

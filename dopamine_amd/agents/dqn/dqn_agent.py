@@ -1396,12 +1396,17 @@ class DQNAgent(object):
 
   _loss_name = 'HuberLoss'
 
+  def check_exchange(self):
+    """Raises if a wait of the peer exchange timed out (the latched error word: another
+    learner stopped or fell out of step); a synchronising read.  No-op otherwise."""
+    if self._peer is not None:
+      self._peer.check()
+
   def mean_loss(self):
     """Mean loss of the last gradient step (the summary scalar, dqn:318-321); the fused
     head's loss kernel leaves the mean to this call (it is not on the gradient path).
-    With the peer exchange it also raises if a wait of it timed out (a latched error)."""
-    if self._peer is not None:
-      self._peer.check()
+    With the peer exchange it also raises if a wait of it timed out (check_exchange)."""
+    self.check_exchange()
     if self._fused():
       return float(self._loss_out['loss'].double().mean().item())
     return float(self._loss_out['mean_loss'].item())

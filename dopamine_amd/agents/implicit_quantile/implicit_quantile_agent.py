@@ -80,6 +80,7 @@ class ImplicitQuantileAgent(rainbow_agent.RainbowAgent):
 
   def mean_loss(self):
     """mean over the batch of the quantile loss (the QuantileLoss summary, iqn:316-319)."""
+    self.check_exchange()
     return float(self._loss_out['loss'].double().mean().item())
 
   def _needs_flat_grad(self):

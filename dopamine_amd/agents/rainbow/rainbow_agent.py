@@ -131,6 +131,7 @@ class RainbowAgent(dqn_agent.DQNAgent):
 
   def mean_loss(self):
     """mean(w * CE) of the last step (the CrossEntropyLoss summary, rb:298-301)."""
+    self.check_exchange()
     loss = self._loss_out['loss']
     if self._replay_scheme == 'prioritized':
       w = 1.0 / torch.sqrt(self._replay.transition['sampling_probabilities'] + 1e-10)

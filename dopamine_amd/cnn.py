@@ -61,7 +61,7 @@ class HipNatureCNN(object):
 
   @staticmethod
   def _stream(t):
-    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+    return _lib.stream_of(t.device)
 
   def _nhwc(self, x):
     if x.dim() == 4 and x.shape[1] == self.in_ch and x.shape[-1] != self.in_ch:

@@ -405,11 +405,42 @@ struct PeerRsAdamOp {
   int blocks() const { return nb; }
 };
 
-// the exchange launch: block 0 publishes the conv bucket; blocks [0, nc) wait for every
-// rank's, take the rank-ordered mean of [0, lo) and apply TF1 Adam (replicated; block 0 also
-// advances the beta powers); blocks [nc, nc + na) all-gather: every other rank's updated
-// slice of [lo, n) once its kPeerParam flag passed e.  Every block takes a ticket; the last
-// advances the step counter.
+// all-gather: every other rank's updated slice of [lo, n) once its kPeerParam flag passed e
+// (rides in the launch that publishes this rank's: launch 5)
+struct PeerAgOp {
+  static constexpr int kT = kGroupT;
+  static constexpr int kLds = 1;
+  dq_peer P;
+  float* var;
+  int nb;
+  __device__ __forceinline__ void run(int blk, float* smem) const {
+    const uint64_t e = peer_step(P);
+    if (!peer_wait(P, kPeerParam, e, smem)) return;
+    const int64_t S4 = ((P.n - P.lo) / P.world) >> 2;       // float4 per slice
+    const int64_t tot = S4 * (P.world - 1), st = (int64_t)nb * kT;
+    for (int64_t j0 = (int64_t)blk * kT + threadIdx.x; j0 < tot; j0 += 4 * st) {
+      float4 x[4];
+      int64_t at[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {                // loads of 4 elements in flight
+        const int64_t j = min(j0 + u * st, tot - 1);
+        int q = (int)(j / S4);
+        q += q >= P.rank ? 1 : 0;                    // every rank but this one
+        at[u] = (P.lo >> 2) + (int64_t)q * S4 + (j - (int64_t)(j / S4) * S4);
+        x[u] = peer_load4(P.param[q], at[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (j0 + u * st < tot) reinterpret_cast<float4*>(var)[at[u]] = x[u];
+    }
+  }
+  int blocks() const { return nb; }
+};
+
+// the exchange launch (6): block 0 publishes the conv bucket; every block waits for every
+// rank's, takes the rank-ordered mean of [0, lo) and applies TF1 Adam (replicated; block 0
+// also advances the beta powers).  Every block takes a ticket; the last advances the step
+// counter.
 struct PeerExchOp {
   static constexpr int kT = kGroupT;
   static constexpr int kLds = 1;
@@ -418,35 +449,24 @@ struct PeerExchOp {
   float* var;
   float* m;
   float* v;
-  int nc, na;
+  int nc;
   __device__ __forceinline__ void run(int blk, float* smem) const {
     const uint64_t e = peer_step(P);
-    if (blk < nc) {
-      if (blk == 0 && threadIdx.x == 0) peer_publish(P, kPeerConv);
-      if (peer_wait(P, kPeerConv, e, smem)) {
-        const float alpha = adam_alpha_of(o.state, o.slot, o.lr);
-        const float omb1 = __fsub_rn(1.0f, o.b1), omb2 = __fsub_rn(1.0f, o.b2);
-        const float inv = __fdiv_rn(1.0f, (float)P.world);
-        const int64_t e4 = P.lo >> 2, st = (int64_t)nc * kT;
-        for (int64_t i = (int64_t)blk * kT + threadIdx.x; i < e4; i += 2 * st) {
-          const int64_t idx[2] = {i, i + st};
-          peer_mean_adam<2>(P, var, m, v, idx, e4, alpha, omb1, omb2, o.eps, inv);
-        }
-        if (blk == 0 && threadIdx.x == 0) adam_bump(o.state, o.slot, o.b1, o.b2);
+    if (blk == 0 && threadIdx.x == 0) peer_publish(P, kPeerConv);
+    if (peer_wait(P, kPeerConv, e, smem)) {
+      const float alpha = adam_alpha_of(o.state, o.slot, o.lr);
+      const float omb1 = __fsub_rn(1.0f, o.b1), omb2 = __fsub_rn(1.0f, o.b2);
+      const float inv = __fdiv_rn(1.0f, (float)P.world);
+      const int64_t e4 = P.lo >> 2, st = (int64_t)nc * kT;
+      for (int64_t i = (int64_t)blk * kT + threadIdx.x; i < e4; i += 2 * st) {
+        const int64_t idx[2] = {i, i + st};
+        peer_mean_adam<2>(P, var, m, v, idx, e4, alpha, omb1, omb2, o.eps, inv);
       }
-    } else if (peer_wait(P, kPeerParam, e, smem)) {
-      const int64_t S4 = ((P.n - P.lo) / P.world) >> 2;       // float4 per slice
-      const int64_t tot = S4 * P.world;
-      for (int64_t j = (int64_t)(blk - nc) * kT + threadIdx.x; j < tot; j += (int64_t)na * kT) {
-        const int q = (int)(j / S4);
-        if (q == P.rank) continue;
-        const int64_t i = (P.lo >> 2) + j;
-        reinterpret_cast<float4*>(var)[i] = peer_load4(P.param[q], i);
-      }
+      if (blk == 0 && threadIdx.x == 0) adam_bump(o.state, o.slot, o.b1, o.b2);
     }
-    peer_ticket(P, nc + na, e);
+    peer_ticket(P, nc, e);
   }
-  int blocks() const { return nc + na; }
+  int blocks() const { return nc; }
 };
 
 // TF1 RMSProp (the arithmetic of dq_rmsprop_tf1) over a contiguous range, as AdamOp
@@ -1248,17 +1268,25 @@ void backward_peer(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int B
     return PeerRsAdamOp{P, od, oa->var, oa->m, oa->v, b0, b1, blocks_for(b1 - b0, 2)};
   };
   const int nc = blocks_for(P.lo, 2);
-  const int na = P.world > 1 ? blocks_for((P.n - P.lo) * (P.world - 1) / P.world, 4) : 0;
+  const int na = blocks_for((P.n - P.lo) * (P.world - 1) / P.world, 4);
   auto rd = [&](int i) { return i >= 1 && i - 1 < n_riders ? riders + (i - 1) : nullptr; };
   group_r(c, rd(1), dX_fc1);
   group_r(c, rd(2), dW_fc1, dX_c3, dW_fc2);
   group_r(c, rd(3), PeerPubOp{P, kPeerGrad}, dW_c3, sp00, sp01, sp10, sp11, dW_c2, rs(s0, sm));
   group_r(c, rd(4), sum_c3, dW_c1, rs(sm, s1));
-  if (head)
+  // launch 5: this rank's slice published, the others' gathered (world 1: nothing to gather)
+  const PeerAgOp ag{P, oa->var, na};
+  if (P.world > 1) {
+    if (head)
+      group_r(c, rd(5), PeerPubOp{P, kPeerParam}, sum_c2, sum_c1, head->conv1(), ag);
+    else
+      group_r(c, rd(5), PeerPubOp{P, kPeerParam}, sum_c2, sum_c1, ag);
+  } else if (head) {
     group_r(c, rd(5), PeerPubOp{P, kPeerParam}, sum_c2, sum_c1, head->conv1());
-  else
+  } else {
     group_r(c, rd(5), PeerPubOp{P, kPeerParam}, sum_c2, sum_c1);
-  group(c, PeerExchOp{P, od, oa->var, oa->m, oa->v, nc, na});
+  }
+  group(c, PeerExchOp{P, od, oa->var, oa->m, oa->v, nc});
 }
 
 // backward_grouped with the runtime head_from (7: the whole target head runs in the next

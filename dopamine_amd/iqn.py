@@ -24,7 +24,7 @@ def _head_struct(fp, buf, num_actions, embed_dim):
 
 
 def _stream(device):
-  return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+  return _lib.stream_of(device)
 
 
 class TauSampler(object):

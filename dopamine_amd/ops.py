@@ -13,7 +13,7 @@ p = _lib.ptr
 
 
 def _stream(t):
-  return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+  return _lib.stream_of(t.device)
 
 
 def _c(t, dtype):

@@ -113,7 +113,7 @@ MAX_RECORDED = _MaxRecorded(float('nan'))
 
 
 def _stream_handle(device):
-  return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+  return _lib.stream_of(device)
 
 
 class OutOfGraphReplayBuffer(object):

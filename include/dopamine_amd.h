@@ -594,9 +594,9 @@ int dq_comm_version(void);
  *             (the gloo reference's order, parallel.allreduce_mean_), ApplyAdam on the slice;
  *   launch 4: the second half of that slice;
  *   launch 5: publish "my slice's parameters of step e are updated" (flags[2] = e + 1);
+ *             all-gather: every other rank's slice of the parameters once its flags[2] > e;
  *   launch 6: publish the conv bucket [0, lo) (flags[3]), wait for every rank's, its rank-
  *             ordered mean and ApplyAdam (replicated; this one advances the beta powers);
- *             all-gather: every other rank's slice of the parameters once its flags[2] > e;
  *             the step counter flags[0] += 1 by the launch's last block.
  * No collective library, no second queue, no graph fork or join.  Remote loads are
  * system-coherent (sc0 sc1), the flags system-scope stores behind a system release; every

@@ -111,20 +111,29 @@ def test_tau_sampler_is_uniform_and_replays_in_graphs():
     np.testing.assert_array_equal(e, r)
 
 
+@pytest.mark.parametrize('kind', ['adam', 'rmsprop_centered', 'rmsprop'])
 @pytest.mark.parametrize('store', [True, False])
-def test_fused_optimizer_torso_backward_equals_backward_then_adam(store):
-  """dq_cnn_backward_torso_opt (the IQN learner's TF1 Adam inside the torso's grouped
+def test_fused_optimizer_torso_backward_equals_backward_then_adam(store, kind):
+  """dq_cnn_backward_torso_opt (the IQN learner's optimizer inside the torso's grouped
   backward launches: the head as float4 riders, conv3 after its sum, conv2 / conv1 in their
-  split-K sums' epilogues) == head + torso backward followed by dq_adam_tf1 over the whole
-  flat buffer, bitwise, over two steps (both beta-power slots); store False: the fused
-  epilogues skip the gradient stores, the parameters and moments unchanged."""
+  split-K sums' epilogues) == head + torso backward followed by the separate optimizer
+  launch (dq_adam_tf1, or dq_rmsprop_tf1 centered and not: the RmsOp riders and GradEpi<2>
+  epilogues) over the whole flat buffer, bitwise, over two steps (both beta-power slots);
+  store False: the fused epilogues skip the gradient stores, the parameters and optimizer
+  state unchanged."""
   from dopamine_amd import ops
   from dopamine_amd.agents.networks import ImplicitQuantileNetwork
   from dopamine_amd.iqn import HipIqnNet
   B, nq, A = 16, 8, 4
   nets = [ImplicitQuantileNetwork(A, device='cuda', seed=7) for _ in range(2)]
   exs = [HipIqnNet(n, B, nq, keep=True) for n in nets]
-  opts = [ops.TF1Adam(n.fp.flat, learning_rate=5e-5, epsilon=3.125e-4) for n in nets]
+  if kind == 'adam':
+    opts = [ops.TF1Adam(n.fp.flat, learning_rate=5e-5, epsilon=3.125e-4) for n in nets]
+    names = ('params', 'm', 'v', 'state')
+  else:
+    opts = [ops.TF1RMSProp(n.fp.flat, learning_rate=2.5e-4, decay=0.95, momentum=0.0,
+                           epsilon=1e-5, centered=kind == 'rmsprop_centered') for n in nets]
+    names = ('params', 'ms', 'mom') + (('mg',) if kind == 'rmsprop_centered' else ())
   rs = np.random.RandomState(1)
   for step in range(2):
     x = torch.from_numpy(rs.rand(B, 84, 84, 4).astype(np.float32)).cuda()
@@ -136,7 +145,43 @@ def test_fused_optimizer_torso_backward_equals_backward_then_adam(store):
     exs[1].backward(dq)
     opts[1].step(nets[1].fp.grad, slot=step % 2)
     torch.cuda.synchronize()
-    for n in ('params', 'm', 'v', 'state'):
+    for n in names:
       assert torch.equal(getattr(opts[0], n), getattr(opts[1], n)), (step, n)
     if store:
       assert torch.equal(nets[0].fp.grad, nets[1].fp.grad)
+
+
+@pytest.mark.parametrize('kind', ['adam', 'rmsprop'])
+def test_iqn_agent_fused_optimizer_equals_separate_step_bitwise(kind):
+  """The IQN agent with fuse_optimizer on (the optimizer inside the torso's backward, the
+  pipelined two-stream schedule, graph capture, keep_gradients off as the bench drives it)
+  and off (the separate optimizer launch after the step): parameters and optimizer state
+  bitwise equal after graph-captured steps."""
+  from dopamine_amd.agents.implicit_quantile.implicit_quantile_agent import ImplicitQuantileAgent
+  from dopamine_amd.agents.optimizers import AdamOptimizer, RMSPropOptimizer
+  import bench
+  import random
+
+  def make(fused):
+    opt = (AdamOptimizer(learning_rate=5e-5, epsilon=3.125e-4) if kind == 'adam' else
+           RMSPropOptimizer(learning_rate=2.5e-4, decay=0.95, momentum=0.0, epsilon=1e-5,
+                            centered=True))
+    ag = ImplicitQuantileAgent(num_actions=4, num_tau_samples=16, num_tau_prime_samples=16,
+                               num_quantile_samples=8, update_horizon=3, min_replay_history=100,
+                               update_period=4, target_update_period=40, optimizer=opt,
+                               replay_capacity=20000, batch_size=16, device=torch.device('cuda', 0),
+                               seed=3, fuse_optimizer=fused)
+    ag.keep_gradients = False
+    random.seed(5)
+    bench.fill_synthetic(ag._replay.memory, 4, seed=9)
+    return ag
+  agents = [make(True), make(False)]
+  assert agents[0]._fused_opt() and not agents[1]._fused_opt()
+  for ag in agents:
+    ag.train_gradient_steps(10)
+  torch.cuda.synchronize()
+  assert agents[0]._graph_sets and agents[1]._graph_sets    # captured steps were replayed
+  a, b = agents[0]._opt, agents[1]._opt
+  names = ('params', 'm', 'v', 'state') if kind == 'adam' else ('params', 'ms', 'mom', 'mg')
+  for n in names:
+    assert torch.equal(getattr(a, n), getattr(b, n)), n
