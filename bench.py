@@ -509,7 +509,25 @@ def main(argv=None):
       elapsed = max(per_rank)
       deadline.done()
     agent._replay.memory.sync_rng()   # raises if the device latched a sampling error
-    loss = agent.mean_loss()
+    try:
+      loss, err = agent.mean_loss(), None     # raises if a peer-exchange wait timed out
+    except RuntimeError as e:
+      loss, err = float('nan'), str(e)
+    if pg is not None and len(names) > 1:
+      # every rank drops a schedule that failed on any rank (each rank's bounded waits end
+      # its window, so all ranks reach this point) and the next one is timed
+      deadline.phase('agreeing on the %s schedule\'s errors' % name, DEADLINE_S)
+      f = torch.tensor([0 if err is None else 1], dtype=torch.int32,
+                       device='cpu' if rehearse else dev)
+      dist.all_reduce(f, op=dist.ReduceOp.MAX)
+      deadline.done()
+      if int(f.item()):
+        schedules[name] = {'error': err or 'failed on another rank'}
+        print('bench: rank %d: schedule %s failed: %s' % (rank, name, schedules[name]['error']),
+              file=sys.stderr)
+        continue
+    if err is not None:
+      raise RuntimeError(err)
     assert np.isfinite(loss), 'non-finite loss'
     schedules[name] = {
         'value': round(world * args.steps / elapsed, 2), 'ms_per_step': round(1e3 * elapsed / args.steps, 4),
@@ -518,11 +536,14 @@ def main(argv=None):
         'comm': ('peer memory (one stream)' if agent._peer is not None else
                  args.comm if agent._rccl is not None or args.comm == 'torch' else 'torch')
         if pg is not None else None}
-  best = min(schedules, key=lambda k: schedules[k]['_elapsed'])
+  timed = [k for k in schedules if '_elapsed' in schedules[k]]
+  if not timed:
+    raise RuntimeError('every data-parallel schedule failed: %r' % schedules)
+  best = min(timed, key=lambda k: schedules[k]['_elapsed'])
   elapsed, prime, loss = (schedules[best]['_elapsed'], schedules[best]['prime_steps'],
                           schedules[best]['final_mean_loss'])
   for v in schedules.values():
-    del v['_elapsed']
+    v.pop('_elapsed', None)
 
   graph_us, algo_bytes, gname = time_gather(agent, args.gather_iters)
   large = time_gather_large(agent)

@@ -229,7 +229,11 @@ SIGNATURES = {
     'dq_cnn_backward_peer': [ctypes.POINTER(CnnParams), ctypes.POINTER(CnnParams), _I32, _P,
                              ctypes.POINTER(CnnActs), _P, ctypes.POINTER(CnnActs), _P,
                              ctypes.POINTER(Rider), _I32, ctypes.POINTER(AdamArgs),
-                             ctypes.POINTER(CnnNet), ctypes.POINTER(Peer), _P],
+                             ctypes.POINTER(CnnNet), ctypes.POINTER(Peer), _I32, _P],
+    'dq_cnn_forward_fused_peer': [ctypes.POINTER(CnnParams), _P, ctypes.POINTER(CnnActs), _P,
+                                  ctypes.POINTER(CnnParams), _P, ctypes.POINTER(CnnActs), _P,
+                                  _I32, _I32, ctypes.POINTER(Peer), _P, _P],
+    'dq_peer_all_gather': [ctypes.POINTER(Peer), _P, _P],
 }
 RESTYPES = {'dq_last_error': ctypes.c_char_p, 'dq_build_flags': ctypes.c_char_p, 'dq_cnn_workspace_floats': ctypes.c_size_t,
             'dq_iqn_workspace_floats': ctypes.c_size_t,

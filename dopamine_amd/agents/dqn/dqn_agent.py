@@ -484,7 +484,8 @@ class DQNAgent(object):
         return
       cnn.forward_fused(self._hip['online'], self._pbuf[c]['state'], self._hip['target'][c],
                         conv3_b=hf >= 5, conv2_b=hf >= 6, part=part,
-                        xb=self._pbuf[c]['next_state'] if hf == 7 else None)
+                        xb=self._pbuf[c]['next_state'] if hf == 7 else None,
+                        **self._peer_fwd_gather())
       return
     assert part is None
     on, tg = cnn.forward_with_tail(self._hip['online'], self._pbuf[c]['state'], self._hip['target'][c])
@@ -536,6 +537,20 @@ class DQNAgent(object):
 
   def _forward_fused_c51(self, c, part=None):
     raise NotImplementedError
+
+  # The peer exchange's all-gather inside the learner loop's chunk graphs: every step but the
+  # last publishes its updated slice without gathering the others' (backward launch 5 loses
+  # its gather blocks), the next step's three conv forward launches gather them (they read no
+  # fc parameter; fc1's launch follows) and the chunk ends with dq_peer_all_gather.  Per-call
+  # steps keep the gather in launch 5.  Bitwise the same parameters either way.
+  _peer_defer_ag = False     # the backward being recorded defers its gather
+  _peer_fwd_ag = False       # the forward being recorded gathers the previous step's
+
+  def _peer_fwd_gather(self):
+    """forward_fused* keyword arguments of the deferred gather ({} when none rides)."""
+    if not self._peer_fwd_ag:
+      return {}
+    return {'peer': self._peer.desc, 'var': self._opt.params}
 
   def _bwd_head_from(self):
     """head_from for the backward: 8 places the target's conv1 as 6 does."""
@@ -616,7 +631,7 @@ class DQNAgent(object):
       riders = self._place_riders(riders)
       if self._peer is not None:      # the exchange inside the backward's launches (one stream)
         self._hip['online'].backward_peer(g, self._opt, k, self._peer.desc, riders=riders,
-                                          head=self._head)
+                                          head=self._head, defer_ag=self._peer_defer_ag)
         self._head = None
         return
       adam = self._opt if self._fused_opt() else None
@@ -1344,12 +1359,20 @@ class DQNAgent(object):
       torch.cuda.synchronize(self._device)
       g = torch.cuda.CUDAGraph()
       if not self._collective():
-        with torch.cuda.graph(g, pool=self._graph_pool):
-          for j in range(K):
-            k = (k0 + j) % 2
-            self._grad_step(k, k, True)
-            self._device_opt_step(k)
-            self._trace_step(j, k)
+        defer = self._peer is not None and self._peer.world > 1 and self._fused()
+        try:
+          with torch.cuda.graph(g, pool=self._graph_pool):
+            for j in range(K):
+              k = (k0 + j) % 2
+              self._peer_fwd_ag, self._peer_defer_ag = defer and j > 0, defer
+              self._grad_step(k, k, True)
+              self._device_opt_step(k)
+              self._trace_step(j, k)
+            if defer:                 # every parameter current when the chunk returns
+              self._peer.all_gather(self._opt.params,
+                                    _lib.stream_of(self._device))
+        finally:
+          self._peer_fwd_ag = self._peer_defer_ag = False
       else:
         # N > 1: each step's split schedule with its RCCL all-reduces captured (the comm
         # stream and RCCL's own streams fork from and join back into the capture; each

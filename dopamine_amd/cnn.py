@@ -112,12 +112,14 @@ class HipNatureCNN(object):
                          state=adam.state.data_ptr(), slot=int(slot), lr=adam.lr,
                          beta1=adam.b1, beta2=adam.b2, epsilon=adam.eps, no_grad_store=ngs)
 
-  def backward_peer(self, dout, adam, slot, peer, riders=None, head=None):
+  def backward_peer(self, dout, adam, slot, peer, riders=None, head=None, defer_ag=False):
     """The fused Rainbow schedule's backward (head_from 6, from launch 1) with the data-
     parallel exchange over peer memory (dq_cnn_backward_peer; ``peer``: a _lib.Peer) in
     place of the fused optimizer's updates: the gradients are stored, this rank's slice of
-    the fc bucket is reduce-scattered and updated inside launches 3-4, the conv bucket and
-    the all-gather in launch 6.  Rider i rides in launch 1 + i."""
+    the fc bucket is reduce-scattered and updated inside launches 3-4, published with the
+    others' slices gathered in launch 5 (defer_ag: gathered by the next step's
+    ``forward_fused*(..., peer=)`` or ``PeerExchange.all_gather`` instead), the conv bucket
+    in launch 6.  Rider i rides in launch 1 + i."""
     dout = dout.reshape(self.B, self.n_out)
     assert dout.is_contiguous() and self._x is not None
     args = self._adam_args(adam, slot)
@@ -131,7 +133,8 @@ class HipNatureCNN(object):
     _lib.check(_lib.lib.dq_cnn_backward_peer(
         ctypes.byref(self._p), ctypes.byref(self._g), self.B, self._x.data_ptr(),
         ctypes.byref(self._a), dout.data_ptr(), ctypes.byref(self._d), self.ws.data_ptr(),
-        arr, len(riders), ctypes.byref(args), hn, ctypes.byref(peer), self._stream(dout)),
+        arr, len(riders), ctypes.byref(args), hn, ctypes.byref(peer), int(bool(defer_ag)),
+        self._stream(dout)),
         'dq_cnn_backward_peer')
     return self.net.fp.grad
 
@@ -263,7 +266,8 @@ def fc2_parts(net):
   return net.ws[off:off + n].view(16, net.B, net.n_out)
 
 
-def forward_fused(a, xa, b, fc1_b=True, conv3_b=False, part=None, conv2_b=False, xb=None):
+def forward_fused(a, xa, b, fc1_b=True, conv3_b=False, part=None, conv2_b=False, xb=None,
+                  peer=None, var=None):
   """The Rainbow fast path's forward (dq_cnn_forward_fused): ``a`` (online) on
   ``xa`` through fc1, ``b`` (target; conv1..conv3 already run, e.g. riding in the
   previous backward with head_from=4) from its fc1 slabs (if ``fc1_b``; with
@@ -273,11 +277,21 @@ def forward_fused(a, xa, b, fc1_b=True, conv3_b=False, part=None, conv2_b=False,
   (bitwise the logits of ``forward``).  part='convs' / 'fcs': only the three conv
   launches / only the fc launches (the same launches in two calls).  conv2_b / xb:
   ``b``'s conv2 beside ``a``'s conv2 (head_from=6) / ``b``'s conv1 on ``xb`` beside
-  ``a``'s conv1 (head_from=7: no target head in the backward).  Returns the two
-  partial views."""
+  ``a``'s conv1 (head_from=7: no target head in the backward).  peer / var (head_from 6, the
+  whole forward): the data-parallel exchange's deferred all-gather (the previous step's
+  ``backward_peer(..., defer_ag=True)``) into ``a``'s flat parameters ``var`` rides in the
+  three conv launches (dq_cnn_forward_fused_peer).  Returns the two partial views."""
   assert a.B == b.B and a is not b
   xa = a._nhwc(xa)
   a._x = xa
+  if peer is not None:
+    assert conv2_b and part is None and xb is None
+    _lib.check(_lib.lib.dq_cnn_forward_fused_peer(
+        ctypes.byref(a._p), xa.data_ptr(), ctypes.byref(a._a), a.ws.data_ptr(),
+        ctypes.byref(b._p), None, ctypes.byref(b._a), b.ws.data_ptr(), a.B,
+        int(bool(fc1_b)) | 2 * int(bool(conv3_b)) | 16, ctypes.byref(peer), var.data_ptr(),
+        a._stream(xa)), 'dq_cnn_forward_fused_peer')
+    return fc2_parts(a), fc2_parts(b)
   _lib.check(_lib.lib.dq_cnn_forward_fused(
       ctypes.byref(a._p), xa.data_ptr(), ctypes.byref(a._a), a.ws.data_ptr(),
       ctypes.byref(b._p), None if xb is None else b._nhwc(xb).data_ptr(), ctypes.byref(b._a),

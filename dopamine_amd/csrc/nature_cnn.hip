@@ -405,20 +405,25 @@ struct PeerRsAdamOp {
   int blocks() const { return nb; }
 };
 
-// all-gather: every other rank's updated slice of [lo, n) once its kPeerParam flag passed e
-// (rides in the launch that publishes this rank's: launch 5)
+// all-gather: every other rank's updated slice of [lo, n) once its kPeerParam flag shows the
+// step, float4s [f0, f1) of the (world - 1) slices in rank order.  lag 0: in the step that
+// updated them (launch 5, publishing this rank's; the step counter is still e); lag 1: after
+// that step's exchange launch advanced the counter -- the next step's conv forward launches
+// (the learner loop's deferred gather) or a launch of its own (dq_peer_all_gather).
 struct PeerAgOp {
   static constexpr int kT = kGroupT;
   static constexpr int kLds = 1;
   dq_peer P;
   float* var;
-  int nb;
+  int nb, lag;
+  int64_t f0, f1;
   __device__ __forceinline__ void run(int blk, float* smem) const {
     const uint64_t e = peer_step(P);
-    if (!peer_wait(P, kPeerParam, e, smem)) return;
+    if (e < (uint64_t)lag) return;                 // before the first step: nothing updated
+    if (!peer_wait(P, kPeerParam, e - lag, smem)) return;
     const int64_t S4 = ((P.n - P.lo) / P.world) >> 2;       // float4 per slice
-    const int64_t tot = S4 * (P.world - 1), st = (int64_t)nb * kT;
-    for (int64_t j0 = (int64_t)blk * kT + threadIdx.x; j0 < tot; j0 += 4 * st) {
+    const int64_t tot = min(f1, S4 * (P.world - 1)), st = (int64_t)nb * kT;
+    for (int64_t j0 = f0 + (int64_t)blk * kT + threadIdx.x; j0 < tot; j0 += 4 * st) {
       float4 x[4];
       int64_t at[4];
 #pragma unroll
@@ -783,15 +788,49 @@ struct FwdOps {
 // partials, net 1 (target, head run earlier: conv1..conv3 into a1) finishing with
 // its fc1 slabs (if fc1_1) in net 0's fc1 launch and its fused head beside net 0's:
 // 5 launches.  The logits are summed by dq_c51_loss_fused.
+// The peer exchange's deferred all-gather: the first kAgLaunch5 / 16 of the (world - 1)
+// slices' float4s in the step's own launch 5 (lag 0, beside the publish), the rest in thirds
+// in the next forward's three conv launches (lag 1: they read no fc parameter; fc1's launch
+// follows) -- launch 5 (~8 us) and the conv launches (~27 us) share the pull about in
+// proportion to their length (tools/peer_n8_model.py).  The learner loop's last step leaves
+// the rest to dq_peer_all_gather.
+constexpr int kAgLaunch5 = 4;
+struct AgParts {
+  const dq_peer* P;
+  float* var;
+  int64_t total() const { return ((P->n - P->lo) / P->world / 4) * (P->world - 1); }
+  int64_t split() const { return total() * kAgLaunch5 / 16; }
+  PeerAgOp op(int64_t a, int64_t b, int lag) const {
+    const int nb = (int)std::min<int64_t>(kPeerMaxBlocks,
+                                          std::max<int64_t>(1, (b - a + 4 * kGroupT - 1) / (4 * kGroupT)));
+    return PeerAgOp{*P, var, nb, lag, a, b};
+  }
+  PeerAgOp head() const { return op(0, split(), 0); }
+  PeerAgOp part(int i) const {
+    const int64_t s = split(), t = total();
+    return op(s + (t - s) * i / 3, s + (t - s) * (i + 1) / 3, 1);
+  }
+};
+
 void forward_fused(Ctx& c0, Ctx& c1, const FwdOps& f0, const FwdOps& f1, bool fc1_1,
                    bool conv3_1 = false, bool convs = true, bool fcs = true,
-                   bool conv2_1 = false, bool conv1_1 = false) {
+                   bool conv2_1 = false, bool conv1_1 = false, const AgParts* ag = nullptr) {
   const size_t n0 = FwdOps::fused_ws_floats(f0.B, f0.p->n_out);
   const size_t n1 = FwdOps::fused_ws_floats(f1.B, f1.p->n_out);
   c0.need = n0 > c0.need ? n0 : c0.need;
   c1.need = n1 > c1.need ? n1 : c1.need;
   if (c0.dry) return;
-  if (convs) {
+  if (convs && ag) {           // head_from 6 (the Rainbow fast path) with the deferred gather
+    group(c0, f0.conv1<false>(), ag->part(0));
+    if (conv2_1)
+      group(c0, f0.conv2<true>(), f1.conv2(), ag->part(1));
+    else
+      group(c0, f0.conv2<false>(), ag->part(1));
+    if (conv3_1)
+      group(c0, f0.conv3<false>(), f1.conv3(), ag->part(2));
+    else
+      group(c0, f0.conv3<false>(), ag->part(2));
+  } else if (convs) {
     // single-round launches fetch early; the conv2 launch with the target's conv2 late
     // (+0.9%); net 1's conv3 (head_from = 5) rides in net 0's conv3 launch (+1.1% over the
     // conv1 launch, +2.2% over the conv2 launch)
@@ -1219,7 +1258,8 @@ if constexpr (kHeadFrom == 4) {
 // the single learner's fused step.
 void backward_peer(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int B, const float* x,
                    const dq_cnn_acts* a, const float* dout, dq_cnn_acts* d, const dq_adam_args* oa,
-                   const RiderDesc* riders, int n_riders, const FwdOps* head, const dq_peer& P) {
+                   const RiderDesc* riders, int n_riders, const FwdOps* head, const dq_peer& P,
+                   bool defer_ag) {
   const int NO = p->n_out;
   using W16 = Tile<1, 1, 16>;
   const int K3 = B * 121, K1 = B * 441;
@@ -1274,8 +1314,10 @@ void backward_peer(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int B
   group_r(c, rd(2), dW_fc1, dX_c3, dW_fc2);
   group_r(c, rd(3), PeerPubOp{P, kPeerGrad}, dW_c3, sp00, sp01, sp10, sp11, dW_c2, rs(s0, sm));
   group_r(c, rd(4), sum_c3, dW_c1, rs(sm, s1));
-  // launch 5: this rank's slice published, the others' gathered (world 1: nothing to gather)
-  const PeerAgOp ag{P, oa->var, na};
+  // launch 5: this rank's slice published, the others' gathered (world 1: nothing to gather;
+  // defer_ag: the head of the range (AgParts), the rest by the next forward's conv launches)
+  const PeerAgOp ag = defer_ag ? AgParts{&P, oa->var}.head()
+                               : PeerAgOp{P, oa->var, na, 0, 0, INT64_MAX};
   if (P.world > 1) {
     if (head)
       group_r(c, rd(5), PeerPubOp{P, kPeerParam}, sum_c2, sum_c1, head->conv1(), ag);
@@ -1518,7 +1560,7 @@ int dq_cnn_backward_peer(const dq_cnn_params* p, const dq_cnn_params* g, int32_t
                          const float* x, const dq_cnn_acts* a, const float* dout,
                          dq_cnn_acts* d, float* ws, const dq_rider* riders, int32_t n_riders,
                          const dq_adam_args* opt, const dq_cnn_net* head, const dq_peer* peer,
-                         void* stream) {
+                         int32_t defer_ag, void* stream) {
   DQ_CHECK_ARG(p && g && a && d && x && dout && ws && opt && peer && batch >= 1, "null argument");
   DQ_CHECK_ARG(p->in_channels == 4 && p->n_out >= 1, "the Nature CNN takes 84x84x4 NHWC input");
   DQ_CHECK_ARG(opt->kind == DQ_OPT_ADAM, "the peer exchange applies TF1 Adam");
@@ -1553,8 +1595,56 @@ int dq_cnn_backward_peer(const dq_cnn_params* p, const dq_cnn_params* g, int32_t
     hf = FwdOps{head->p, head->x, head->a, head->ws, batch};
   }
   Ctx c{(hipStream_t)stream, ws, false, 0};
-  backward_peer(c, p, g, batch, x, a, dout, d, opt, r, n_riders, head ? &hf : nullptr, P);
+  backward_peer(c, p, g, batch, x, a, dout, d, opt, r, n_riders, head ? &hf : nullptr, P,
+                defer_ag != 0);
   DQ_CHECK_LAUNCH("dq_cnn_backward_peer");
+  return DQ_OK;
+}
+
+static int check_peer(const dq_peer* peer, const float* var) {
+  DQ_CHECK_ARG(peer && var, "null argument");
+  const dq_peer& P = *peer;
+  DQ_CHECK_ARG(P.world >= 1 && P.world <= DQ_PEER_MAX && P.rank >= 0 && P.rank < P.world,
+               "peer: 1 <= world <= DQ_PEER_MAX, 0 <= rank < world");
+  DQ_CHECK_ARG(P.lo >= 0 && P.lo % 4 == 0 && P.n > P.lo && (P.n - P.lo) % (4 * P.world) == 0,
+               "peer: lo % 4 == 0 and (n - lo) % (4 world) == 0");
+  DQ_CHECK_ARG(P.param[P.rank] == var, "peer: var must be this rank's parameter buffer");
+  for (int q = 0; q < P.world; ++q)
+    DQ_CHECK_ARG(P.grad[q] && P.param[q] && P.flags[q], "peer: null rank buffer");
+  DQ_CHECK_ARG(P.max_polls > 0, "peer: max_polls must be positive");
+  return DQ_OK;
+}
+
+int dq_peer_all_gather(const dq_peer* peer, float* var, void* stream) {
+  const int rc = check_peer(peer, var);
+  if (rc != DQ_OK) return rc;
+  const dq_peer& P = *peer;
+  if (P.world > 1) {
+    Ctx c{(hipStream_t)stream, nullptr, false, 0};
+    group(c, AgParts{peer, var}.part(0), AgParts{peer, var}.part(1), AgParts{peer, var}.part(2));
+  }
+  DQ_CHECK_LAUNCH("dq_peer_all_gather");
+  return DQ_OK;
+}
+
+int dq_cnn_forward_fused_peer(const dq_cnn_params* p0, const float* x0, dq_cnn_acts* a0, float* ws0,
+                              const dq_cnn_params* p1, const float* x1, dq_cnn_acts* a1, float* ws1,
+                              int32_t batch, int32_t fc1_1, const dq_peer* peer, float* var,
+                              void* stream) {
+  DQ_CHECK_ARG(p0 && a0 && x0 && ws0 && p1 && a1 && ws1 && batch >= 1, "null argument");
+  DQ_CHECK_ARG(p0->in_channels == 4 && p1->in_channels == 4 && p0->n_out >= 1 && p1->n_out >= 1,
+               "the Nature CNN takes 84x84x4 NHWC input");
+  DQ_CHECK_ARG(ws0 != ws1, "the two networks need separate workspaces");
+  DQ_CHECK_ARG((fc1_1 & (4 | 8 | 32)) == 0 && (fc1_1 & 16),
+               "the deferred gather rides in the head_from 6 schedule's conv launches (flag 16)");
+  const int rc = check_peer(peer, var);
+  if (rc != DQ_OK) return rc;
+  Ctx c0{(hipStream_t)stream, ws0, false, 0}, c1{(hipStream_t)stream, ws1, false, 0};
+  const AgParts ag{peer, var};
+  forward_fused(c0, c1, FwdOps{p0, x0, a0, ws0, batch}, FwdOps{p1, x1, a1, ws1, batch},
+                (fc1_1 & 1) != 0, (fc1_1 & 2) != 0, true, true, true, false,
+                peer->world > 1 ? &ag : nullptr);
+  DQ_CHECK_LAUNCH("dq_cnn_forward_fused_peer");
   return DQ_OK;
 }
 

@@ -195,7 +195,8 @@ class PeerExchange(object):
   learner running the same protocol with itself (world 1).  Requires every learner on one
   node with peer access between their devices (``available``)."""
 
-  MAX_POLLS = 4_000_000      # per wait (~1-2 us per poll): a dead peer latches an error in seconds
+  MAX_POLLS = 30_000_000     # per wait (~1-2 us per poll): a dead peer latches an error in < 1 min,
+  # a live one may lag by tens of seconds (first-use code loads, host noise) without one
 
   def __init__(self, group, device, grad, params, lo, n, max_polls=None):
     from dopamine_amd import _lib
@@ -249,6 +250,13 @@ class PeerExchange(object):
     flags = [None] * dist.get_world_size(group)
     dist.all_gather_object(flags, bool(ok), group=group)
     return all(flags)
+
+  def all_gather(self, var, stream):
+    """The deferred all-gather in a launch of its own (dq_peer_all_gather): every other
+    rank's slice of ``var`` (this learner's flat parameters) as of its last published step
+    (the learner loop's last step, so every parameter is current when the loop returns)."""
+    self._lib.call('dq_peer_all_gather', ctypes.byref(self.desc), ctypes.c_void_p(var.data_ptr()),
+                   stream)
 
   def error(self):
     """0, or 1 + the flag a wait of this learner timed out on (a synchronising read)."""

@@ -631,7 +631,17 @@ int dq_cnn_backward_peer(const dq_cnn_params* p, const dq_cnn_params* g, int32_t
                          const float* x, const dq_cnn_acts* a, const float* dout,
                          dq_cnn_acts* d, float* ws, const dq_rider* riders, int32_t n_riders,
                          const dq_adam_args* opt, const dq_cnn_net* head, const dq_peer* peer,
-                         void* stream);
+                         int32_t defer_ag, void* stream);
+/* defer_ag != 0: launch 5 publishes this rank's slice and gathers the first quarter of the
+   others'; the next step's dq_cnn_forward_fused_peer gathers the rest in its three conv
+   launches (which read no fc parameter), or dq_peer_all_gather in a launch of its own (the
+   learner loop's last step: every parameter is current when the loop returns).  var: this
+   rank's flat parameters. */
+int dq_cnn_forward_fused_peer(const dq_cnn_params* p0, const float* x0, dq_cnn_acts* a0, float* ws0,
+                              const dq_cnn_params* p1, const float* x1, dq_cnn_acts* a1, float* ws1,
+                              int32_t batch, int32_t fc1_1, const dq_peer* peer, float* var,
+                              void* stream);
+int dq_peer_all_gather(const dq_peer* peer, float* var, void* stream);
 
 #ifdef __cplusplus
 }
