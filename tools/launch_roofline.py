@@ -1,7 +1,8 @@
 """Per-launch roofline of the Rainbow step (bench.py's default schedule, B = 32, 9 actions x
 51 atoms): each of the step's 11 launches with its duration (rocprofv3 --kernel-trace), its
 HBM-side bytes (rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE, one counter per pass), its
-algorithmic FLOPs, and its fraction of the binding resource.
+algorithmic FLOPs, its fraction of the binding resource, and its counted bytes against its
+algorithmic bytes (every tensor it reads once, every tensor it writes once: ALGO).
 
     rocprofv3 --kernel-trace -d T -o run -- python3 bench.py --skip-cpu-baseline --skip-configs
     rocprofv3 --pmc FETCH_SIZE -d F -o run --output-format csv -- python3 bench.py <same, short>
@@ -41,6 +42,37 @@ DW = {'fc2': NO * 513 * B, 'fc1': 512 * 7745 * B, 'conv3': 64 * 577 * 121 * B,
 DX = {'fc1': 7744 * 512 * B, 'conv3': 121 * 64 * 576 * B,
       'conv2': 21 * 21 * 32 * (2 * 2 * 64) * B}   # sub-pixel classes: 2 x 2 taps x 64
 DH = 51 * 512 * B                                      # d h = dlogits . W2 (chosen action)
+
+# Algorithmic bytes: every tensor a launch reads once, every tensor it writes once (fp32; TF1
+# Adam in an epilogue reads and writes p, m, v: 3 + 3 times the weights).
+STATE = B * 84 * 84 * 4 * 4                 # a gathered state stack, NHWC fp32
+A1, A2, A3 = B * 441 * 32 * 4, B * 121 * 64 * 4, B * 121 * 64 * 4
+H, DOUT = B * 512 * 4, B * NO * 4
+W_C1, W_C2, W_C3 = (8 * 8 * 4 * 32 + 32) * 4, (4 * 4 * 32 * 64 + 64) * 4, (3 * 3 * 64 * 64 + 64) * 4
+W_FC1, W_FC2 = (7744 * 512 + 512) * 4, (512 * NO + NO) * 4
+NZ3, NZ1 = 8, 28                            # split-K slabs (kSplitConvW, kSplitConv1W)
+SLAB3, SLAB2, SLAB1 = NZ3 * 64 * 577 * 4, NZ3 * 64 * 513 * 4, NZ1 * 32 * 257 * 4
+FC1_PARTS = 2 * 16 * B * 512 * 4            # fc1 split-K partials, both nets (kSplitFc1 16)
+FC2_PARTS = 2 * 16 * B * NO * 4             # fc2 k-band partials, both nets (FcHeadOp::kBands)
+FRAMES = 2 * B * 4 * 84 * 84                # the PER gather rider's frames in (two stacks out)
+TREE = B * 21 * 8 * 2                       # a PER write-back or sample rider's tree path
+ALGO = [  # (bytes read, bytes written) per launch, in LAUNCHES order
+    (FC2_PARTS + W_FC2, H + DOUT),                                       # C: d h, dlogits
+    (H + W_FC1 + A3, A3),                                                # B1: d a3
+    (H + A3 + 3 * W_FC1 + A3 + W_C3 + A2 + DOUT + 3 * W_FC2 + TREE,     # B2 (d h, a3 once)
+     3 * W_FC1 + A2 + 3 * W_FC2 + TREE),
+    (A3 + A2 + A2 + W_C2 + A1 + TREE, SLAB3 + A1 + SLAB2),               # B3 (d a2, a1 once)
+    (SLAB3 + A1 + STATE + FRAMES, W_C3 + SLAB1 + 2 * STATE),            # B4 + gather
+    (SLAB2 + 3 * W_C2 + SLAB1 + 3 * W_C1 + 4 * W_C3 + STATE + W_C1,     # B5 + target conv1
+     3 * W_C2 + 3 * W_C1 + 3 * W_C3 + A1),
+    (STATE + W_C1, A1),                                                  # F1
+    (2 * A1 + 2 * W_C2, 2 * A2),                                         # F2
+    (2 * A2 + 2 * W_C3, 2 * A3),                                         # F3
+    (2 * A3 + 2 * W_FC1, FC1_PARTS),                                     # F4
+    (FC1_PARTS + 2 * W_FC2, 2 * H + FC2_PARTS),                          # F5
+]
+# counter scale factors (tools/micro/pmc_calib.hip, profiles/r5_roofline/pmc_calib.md)
+FETCH_SCALE, WRITE_SCALE = 2.0, 1.0
 
 # the step's launches in order from the loss kernel and what they compute
 LAUNCHES = [
@@ -101,25 +133,29 @@ def main():
   dur = durations(sys.argv[1])
   fetch, kn = counters(sys.argv[2], 'FETCH_SIZE')
   write, _ = counters(sys.argv[3], 'WRITE_SIZE')
-  print('| launch | work | us | GFLOP | TFLOP/s | frac fp32 MFMA | fetch MB (x2) | write MB | '
-        'TB/s | frac HBM | binding |')
-  print('|---|---|---|---|---|---|---|---|---|---|---|')
-  tot = [0.0, 0.0, 0.0]
-  for (name, what, macs), t, f, w, k in zip(LAUNCHES, dur, fetch, write, kn):
+  print('| launch | work | us | GFLOP | TFLOP/s | frac fp32 MFMA | fetch MB (x%g) | write MB | '
+        'TB/s | frac HBM | binding | algo MB (r + w) | measured / algo |' % FETCH_SCALE)
+  print('|---|---|---|---|---|---|---|---|---|---|---|---|---|')
+  tot = [0.0, 0.0, 0.0, 0.0]
+  for (name, what, macs), t, f, w, k, (ar, aw) in zip(LAUNCHES, dur, fetch, write, kn, ALGO):
     fl = 2.0 * macs
     tf = fl / (t * 1e-6)
-    by = 2.0 * f + w
+    f, w = FETCH_SCALE * f, WRITE_SCALE * w
+    by = f + w
     bw = by / (t * 1e-6)
     fm, fh = tf / FP32_MFMA_PEAK, bw / HBM_PEAK
     tot[0] += t
     tot[1] += fl
     tot[2] += by
-    print('| %s | %s | %.1f | %.3f | %.1f | %.3f | %.2f | %.2f | %.2f | %.3f | %s |' % (
-        name, what, t, fl / 1e9, tf / 1e12, fm, 2 * f / 1e6, w / 1e6, bw / 1e12, fh,
-        'MFMA' if fm > fh else 'HBM'))
-  print('| step | | %.1f | %.3f | %.1f | %.3f | | | %.2f | %.3f | |' % (
+    tot[3] += ar + aw
+    print('| %s | %s | %.1f | %.3f | %.1f | %.3f | %.2f | %.2f | %.2f | %.3f | %s | %.2f + %.2f | '
+          '%.2f (r %.2f, w %.2f) |' % (
+              name, what, t, fl / 1e9, tf / 1e12, fm, f / 1e6, w / 1e6, bw / 1e12, fh,
+              'MFMA' if fm > fh else 'HBM', ar / 1e6, aw / 1e6, by / (ar + aw), f / ar, w / aw))
+  print('| step | | %.1f | %.3f | %.1f | %.3f | | | %.2f | %.3f | | %.2f | %.2f |' % (
       tot[0], tot[1] / 1e9, tot[1] / (tot[0] * 1e-6) / 1e12, tot[1] / (tot[0] * 1e-6) / FP32_MFMA_PEAK,
-      tot[2] / (tot[0] * 1e-6) / 1e12, tot[2] / (tot[0] * 1e-6) / HBM_PEAK))
+      tot[2] / (tot[0] * 1e-6) / 1e12, tot[2] / (tot[0] * 1e-6) / HBM_PEAK, tot[3] / 1e6,
+      tot[2] / tot[3]))
   print()
   for (name, _, _), k in zip(LAUNCHES, kn):
     print('- %s: `%s`' % (name, short(k)))
