@@ -490,9 +490,21 @@ def main(argv=None):
     if deadline is not None:
       deadline.phase('building the %s learner (RCCL communicators or peer mappings, rank-0 '
                      'broadcast)' % name, DEADLINE_S)
-    agent = build_agent(args.actions, args.capacity, args.batch, dev, pg=pg,
-                        use_hip_graph=not args.no_graph, native_comm=args.comm == 'native',
-                        **AGENT_OVERRIDES, **kwargs_of[name])
+    try:
+      agent = build_agent(args.actions, args.capacity, args.batch, dev, pg=pg,
+                          use_hip_graph=not args.no_graph, native_comm=args.comm == 'native',
+                          **AGENT_OVERRIDES, **kwargs_of[name])
+    except RuntimeError as e:
+      # the peer exchange's placement check (PeerExchange.available) is collective: every
+      # rank gets the same answer, so every rank skips the schedule together
+      if name != 'peer' or len(names) == 1:
+        raise
+      agent = None
+      schedules[name] = {'error': str(e)}
+      print('bench: rank %d: schedule peer unavailable: %s' % (rank, e), file=sys.stderr)
+      if deadline is not None:
+        deadline.done()
+      continue
     import random
     random.seed(0 + rank)
     fill_synthetic(agent._replay.memory, args.actions, seed=1 + rank)
@@ -545,6 +557,11 @@ def main(argv=None):
   for v in schedules.values():
     v.pop('_elapsed', None)
 
+  if agent is None:                 # the last schedule could not be built: time the gather on the best's
+    agent = build_agent(args.actions, args.capacity, args.batch, dev, pg=pg,
+                        use_hip_graph=not args.no_graph, native_comm=args.comm == 'native',
+                        **AGENT_OVERRIDES, **kwargs_of[best])
+    fill_synthetic(agent._replay.memory, args.actions, seed=1 + rank)
   graph_us, algo_bytes, gname = time_gather(agent, args.gather_iters)
   large = time_gather_large(agent)
   traffic, traffic_src = gather_traffic(args.batch)

@@ -261,6 +261,105 @@ def test_rainbow_bench_path_matches_float64_oracle():
   _check(_run_lockstep(agent, 'rainbow'), 'rainbow')
 
 
+LONG_STEPS = 1000      # gradient steps of the long-horizon run
+LONG_CHECK_EVERY = 100  # a full float64 check of the step's network, loss and gradient
+LONG_PARAM_ATOL = 1e-6  # fp32 updates vs the float64 trajectory after 1,000 steps (|w| ~ 0.05)
+# the conv gradients are sums over B x 441 (conv1) positions that cancel to a small fraction
+# of their terms, more so as training proceeds: measured 2.2e-5 (conv1_b) at step 900 against
+# 1e-5 in the first 13 (north_star's 1e-5 bar is on Q-values and losses, which stay at 1e-6)
+LONG_GRAD_TOL = 1e-4
+
+
+@pytest.mark.timeout(900)
+def test_rainbow_bench_path_long_horizon():
+  """The bench path (1M buffer, B = 32, chunk graphs, riders, fused Adam) over 1,000 gradient
+  steps with a target sync every 100: every step's indices, gathered batch and the host RNG
+  stream against the oracle sampler bit for bit (the oracle's tree takes the device's float32
+  priorities), the parameters against a float64 TF1 Adam trajectory fed the device's
+  gradients, and every 100th step's online logits, loss, priorities and gradient against
+  float64 (the loss on the device's target distribution; the target net's forward is the
+  13-step test's)."""
+  import bench
+  torch.cuda.set_device(0)
+  agent = bench.build_agent(9, 1_000_000, 32, torch.device('cuda', 0))
+  agent.target_update_period = 400          # training steps: a sync every 100 gradient steps
+  agent.enable_trace()
+  random.seed(0)
+  bench.fill_synthetic(agent._replay.memory, 9, seed=1)
+  _prime(agent)
+  mem = agent._replay.memory
+  B, A, U = agent._batch_size, agent.num_actions, agent._UNROLL
+  offsets = agent.online_convnet.fp.offsets
+  w = agent.online_convnet.fp.flat.cpu().double().numpy().copy()
+  opt = _Adam64(agent._opt, agent._opt_steps % 2)
+  orc = _oracle_replay(agent, True)
+  support = agent._support.cpu().double().numpy()
+  N = support.shape[0]
+  cg = np.float64(np.float32(agent.cumulative_gamma))
+  errs = dict(logits=0.0, loss=0.0, priorities=0.0, grad={}, params=0.0, checks=0, chunks=0,
+              single=0, syncs=0)
+  done = 0
+
+  def step(slot, full):
+    tr = {k: v[slot].cpu().numpy() for k, v in agent._trace.items()}
+    idx = orc.sample_index_batch(B)
+    np.testing.assert_array_equal(tr['indices'], idx)
+    b = orc.sample_transition_batch(B, indices=idx)
+    for name, ref in (('action', b[1]), ('reward', b[2]), ('terminal', b[6])):
+      np.testing.assert_array_equal(tr[name], ref, err_msg=name)
+    np.testing.assert_array_equal(tr['sampling_probabilities'], b[8])
+    x = np.moveaxis(b[0], -1, 1).astype(np.float32) / np.float32(255)
+    np.testing.assert_array_equal(tr['state'], x)
+    if full:
+      masks = {k: tr['act_' + k] for k in ('a1', 'a2', 'a3', 'h')}
+      P = ONC.Params64(w, offsets)
+      out = ONC.forward(P, ONC.to_input(np.moveaxis(x, 1, -1)), masks)
+      ref = OL.c51_loss(out.detach().numpy().reshape(B, A, N),
+                        tr['target_out'].astype(np.float64).reshape(B, A, N), b[1], b[2], b[6],
+                        support, cg, b[8], dtype=np.float64)
+      errs['logits'] = max(errs['logits'], _rel(tr['online_out'], out.detach().numpy()))
+      errs['loss'] = max(errs['loss'], _rel(tr['loss'], ref['loss']))
+      errs['priorities'] = max(errs['priorities'], float(
+          (np.abs(tr['priorities'] - ref['priorities']) / np.abs(ref['priorities'])).max()))
+      out.backward(torch.from_numpy(ref['grad'].reshape(B, A * N)))
+      g = P.flat_grad()
+      for name, (o, shape) in offsets.items():
+        n = int(np.prod(shape))
+        errs['grad'][name] = max(errs['grad'].get(name, 0.0), _rel(tr['grad'][o:o + n], g[o:o + n]))
+      errs['checks'] += 1
+    opt.step(w, tr['grad'].astype(np.float64))
+    orc.set_priority(np.asarray(idx, np.int32), tr['priorities'].astype(np.float32))
+
+  while done < LONG_STEPS:
+    syncs = agent.training_steps // agent.target_update_period
+    if agent._chunk_ok() and done + U <= LONG_STEPS:
+      agent.train_gradient_steps(U)             # ONE chunk-graph replay
+      torch.cuda.synchronize()
+      for j in range(U):
+        step(j, (done + j) % LONG_CHECK_EVERY == 0)
+      done += U
+      errs['chunks'] += 1
+    else:                                       # a target sync due inside the next chunk
+      k = agent._opt_steps % 2
+      agent.train_gradient_steps(1)
+      torch.cuda.synchronize()
+      step(U + k, done % LONG_CHECK_EVERY == 0)
+      done += 1
+      errs['single'] += 1
+    errs['syncs'] += agent.training_steps // agent.target_update_period - syncs
+    if done % 100 < (U if errs['single'] == 0 else 1) or done == LONG_STEPS:
+      print('long horizon: %d steps' % done, flush=True)     # progress (a quiet run looks hung)
+  errs['params'] = float(np.abs(agent.online_convnet.fp.flat.cpu().double().numpy() - w).max())
+  agent._discard_prefetch()
+  mem.sync_rng()
+  assert random.getstate() == orc.py_rng.getstate()
+  print(json.dumps({'northstar_long_horizon': errs}), flush=True)
+  assert errs['syncs'] >= 9 and errs['chunks'] >= 200, errs
+  assert errs['logits'] <= Q_TOL and errs['loss'] <= Q_TOL and errs['priorities'] <= Q_TOL, errs
+  assert max(errs['grad'].values()) <= LONG_GRAD_TOL, errs
+  assert errs['params'] <= LONG_PARAM_ATOL, errs
+
+
 @pytest.mark.timeout(600)
 def test_rainbow_bench_drive_without_gradient_stores_is_the_traced_run_bitwise():
   """The bench's exact drive (keep_gradients = False: the fused TF1 Adam consumes fc1's
