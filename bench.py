@@ -166,8 +166,8 @@ def timed_steps(agent, steps, warmup, per_call=False, pg=None, deadline=None):
     prime = 0
     phase('priming (graph capture, steps with their fc / conv bucket all-reduces)')
     while ((not agent.graphs_primed() or prime + warmup < MIN_PRE_STEPS) and prime < 400):
-      grad_steps(5)
-      prime += 5
+      grad_steps(9)     # two chunks and a single step per call: every graph the window replays
+      prime += 9
     grad_steps(warmup)
     torch.cuda.synchronize()
     if pg is not None:

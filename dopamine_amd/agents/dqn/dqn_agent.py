@@ -538,13 +538,23 @@ class DQNAgent(object):
   def _forward_fused_c51(self, c, part=None):
     raise NotImplementedError
 
-  # The peer exchange's all-gather inside the learner loop's chunk graphs: every step but the
-  # last publishes its updated slice without gathering the others' (backward launch 5 loses
-  # its gather blocks), the next step's three conv forward launches gather them (they read no
-  # fc parameter; fc1's launch follows) and the chunk ends with dq_peer_all_gather.  Per-call
-  # steps keep the gather in launch 5.  Bitwise the same parameters either way.
+  # The peer exchange's all-gather inside the learner loop's chunk graphs: every step
+  # publishes its updated slice and gathers a quarter of the others' in backward launch 5, the
+  # next step's three conv forward launches gather the rest (they read no fc parameter; fc1's
+  # launch follows) -- across chunk boundaries too: a chunk after another in the same
+  # train_gradient_steps call starts with the gather its predecessor left (_peer_pending), and
+  # the call ends with one dq_peer_all_gather launch (_peer_flush), as does anything inside it
+  # that reads the parameters (a target sync, a per-call step).  Per-call steps keep the whole
+  # gather in launch 5.  Bitwise the same parameters either way.
   _peer_defer_ag = False     # the backward being recorded defers its gather
   _peer_fwd_ag = False       # the forward being recorded gathers the previous step's
+  _peer_pending = False      # the parameters await the last replayed step's deferred gather
+
+  def _peer_flush(self):
+    """Completes a deferred all-gather (one launch) so every parameter is current."""
+    if self._peer_pending:
+      self._peer.all_gather(self._opt.params, _lib.stream_of(self._device))
+      self._peer_pending = False
 
   def _peer_fwd_gather(self):
     """forward_fused* keyword arguments of the deferred gather ({} when none rides)."""
@@ -1281,6 +1291,7 @@ class DQNAgent(object):
     finally:
       self._defer_fc = False
       self._join_fc()
+      self._peer_flush()
 
   def _train_gradient_steps(self, n):
     while n > 0:
@@ -1292,9 +1303,11 @@ class DQNAgent(object):
         # a sync falling on the chunk's last gradient step or after it (see _chunk_ok)
         for t in range(t0, self.training_steps):
           if t % self.target_update_period == 0:
+            self._peer_flush()
             self._sync_target()
         n -= K
         continue
+      self._peer_flush()
       for _ in range(self.update_period):
         self._train_step()
       n -= 1
@@ -1310,6 +1323,11 @@ class DQNAgent(object):
       return True
     if self._chunk_gathers():
       return all(('gchunk', self._UNROLL, k, 0, False) in self._graph_sets for k in (0, 1))
+    if self._peer is not None and self._peer.world > 1 and self._fused():
+      # the chunk graphs with and without the predecessor's deferred gather (a learner-loop
+      # call of two chunks or more captures the latter)
+      return all(('chunk', self._UNROLL, k, p) in self._graph_sets for k in (0, 1)
+                 for p in (False, True))
     return all(('chunk', self._UNROLL, k) in self._graph_sets for k in (0, 1))
 
   def _captures_collectives(self):
@@ -1352,25 +1370,24 @@ class DQNAgent(object):
       return self._run_gather_chunk(K)
     mem = self._replay.memory
     k0 = self._opt_steps % 2
-    key = ('chunk', K, k0)
+    defer = (not self._collective() and self._peer is not None and self._peer.world > 1 and
+             self._fused())
+    pending = defer and self._peer_pending
+    key = ('chunk', K, k0) + ((pending,) if defer else ())
     g = self._graph_sets.get(key)
     if g is None:
       self._join_fc()                 # nothing outside the capture may be pending
       torch.cuda.synchronize(self._device)
       g = torch.cuda.CUDAGraph()
       if not self._collective():
-        defer = self._peer is not None and self._peer.world > 1 and self._fused()
         try:
           with torch.cuda.graph(g, pool=self._graph_pool):
             for j in range(K):
               k = (k0 + j) % 2
-              self._peer_fwd_ag, self._peer_defer_ag = defer and j > 0, defer
+              self._peer_fwd_ag, self._peer_defer_ag = defer and (j > 0 or pending), defer
               self._grad_step(k, k, True)
               self._device_opt_step(k)
               self._trace_step(j, k)
-            if defer:                 # every parameter current when the chunk returns
-              self._peer.all_gather(self._opt.params,
-                                    _lib.stream_of(self._device))
         finally:
           self._peer_fwd_ag = self._peer_defer_ag = False
       else:
@@ -1393,6 +1410,7 @@ class DQNAgent(object):
       self._join_fc()
     mem.reserve_rng(self._batch_size, steps=K)
     g.replay()
+    self._peer_pending = defer        # the last step's gather is left to the next chunk / flush
     self._opt_steps += K
     c = (k0 + K - 1) % 2
     self._replay._out = self._pbuf[c]

@@ -37,11 +37,12 @@ def _agent(pg, seed, net_seed=0, capacity=CAP, **kw):
   return agent
 
 
-def _run(agent, loop=False):
+def _run(agent, loop=False, steps=None):
+  steps = STEPS if steps is None else steps
   if loop:
-    agent.train_gradient_steps(STEPS)
+    agent.train_gradient_steps(steps)
   else:
-    for _ in range(STEPS):
+    for _ in range(steps):
       for _ in range(agent.update_period):
         agent._train_step()
   torch.cuda.synchronize()
@@ -118,7 +119,7 @@ def test_two_ranks_learner_loop_equal_single_learner_bitwise():
   assert np.array_equal(flat, single)
 
 
-def _mean_gradient_reference(loop=False, moments=False, world=2, capacity=CAP):
+def _mean_gradient_reference(loop=False, moments=False, world=2, capacity=CAP, n_steps=None):
   """Every rank's learner in ONE process, no collective: each _train_step computes its
   own gradient (the optimizer deferred), the flat gradients are averaged in group-rank
   order ((((g0 + g1) + g2) + ...) * (1 / N), parallel.allreduce_mean_'s gloo order), and
@@ -136,7 +137,7 @@ def _mean_gradient_reference(loop=False, moments=False, world=2, capacity=CAP):
   for ag in agents:
     ag._device_opt_step = lambda k, ag=ag: steps.append((ag, k))
     ag._sync_target = lambda ag=ag: steps.append((ag, 'sync'))
-  for _ in range(STEPS * agents[0].update_period):
+  for _ in range((STEPS if n_steps is None else n_steps) * agents[0].update_period):
     steps.clear()
     for ag in agents:
       ag._train_step()

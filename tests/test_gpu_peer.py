@@ -22,7 +22,13 @@ from tests.test_gpu_multirank import STEPS, _agent, _free_port, _mean_gradient_r
 pytestmark = pytest.mark.gpu
 
 
-def _peer_worker(rank, world, port, q, loop, same_seed=False, idle_rank=-1, max_polls=None):
+# the two-rank learner-loop test's steps: enough for two chunks in one train_gradient_steps call
+# between target syncs, so a chunk starts with its predecessor's deferred gather
+LOOP_STEPS = 24
+
+
+def _peer_worker(rank, world, port, q, loop, same_seed=False, idle_rank=-1, max_polls=None,
+                 n_steps=None):
   import sys
   sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
   import torch.distributed as dist
@@ -42,7 +48,7 @@ def _peer_worker(rank, world, port, q, loop, same_seed=False, idle_rank=-1, max_
     dist.destroy_process_group()
     return
   try:
-    flat = _run(agent, loop)
+    flat = _run(agent, loop, n_steps)
     err = None
     agent.mean_loss()
   except RuntimeError as e:
@@ -54,6 +60,9 @@ def _peer_worker(rank, world, port, q, loop, same_seed=False, idle_rank=-1, max_
     raise
   assert agent._graph_sets.get(True) is not None    # the later steps replayed captured graphs
   assert not loop or any(isinstance(k, tuple) and k[0] == 'chunk' for k in agent._graph_sets)
+  # world > 1: a chunk that started with its predecessor's deferred gather ran too
+  assert not loop or world == 1 or any(isinstance(k, tuple) and k[0] == 'chunk' and k[-1] is True
+                                       for k in agent._graph_sets), list(agent._graph_sets)
   ok = parallel.replicas_in_sync(agent.online_convnet.fp.flat)
   ok = ok and parallel.replicas_in_sync(agent.target_convnet.fp.flat)
   agent._gather_opt_state()         # every slice's moments, as a checkpoint sees them
@@ -119,10 +128,11 @@ def test_peer_two_ranks_equal_mean_gradient_reference(loop):
   """Two processes on cuda:0, different buffers and network seeds (rank 0's broadcast at
   construction): parameters and gathered moments bitwise the rank-ordered mean-gradient
   TF1 Adam reference; the replicas stay bit-identical."""
-  res, codes = _spawn(2, loop)
+  n = LOOP_STEPS if loop else STEPS
+  res, codes = _spawn(2, loop, n_steps=n)
   _, ok, flat, m, v, st, steps, _ = res[0]
-  assert codes == [0, 0] and ok and steps == STEPS
-  ref, rm, rv = _mean_gradient_reference(loop, moments=True)
+  assert codes == [0, 0] and ok and steps == n
+  ref, rm, rv = _mean_gradient_reference(loop, moments=True, n_steps=n)
   assert np.array_equal(flat, ref)
   assert np.array_equal(m, rm) and np.array_equal(v, rv)
 
