@@ -112,6 +112,21 @@ def main():
     per.append([evs[j].elapsed_time(evs[j + 1]) * 1e3 for j in range(5)])
   print('GPU us per 4-step chunk of a 20-step window (median of 6):',
         ' '.join('%.1f' % v for v in np.median(np.array(per), axis=0)))
+  # the first chunk against the idle time before the window (host sleep after the sync)
+  for idle_us in (0, 100, 1000, 10000, 100000):
+    per = []
+    for rep in range(6):
+      torch.cuda.synchronize()
+      if idle_us:
+        time.sleep(idle_us * 1e-6)
+      evs[0].record(stream)
+      for j in range(5):
+        agent.train_gradient_steps(4)
+        evs[j + 1].record(stream)
+      torch.cuda.synchronize()
+      per.append([evs[j].elapsed_time(evs[j + 1]) * 1e3 for j in range(5)])
+    print('idle %6d us before the window: GPU us per chunk (median of 6):' % idle_us,
+          ' '.join('%.1f' % v for v in np.median(np.array(per), axis=0)))
   gc.enable()
   print('host us, one 4-step chunk from an idle device: total %.1f; ' % (tot * 1e6) +
         '; '.join('%s %.1f' % (k, v * 1e6) for k, v in spent.items()))
