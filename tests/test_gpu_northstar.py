@@ -271,31 +271,42 @@ LONG_GRAD_TOL = 1e-4
 
 
 @pytest.mark.timeout(900)
-def test_rainbow_bench_path_long_horizon():
-  """The bench path (1M buffer, B = 32, chunk graphs, riders, fused Adam) over 1,000 gradient
-  steps with a target sync every 100: every step's indices, gathered batch and the host RNG
-  stream against the oracle sampler bit for bit (the oracle's tree takes the device's float32
-  priorities), the parameters against a float64 TF1 Adam trajectory fed the device's
-  gradients, and every 100th step's online logits, loss, priorities and gradient against
-  float64 (the loss on the device's target distribution; the target net's forward is the
-  13-step test's)."""
+@pytest.mark.parametrize('kind', ['rainbow', 'dqn'])
+def test_bench_path_long_horizon(kind):
+  """The bench path (1M buffer, B = 32, chunk graphs, riders, fused optimizer) over 1,000
+  gradient steps with a target sync every 100 -- config 3 (Rainbow, PER, TF1 Adam) and config
+  2 (DQN, uniform replay with the chunk gathers, TF1 centered RMSProp): every step's indices,
+  gathered batch and the host RNG stream against the oracle sampler bit for bit (PER: the
+  oracle's tree takes the device's float32 priorities), the parameters against a float64
+  optimizer trajectory fed the device's gradients, and every 100th step's online outputs,
+  loss, (priorities) and gradient against float64 (the loss on the device's target-net
+  outputs; the target net's forward is the 13-step tests')."""
   import bench
+  from dopamine_amd.agents.dqn.dqn_agent import DQNAgent
   torch.cuda.set_device(0)
-  agent = bench.build_agent(9, 1_000_000, 32, torch.device('cuda', 0))
+  prioritized = kind == 'rainbow'
+  if prioritized:
+    agent = bench.build_agent(9, 1_000_000, 32, torch.device('cuda', 0))
+  else:
+    agent = DQNAgent(num_actions=6, replay_capacity=1_000_000, batch_size=32,
+                     device=torch.device('cuda', 0))
   agent.target_update_period = 400          # training steps: a sync every 100 gradient steps
   agent.enable_trace()
   random.seed(0)
-  bench.fill_synthetic(agent._replay.memory, 9, seed=1)
+  np.random.seed(0)
+  bench.fill_synthetic(agent._replay.memory, agent.num_actions, seed=1 if prioritized else 2)
   _prime(agent)
   mem = agent._replay.memory
   B, A, U = agent._batch_size, agent.num_actions, agent._UNROLL
   offsets = agent.online_convnet.fp.offsets
   w = agent.online_convnet.fp.flat.cpu().double().numpy().copy()
-  opt = _Adam64(agent._opt, agent._opt_steps % 2)
-  orc = _oracle_replay(agent, True)
-  support = agent._support.cpu().double().numpy()
-  N = support.shape[0]
+  k0 = agent._opt_steps % 2
+  opt = _Adam64(agent._opt, k0) if prioritized else _RMSProp64(agent._opt, k0)
+  orc = _oracle_replay(agent, prioritized)
   cg = np.float64(np.float32(agent.cumulative_gamma))
+  if prioritized:
+    support = agent._support.cpu().double().numpy()
+    N = support.shape[0]
   errs = dict(logits=0.0, loss=0.0, priorities=0.0, grad={}, params=0.0, checks=0, chunks=0,
               single=0, syncs=0)
   done = 0
@@ -307,28 +318,35 @@ def test_rainbow_bench_path_long_horizon():
     b = orc.sample_transition_batch(B, indices=idx)
     for name, ref in (('action', b[1]), ('reward', b[2]), ('terminal', b[6])):
       np.testing.assert_array_equal(tr[name], ref, err_msg=name)
-    np.testing.assert_array_equal(tr['sampling_probabilities'], b[8])
+    if prioritized:
+      np.testing.assert_array_equal(tr['sampling_probabilities'], b[8])
     x = np.moveaxis(b[0], -1, 1).astype(np.float32) / np.float32(255)
     np.testing.assert_array_equal(tr['state'], x)
     if full:
       masks = {k: tr['act_' + k] for k in ('a1', 'a2', 'a3', 'h')}
       P = ONC.Params64(w, offsets)
       out = ONC.forward(P, ONC.to_input(np.moveaxis(x, 1, -1)), masks)
-      ref = OL.c51_loss(out.detach().numpy().reshape(B, A, N),
-                        tr['target_out'].astype(np.float64).reshape(B, A, N), b[1], b[2], b[6],
-                        support, cg, b[8], dtype=np.float64)
+      tout = tr['target_out'].astype(np.float64)
+      if prioritized:
+        ref = OL.c51_loss(out.detach().numpy().reshape(B, A, N), tout.reshape(B, A, N), b[1],
+                          b[2], b[6], support, cg, b[8], dtype=np.float64)
+        errs['priorities'] = max(errs['priorities'], float(
+            (np.abs(tr['priorities'] - ref['priorities']) / np.abs(ref['priorities'])).max()))
+        gout = ref['grad'].reshape(B, A * N)
+      else:
+        ref = OL.dqn_huber(out.detach().numpy(), tout, b[1], b[2], b[6], cg, dtype=np.float64)
+        gout = ref['grad']
       errs['logits'] = max(errs['logits'], _rel(tr['online_out'], out.detach().numpy()))
       errs['loss'] = max(errs['loss'], _rel(tr['loss'], ref['loss']))
-      errs['priorities'] = max(errs['priorities'], float(
-          (np.abs(tr['priorities'] - ref['priorities']) / np.abs(ref['priorities'])).max()))
-      out.backward(torch.from_numpy(ref['grad'].reshape(B, A * N)))
+      out.backward(torch.from_numpy(gout))
       g = P.flat_grad()
       for name, (o, shape) in offsets.items():
         n = int(np.prod(shape))
         errs['grad'][name] = max(errs['grad'].get(name, 0.0), _rel(tr['grad'][o:o + n], g[o:o + n]))
       errs['checks'] += 1
     opt.step(w, tr['grad'].astype(np.float64))
-    orc.set_priority(np.asarray(idx, np.int32), tr['priorities'].astype(np.float32))
+    if prioritized:
+      orc.set_priority(np.asarray(idx, np.int32), tr['priorities'].astype(np.float32))
 
   while done < LONG_STEPS:
     syncs = agent.training_steps // agent.target_update_period
@@ -352,8 +370,12 @@ def test_rainbow_bench_path_long_horizon():
   errs['params'] = float(np.abs(agent.online_convnet.fp.flat.cpu().double().numpy() - w).max())
   agent._discard_prefetch()
   mem.sync_rng()
-  assert random.getstate() == orc.py_rng.getstate()
-  print(json.dumps({'northstar_long_horizon': errs}), flush=True)
+  if prioritized:
+    assert random.getstate() == orc.py_rng.getstate()
+  else:
+    a, b = np.random.get_state(), orc.np_rng.get_state()
+    assert np.array_equal(a[1], b[1]) and a[2] == b[2]
+  print(json.dumps({'northstar_long_horizon': kind, **errs}), flush=True)
   assert errs['syncs'] >= 9 and errs['chunks'] >= 200, errs
   assert errs['logits'] <= Q_TOL and errs['loss'] <= Q_TOL and errs['priorities'] <= Q_TOL, errs
   assert max(errs['grad'].values()) <= LONG_GRAD_TOL, errs
