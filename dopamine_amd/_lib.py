@@ -105,7 +105,7 @@ class Rider(ctypes.Structure):
 
 PEER_MAX = 8            # DQ_PEER_MAX
 PEER_FLAG_WORDS = 8     # DQ_PEER_FLAG_WORDS
-(PEER_STEP, PEER_GRAD, PEER_PARAM, PEER_CONV, PEER_ERR, PEER_TICKET) = range(6)
+(PEER_STEP, PEER_GRAD, PEER_PARAM, PEER_CONV, PEER_ERR, PEER_TICKET, PEER_PUB_COUNT) = range(7)
 
 
 class IpcHandle(ctypes.Structure):

@@ -221,6 +221,11 @@ class DQNAgent(object):
       raise RuntimeError("exchange='peer': the learners are not on one node with peer access "
                          "between their devices")
     lo, n = self._shard_bounds()
+    if lo != n - self._grad_buckets()[0].numel():
+      # a head of fc1 floats would join the replicated conv bucket, which the peers read in
+      # the exchange launch after this learner may have rewritten it (dq_cnn_backward_peer)
+      raise ValueError("exchange='peer': the fc bucket does not split into %d equal 16-byte "
+                       'slices (networks.FC_BUCKET_ALIGN)' % self._world())
     return parallel.PeerExchange(self._pg, self._device, self.online_convnet.fp.grad,
                                  self.online_convnet.fp.flat, lo, n)
 

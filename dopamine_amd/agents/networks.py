@@ -20,15 +20,23 @@ import torch.nn.functional as F
 
 class FlatParams(object):
   """Allocates named parameter views inside one contiguous fp32 buffer (each
-  slice 16-byte aligned) plus a matching flat gradient buffer."""
+  slice 16-byte aligned) plus a matching flat gradient buffer.  tail_align = (name,
+  multiple): zero padding at the end so that the range from parameter ``name`` to the end
+  is a whole number of ``multiple`` floats (the Nature-CNN nets: the fc bucket splits into
+  world equal 16-byte slices for every world size 1..8 -- the data-parallel exchanges'
+  shards, DQNAgent._shard_bounds; the padding keeps zero gradients, so every optimizer
+  leaves it zero)."""
 
-  def __init__(self, shapes, device):
+  def __init__(self, shapes, device, tail_align=None):
     self.offsets = {}
     off = 0
     for name, shape in shapes:
       n = int(np.prod(shape))
       self.offsets[name] = (off, tuple(shape))
       off += (n + 3) // 4 * 4
+    if tail_align is not None:
+      name, multiple = tail_align
+      off += -(off - self.offsets[name][0]) % multiple
     self.numel = off
     self.flat = torch.zeros(off, dtype=torch.float32, device=device)
     self.grad = torch.zeros(off, dtype=torch.float32, device=device)
@@ -88,8 +96,10 @@ TORSO = [('conv1', (32, None, 8, 8), 4), ('conv2', (64, 32, 4, 4), 2), ('conv3',
 class _Net(object):
   """Base: owns FlatParams; subclasses define shapes() and forward()."""
 
+  tail_align = None
+
   def __init__(self, device, seed, init='rainbow'):
-    self.fp = FlatParams(self.shapes(), device)
+    self.fp = FlatParams(self.shapes(), device, self.tail_align)
     gen = torch.Generator().manual_seed(seed)
     with torch.no_grad():
       for name, (o, shape) in self.fp.offsets.items():
@@ -131,8 +141,14 @@ def _torso_shapes(stack):
           ('conv3_w', (64, 64, 3, 3)), ('conv3_b', (64,))]
 
 
+# the fc bucket (fc1_w .. the end) in 4 * lcm(1..8) floats: equal 16-byte slices at any world
+# size up to 8 (parallel.PeerExchange, ZeRO-1)
+FC_BUCKET_ALIGN = ('fc1_w', 4 * 840)
+
+
 class NatureDQNNetwork(_Net):
   """atari_lib.py:85-105 -> q_values (B, A)."""
+  tail_align = FC_BUCKET_ALIGN
 
   def __init__(self, num_actions, stack_size=4, device='cuda', seed=0):
     self.A, self.S = num_actions, stack_size
@@ -149,6 +165,7 @@ class NatureDQNNetwork(_Net):
 
 class RainbowNetwork(_Net):
   """atari_lib.py:108-144 -> logits (B, A, N); q/probabilities derived."""
+  tail_align = FC_BUCKET_ALIGN
 
   def __init__(self, num_actions, num_atoms=51, stack_size=4, device='cuda', seed=0):
     self.A, self.N, self.S = num_actions, num_atoms, stack_size

@@ -245,7 +245,8 @@ struct AdamOp {
 // Loads of another rank's (and, uniformly, one's own) exchanged words are system-coherent
 // (sc0 sc1: no stale line of a previous step in this GPU's caches); a flag is a system-scope
 // store behind a system release (s_waitcnt after it: the guide's compiler-hazard rule).
-enum { kPeerStep = 0, kPeerGrad = 1, kPeerParam = 2, kPeerConv = 3, kPeerErr = 4, kPeerTicket = 5 };
+enum { kPeerStep = 0, kPeerGrad = 1, kPeerParam = 2, kPeerConv = 3, kPeerErr = 4, kPeerTicket = 5,
+       kPeerPubCount = 6 };
 
 __device__ __forceinline__ uint64_t peer_load(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -267,12 +268,28 @@ __device__ __forceinline__ float4 peer_load4(const float* base, int64_t i4) {
 __device__ __forceinline__ uint64_t peer_step(const dq_peer& P) {
   return __hip_atomic_load(&P.flags[P.rank][kPeerStep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// publish flag `which` of step e: everything this rank stored before this launch is final
-__device__ __forceinline__ void peer_publish(const dq_peer& P, int which) {
+// publish flag `which` of step e: everything this rank stored before this launch is final.
+// The stores were made by earlier launches on every XCD, and each XCD's L2 holds its own
+// dirty lines: a release fence writes back only the L2 of the XCD it runs on, and a peer's
+// loads (over xGMI, or through another process's mapping of this memory) do not see lines
+// still dirty in this device's L2s.  So kPubBlocks blocks -- consecutive workgroups, dealt
+// round-robin over the XCDs -- each write back their XCD's L2, wait for it, and count
+// themselves on a per-rank counter; the last to arrive stores the flag.  (Publishing from one
+// block left stale slices at world 8: tools/peer_world_diag.py)
+constexpr int kPubBlocks = 16;
+__device__ __forceinline__ void peer_publish_xcd(const dq_peer& P, int which) {
+  if (threadIdx.x != 0) return;
   const uint64_t e = peer_step(P);
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");        // this XCD's L2 written back
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  peer_store(&P.flags[P.rank][which], e + 1);
+  const unsigned long long t =
+      __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(&P.flags[P.rank][kPeerPubCount]),
+                             1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if ((t + 1) % kPubBlocks == 0) {                     // every block's write-back is done
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    peer_store(&P.flags[P.rank][which], e + 1);
+  }
 }
 // the whole block waits until every rank's flag `which` passed step e (lane q of wave 0
 // polls rank q; bounded: a timeout latches the error word and every waiter gives up).
@@ -300,6 +317,9 @@ __device__ __forceinline__ bool peer_wait(const dq_peer& P, int which, uint64_t 
       __builtin_amdgcn_s_sleep(2);
     }
     if (q == 0) *ok = bad ? 0 : 1;
+    // acquire: this CU's L1 and this XCD's L2 drop lines of the peers' memory read before
+    // the flags moved
+    if (!bad) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   }
   __syncthreads();
   const bool r = *ok != 0;
@@ -320,16 +340,15 @@ __device__ __forceinline__ void peer_ticket(const dq_peer& P, int total_blocks, 
   }
 }
 
-// one block: publish flag `which` (kPeerGrad / kPeerParam; kPeerConv is PeerConvOp's block 0)
+// publish flag `which` (kPeerGrad / kPeerParam; kPeerConv is PeerExchOp's first blocks'):
+// kPubBlocks one-wave blocks, peer_publish_xcd
 struct PeerPubOp {
   static constexpr int kT = 64;
   static constexpr int kLds = 0;
   dq_peer P;
   int which;
-  __device__ __forceinline__ void run(int, float*) const {
-    if (threadIdx.x == 0) peer_publish(P, which);
-  }
-  int blocks() const { return 1; }
+  __device__ __forceinline__ void run(int, float*) const { peer_publish_xcd(P, which); }
+  int blocks() const { return kPubBlocks; }
 };
 
 // float4 i of the rank-ordered mean over the ranks' gradients, ApplyAdam'd into var / m / v
@@ -442,7 +461,7 @@ struct PeerAgOp {
   int blocks() const { return nb; }
 };
 
-// the exchange launch (6): block 0 publishes the conv bucket; every block waits for every
+// the exchange launch (6): blocks 0..kPubBlocks-1 publish the conv bucket; every block waits for every
 // rank's, takes the rank-ordered mean of [0, lo) and applies TF1 Adam (replicated; block 0
 // also advances the beta powers).  Every block takes a ticket; the last advances the step
 // counter.
@@ -457,7 +476,7 @@ struct PeerExchOp {
   int nc;
   __device__ __forceinline__ void run(int blk, float* smem) const {
     const uint64_t e = peer_step(P);
-    if (blk == 0 && threadIdx.x == 0) peer_publish(P, kPeerConv);
+    if (blk < kPubBlocks) peer_publish_xcd(P, kPeerConv);
     if (peer_wait(P, kPeerConv, e, smem)) {
       const float alpha = adam_alpha_of(o.state, o.slot, o.lr);
       const float omb1 = __fsub_rn(1.0f, o.b1), omb2 = __fsub_rn(1.0f, o.b2);
@@ -1307,7 +1326,7 @@ void backward_peer(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int B
   auto rs = [&](int64_t b0, int64_t b1) {
     return PeerRsAdamOp{P, od, oa->var, oa->m, oa->v, b0, b1, blocks_for(b1 - b0, 2)};
   };
-  const int nc = blocks_for(P.lo, 2);
+  const int nc = std::max(kPubBlocks, blocks_for(P.lo, 2));   // its first blocks publish
   const int na = blocks_for((P.n - P.lo) * (P.world - 1) / P.world, 4);
   auto rd = [&](int i) { return i >= 1 && i - 1 < n_riders ? riders + (i - 1) : nullptr; };
   group_r(c, rd(1), dX_fc1);
@@ -1575,8 +1594,12 @@ int dq_cnn_backward_peer(const dq_cnn_params* p, const dq_cnn_params* g, int32_t
                "peer: lo % 4 == 0 and (n - lo) % (4 world) == 0");
   DQ_CHECK_ARG(P.n >= (int64_t)(p->fc2_b + p->n_out - opt->var),
                "peer: [lo, n) must reach the end of the flat parameter buffer");
-  DQ_CHECK_ARG(P.lo >= (int64_t)(p->fc1_w - opt->var),
-               "peer: the sharded range lies in the fc bucket (its gradient final after launch 2)");
+  // exactly the fc bucket: a head of fc1 floats in the conv bucket would be read by the peers
+  // in launch 6 after this rank may have rewritten it in the next step's launch 2 (the conv
+  // gradients proper are rewritten only after the next step's launch-3 wait)
+  DQ_CHECK_ARG(P.lo == (int64_t)(p->fc1_w - opt->var),
+               "peer: the sharded range is exactly the fc bucket [fc1_w, n) (pad the flat buffer "
+               "so that its length divides into 4 world-float slices)");
   DQ_CHECK_ARG(P.param[P.rank] == opt->var && P.grad[P.rank] == g->conv1_w - (p->conv1_w - opt->var),
                "peer: this rank's buffers must be opt->var and the gradient of its layout");
   for (int q = 0; q < P.world; ++q)

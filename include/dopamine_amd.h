@@ -599,9 +599,10 @@ int dq_comm_version(void);
  *             ordered mean and ApplyAdam (replicated; this one advances the beta powers);
  *             the step counter flags[0] += 1 by the launch's last block.
  * No collective library, no second queue, no graph fork or join.  Remote loads are
- * system-coherent (sc0 sc1), the flags system-scope stores behind a system release; every
- * wait is bounded (max_polls) and a timeout latches flags[4] (dq_peer_flags_words words
- * per rank, zero-initialised; flags[0] = the step counter, equal on every rank). */
+ * system-coherent (sc0 sc1) behind an acquire; a flag is stored by the last of 16 blocks
+ * that each wrote back their XCD's L2 behind a system release (counted in flags[6]); every
+ * wait is bounded (max_polls) and a timeout latches flags[4] (DQ_PEER_FLAG_WORDS words per
+ * rank, zero-initialised; flags[0] = the step counter, equal on every rank). */
 #define DQ_PEER_MAX 8
 #define DQ_PEER_FLAG_WORDS 8
 typedef struct dq_ipc_handle {

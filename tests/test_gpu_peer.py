@@ -137,6 +137,26 @@ def test_peer_two_ranks_equal_mean_gradient_reference(loop):
   assert np.array_equal(m, rm) and np.array_equal(v, rv)
 
 
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize('world', [4, 8])
+def test_peer_world_n_equal_mean_gradient_reference(world):
+  """4 and 8 processes on cuda:0 in the learner loop (world - 1 remote slices per gather,
+  the rank-ordered mean of world gradients, the deferred gather across chunks; world 8 is
+  config 4's): bitwise the mean-gradient TF1 Adam reference, parameters and gathered
+  moments."""
+  res, codes = _spawn(world, True, n_steps=LOOP_STEPS, max_polls=4_000_000)
+  _, ok, flat, m, v, st, steps, _ = res[0]
+  assert codes == [0] * world
+  assert steps == LOOP_STEPS, steps
+  ref, rm, rv = _mean_gradient_reference(True, moments=True, world=world, n_steps=LOOP_STEPS)
+  d = np.abs(flat - ref)
+  assert np.array_equal(flat, ref), ('replicas in sync: %s; params differ at %d of %d, first %s, '
+                                     'max %g' % (ok, int((d > 0).sum()), d.size,
+                                                 np.flatnonzero(d)[:8], float(d.max())))
+  assert ok
+  assert np.array_equal(m, rm) and np.array_equal(v, rv)
+
+
 @pytest.mark.timeout(600)
 def test_peer_wait_times_out_instead_of_hanging():
   """Rank 1 builds its learner (the handles are exchanged) but never trains: rank 0's waits

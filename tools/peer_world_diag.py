@@ -1,0 +1,78 @@
+"""Diagnostic for the peer exchange at world N on one GPU (tests/test_gpu_peer.py's setup):
+every rank's parameters after the learner loop, per parameter tensor: the largest difference
+from rank 0 and from the mean-gradient reference, and which ranks differ.
+
+    python tools/peer_world_diag.py N [steps] [loop 0|1]
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+
+def worker(rank, world, port, q, steps, loop):
+  sys.path.insert(0, ROOT)
+  import torch.distributed as dist
+  os.environ['MASTER_ADDR'] = '127.0.0.1'
+  os.environ['MASTER_PORT'] = str(port)
+  torch.cuda.set_device(0)
+  dist.init_process_group('gloo', rank=rank, world_size=world)
+  from tests.test_gpu_multirank import _agent, _run
+  agent = _agent(dist.group.WORLD, rank, net_seed=1000 * rank, exchange='peer')
+  flat = _run(agent, loop, steps)
+  agent.check_exchange()
+  q.put((rank, flat.numpy(), int(agent._peer.flags[0].item()),
+         sorted(str(k) for k in agent._graph_sets)))
+  agent.close()
+  dist.barrier()
+  dist.destroy_process_group()
+
+
+def main():
+  world = int(sys.argv[1])
+  steps = int(sys.argv[2]) if len(sys.argv) > 2 else 24
+  loop = (sys.argv[3] != '0') if len(sys.argv) > 3 else True
+  from tests.test_gpu_multirank import _free_port, _mean_gradient_reference
+  from dopamine_amd.agents.networks import RainbowNetwork
+  ctx = mp.get_context('spawn')
+  q = ctx.Queue()
+  port = _free_port()
+  procs = [ctx.Process(target=worker, args=(r, world, port, q, steps, loop)) for r in range(world)]
+  for p in procs:
+    p.start()
+  res = {}
+  for _ in range(world):
+    r, flat, st, keys = q.get(timeout=600)
+    res[r] = flat
+    print('rank %d: step counter %d, graphs %s' % (r, st, keys), flush=True)
+  for p in procs:
+    p.join(timeout=120)
+  ref = _mean_gradient_reference(loop, world=world, n_steps=steps)
+  offs = RainbowNetwork(9, device='cpu').fp.offsets
+  print('%-8s %12s %12s  ranks differing from rank 0' % ('tensor', 'max |r - r0|', 'max |r0-ref|'))
+  n_all = res[0].size
+  lo = 77984 + (n_all - 77984) % (4 * world)   # DQNAgent._shard_bounds (fc1_w at 77,984)
+  S = (n_all - lo) // world
+  for r in range(1, world):
+    bad = np.flatnonzero(res[r] != res[0])
+    sl = np.where(bad >= lo, (bad - lo) // S, -1)
+    print('rank %d vs rank 0: %d elements differ; by slice %s; first %s' % (
+        r, bad.size, {int(k): int(v) for k, v in zip(*np.unique(sl, return_counts=True))},
+        bad[:6].tolist()))
+  bad = np.flatnonzero(res[0] != ref)
+  sl = np.where(bad >= lo, (bad - lo) // S, -1)
+  print('rank 0 vs reference: %d elements differ; by slice %s' % (
+      bad.size, {int(k): int(v) for k, v in zip(*np.unique(sl, return_counts=True))}))
+  for name, (o, shape) in offs.items():
+    n = int(np.prod(shape))
+    d0 = [float(np.abs(res[r][o:o + n] - res[0][o:o + n]).max()) for r in range(world)]
+    dr = float(np.abs(res[0][o:o + n] - ref[o:o + n]).max())
+    print('%-8s %12.3g %12.3g  %s' % (name, max(d0), dr, [r for r in range(world) if d0[r] > 0]))
+
+
+if __name__ == '__main__':
+  main()
