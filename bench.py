@@ -509,6 +509,10 @@ def main(argv=None):
     random.seed(0 + rank)
     fill_synthetic(agent._replay.memory, args.actions, seed=1 + rank)
     torch.cuda.synchronize()
+    if pg is not None:       # the ranks fill their buffers at their own pace; start together
+      deadline.phase('the barrier after the replay fill', DEADLINE_S)
+      dist.barrier()
+      deadline.done()
     elapsed, prime = timed_steps(agent, args.steps, args.warmup, args.per_call, pg, deadline)
     per_rank = [elapsed]
     if pg is not None:

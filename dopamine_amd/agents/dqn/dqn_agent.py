@@ -555,6 +555,24 @@ class DQNAgent(object):
   _peer_fwd_ag = False       # the forward being recorded gathers the previous step's
   _peer_pending = False      # the parameters await the last replayed step's deferred gather
 
+  _peer_synced = False       # the learners met at a host barrier before this exchange began
+
+  def resync_exchange(self):
+    """The next gradient step of the peer exchange starts behind a host-side barrier of the
+    process group (collective: every learner calls it at the same point, e.g. at the start of
+    a training phase).  The exchange's device-side waits are bounded (they latch an error
+    after PeerExchange.MAX_POLLS polls, tens of seconds), so learners that reach their first
+    step far apart -- one still filling its replay or finishing an evaluation phase -- meet
+    on the host first.  No-op without the peer exchange."""
+    self._peer_synced = False
+
+  def _peer_ready(self):
+    if self._peer is not None and not self._peer_synced:
+      import torch.distributed as dist
+      torch.cuda.synchronize(self._device)
+      dist.barrier(group=self._pg)
+      self._peer_synced = True
+
   def _peer_flush(self):
     """Completes a deferred all-gather (one launch) so every parameter is current."""
     if self._peer_pending:
@@ -1290,6 +1308,7 @@ class DQNAgent(object):
     n = int(n)
     if self._closed:
       raise RuntimeError('the agent was closed (its communicators are destroyed)')
+    self._peer_ready()
     self._defer_fc = True
     try:
       self._train_gradient_steps(n)
@@ -1432,6 +1451,7 @@ class DQNAgent(object):
       raise RuntimeError('the agent was closed (its communicators are destroyed)')
     if self._replay.memory.add_count > self.min_replay_history:
       if self.training_steps % self.update_period == 0:
+        self._peer_ready()
         self._run_train_op()
         if (self.summary_writer is not None and self.training_steps > 0 and
             self.training_steps % self.summary_writing_frequency == 0):

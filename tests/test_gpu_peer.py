@@ -44,7 +44,8 @@ def _peer_worker(rank, world, port, q, loop, same_seed=False, idle_rank=-1, max_
   assert agent._peer is not None and agent._sharded() and not agent._collective()
   if rank == idle_rank:
     q.put((rank, 'idle'))
-    dist.barrier()
+    dist.barrier()          # the others' host barrier before their first exchange step
+    dist.barrier()          # and their closing one
     dist.destroy_process_group()
     return
   try:
