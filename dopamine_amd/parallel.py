@@ -221,15 +221,26 @@ class PeerExchange(object):
       allh = [None] * self.world
       dist.all_gather_object(allh, mine, group=group)
       torch.cuda.synchronize(device)
-      for q in range(self.world):
-        if q == self.rank:
-          continue
-        for k in range(3):
-          h = _lib.IpcHandle.from_buffer_copy(allh[q][k])
-          ptr, base = ctypes.c_void_p(), ctypes.c_void_p()
-          _lib.call('dq_peer_ipc_open', ctypes.byref(h), ctypes.byref(ptr), ctypes.byref(base))
-          self._opened.append(base.value)
-          ptrs[q][k] = ptr.value
+      err = None
+      try:
+        for q in range(self.world):
+          if q == self.rank:
+            continue
+          for k in range(3):
+            h = _lib.IpcHandle.from_buffer_copy(allh[q][k])
+            ptr, base = ctypes.c_void_p(), ctypes.c_void_p()
+            _lib.call('dq_peer_ipc_open', ctypes.byref(h), ctypes.byref(ptr), ctypes.byref(base))
+            self._opened.append(base.value)
+            ptrs[q][k] = ptr.value
+      except _lib.DQError as e:
+        err = str(e)
+      # every rank learns whether every mapping opened: all raise together or none does
+      errs = [None] * self.world
+      dist.all_gather_object(errs, err, group=group)
+      if any(e is not None for e in errs):
+        self.close()
+        raise RuntimeError('peer exchange: mapping the other learners\' buffers failed: %s'
+                           % next(e for e in errs if e is not None))
     d = _lib.Peer(world=self.world, rank=self.rank, lo=self.lo, n=self.n,
                   max_polls=int(max_polls or self.MAX_POLLS))
     for q in range(self.world):
