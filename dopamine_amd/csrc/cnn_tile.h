@@ -1282,24 +1282,39 @@ __global__ __launch_bounds__(256) void k_splitk_reduce(const float* ws, int spli
 
 // the same sums 4 elements per thread with 16-B slab loads (M * N % 4 == 0); each element
 // still goes through the epilogue on its own, in the same slab order
-template <class EP>
-__global__ __launch_bounds__(256) void k_splitk_reduce4(const float* ws, int splits, int M, int N, EP E) {
-  const int64_t i = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
-  const int64_t MN = (int64_t)M * N;
-  if (i >= MN) return;
-  float4 s = ld4(ws + i);
-  for (int z0 = 1; z0 < splits; z0 += 8) {
-    float4 v[8];
+// kU slab loads in flight per round, summed in slab order
+template <int kU>
+__device__ __forceinline__ void splitk_sum4(const float* ws, int splits, int64_t MN, int64_t i,
+                                            float4& s) {
+  for (int z0 = 1; z0 < splits; z0 += kU) {
+    float4 v[kU];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = ld4(ws + (int64_t)min(z0 + u, splits - 1) * MN + i);
+    for (int u = 0; u < kU; ++u) v[u] = ld4(ws + (int64_t)min(z0 + u, splits - 1) * MN + i);
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
+    for (int u = 0; u < kU; ++u)
       if (z0 + u < splits) {
         s.x = __fadd_rn(s.x, v[u].x);
         s.y = __fadd_rn(s.y, v[u].y);
         s.z = __fadd_rn(s.z, v[u].z);
         s.w = __fadd_rn(s.w, v[u].w);
       }
+  }
+}
+
+template <class EP>
+__global__ __launch_bounds__(256) void k_splitk_reduce4(const float* ws, int splits, int M, int N, EP E) {
+  const int64_t i = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+  const int64_t MN = (int64_t)M * N;
+  if (i >= MN) return;
+  float4 s = ld4(ws + i);
+  // few slabs (IQN's FC1 / dW1: 4 / 2): no clamped duplicate loads of the last slab
+  switch (splits) {
+    case 1: break;
+    case 2: splitk_sum4<1>(ws, splits, MN, i, s); break;
+    case 3: splitk_sum4<2>(ws, splits, MN, i, s); break;
+    case 4: splitk_sum4<3>(ws, splits, MN, i, s); break;
+    case 5: splitk_sum4<4>(ws, splits, MN, i, s); break;
+    default: splitk_sum4<8>(ws, splits, MN, i, s); break;
   }
   const float r[4] = {s.x, s.y, s.z, s.w};
   int m = (int)(i / N), n = (int)(i - (int64_t)m * N);   // one division, then step along the row
