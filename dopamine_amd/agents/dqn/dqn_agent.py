@@ -239,10 +239,14 @@ class DQNAgent(object):
     """Releases the learner's RCCL communicators (each holds proxy threads and device
     buffers until destroyed) or peer mappings: waits for the device, drops the HIP graphs
     that captured their collectives, then destroys them.  The agent cannot train
-    afterwards.  A no-op for a single replica."""
+    afterwards.  A no-op for a single replica.  With the peer exchange it is collective: the
+    learners meet at a host barrier before unmapping, so none frees buffers another's last
+    launches still read."""
     self._join_fc()
     torch.cuda.synchronize(self._device)
     if self._peer is not None:
+      import torch.distributed as dist
+      dist.barrier(group=self._pg)
       self._graph_sets = {}
       self._graph_pool = None
       self._peer.close()
