@@ -565,3 +565,78 @@ def test_iqn_breakout_step_matches_float64_oracle(double_dqn):
   assert errs['dq'] <= Q_TOL, errs
   assert max(errs['grad'].values()) <= GRAD_TOL, errs
   assert errs['params'] <= PARAM_ATOL, errs
+
+
+IQN_LONG_STEPS = 500
+
+
+@pytest.mark.timeout(900)
+def test_iqn_breakout_long_horizon():
+  """Config 5 over 500 graph-replayed gradient steps with a target sync every 100: every
+  step's indices, gathered batch and Python's RNG stream bit for bit against the oracle
+  sampler, the parameters against a float64 TF1 Adam trajectory fed the device's gradients,
+  and every 100th step's online quantiles, quantile loss, d loss / d Z and gradient against
+  float64 on the device's taus and ReLU decisions (the loss on the device's target and
+  argmax quantiles; the target net's forward is the 6-step test's)."""
+  import bench
+  torch.cuda.set_device(0)
+  agent = _iqn_agent(False)
+  agent.target_update_period = 400          # training steps: a sync every 100 gradient steps
+  agent.enable_trace()
+  random.seed(0)
+  np.random.seed(0)
+  bench.fill_synthetic(agent._replay.memory, 4, seed=3)
+  _prime(agent)
+  B, U, Np = 64, agent._UNROLL, 64
+  offsets = agent.online_convnet.fp.offsets
+  k0 = agent._opt_steps % 2
+  w = agent.online_convnet.fp.flat.cpu().double().numpy().copy()
+  opt = _Adam64(agent._opt, k0)
+  orc = _oracle_replay(agent, True)
+  cg = np.float64(np.float32(agent.cumulative_gamma))
+  errs = dict(q=0.0, loss=0.0, dq=0.0, grad={}, params=0.0, checks=0, syncs=0)
+  for s in range(IQN_LONG_STEPS):
+    syncs = agent.training_steps // agent.target_update_period
+    full = s % 100 == 0
+    if full:
+      masks_of = agent._iqn['online']
+    agent.train_gradient_steps(1)
+    torch.cuda.synchronize()
+    errs['syncs'] += agent.training_steps // agent.target_update_period - syncs
+    tr = {k: v[U + (k0 + s) % 2].cpu().numpy() for k, v in agent._trace.items()}
+    idx = orc.sample_index_batch(B)
+    np.testing.assert_array_equal(tr['indices'], idx)
+    b = orc.sample_transition_batch(B, indices=idx)
+    st, act, rew, nst, term = b[0], b[1], b[2], b[3], b[6]
+    x = np.moveaxis(st, -1, 1).astype(np.float32) / np.float32(255)
+    np.testing.assert_array_equal(tr['state'], x)
+    np.testing.assert_array_equal(tr['next_state'],
+                                  np.moveaxis(nst, -1, 1).astype(np.float32) / np.float32(255))
+    if full:
+      masks = ONC.iqn_masks(masks_of)
+      P = ONC.Params64(w, offsets)
+      q = ONC.iqn_forward(P, ONC.to_input(np.moveaxis(x, 1, -1)),
+                          torch.from_numpy(tr['taus']).double(), masks=masks)
+      tq_all = tr['target_q'].astype(np.float64)
+      ref = OL.iqn_loss(q.detach().numpy(), tq_all[:Np * B], tq_all[Np * B:], tr['taus'], act,
+                        rew, term, cg, 1.0, dtype=np.float64)
+      errs['q'] = max(errs['q'], _rel(tr['qv'], q.detach().numpy()))
+      errs['loss'] = max(errs['loss'], _rel(tr['loss'], ref['loss']))
+      errs['dq'] = max(errs['dq'], _rel(tr['grad_out'], ref['grad']))
+      q.backward(torch.from_numpy(ref['grad']))
+      g = P.flat_grad()
+      for name, (o, shape) in offsets.items():
+        n = int(np.prod(shape))
+        errs['grad'][name] = max(errs['grad'].get(name, 0.0), _rel(tr['grad'][o:o + n], g[o:o + n]))
+      errs['checks'] += 1
+      print('iqn long horizon: %d steps' % s, flush=True)   # progress (a quiet run looks hung)
+    opt.step(w, tr['grad'].astype(np.float64))
+  errs['params'] = float(np.abs(agent.online_convnet.fp.flat.cpu().double().numpy() - w).max())
+  agent._discard_prefetch()
+  agent._replay.memory.sync_rng()
+  assert random.getstate() == orc.py_rng.getstate()     # the sum tree's stratified sampler
+  print(json.dumps({'northstar_long_horizon': 'iqn', **errs}), flush=True)
+  assert errs['syncs'] >= 4 and errs['checks'] == 5, errs
+  assert errs['q'] <= Q_TOL and errs['loss'] <= Q_TOL and errs['dq'] <= Q_TOL, errs
+  assert max(errs['grad'].values()) <= LONG_GRAD_TOL, errs
+  assert errs['params'] <= LONG_PARAM_ATOL, errs
