@@ -145,7 +145,7 @@ def test_peer_world_n_equal_mean_gradient_reference(world):
   the rank-ordered mean of world gradients, the deferred gather across chunks; world 8 is
   config 4's): bitwise the mean-gradient TF1 Adam reference, parameters and gathered
   moments."""
-  res, codes = _spawn(world, True, n_steps=LOOP_STEPS, max_polls=4_000_000)
+  res, codes = _spawn(world, True, n_steps=LOOP_STEPS)
   _, ok, flat, m, v, st, steps, _ = res[0]
   assert codes == [0] * world
   assert steps == LOOP_STEPS, steps
