@@ -55,7 +55,8 @@ def main():
   offs = RainbowNetwork(9, device='cpu').fp.offsets
   print('%-8s %12s %12s  ranks differing from rank 0' % ('tensor', 'max |r - r0|', 'max |r0-ref|'))
   n_all = res[0].size
-  lo = 77984 + (n_all - 77984) % (4 * world)   # DQNAgent._shard_bounds (fc1_w at 77,984)
+  o = offs['fc1_w'][0]
+  lo = o + (n_all - o) % (4 * world)           # DQNAgent._shard_bounds
   S = (n_all - lo) // world
   for r in range(1, world):
     bad = np.flatnonzero(res[r] != res[0])
