@@ -251,6 +251,11 @@ class Runner(object):
     return episodes, average
 
   def _run_train_phase(self, statistics):
+    # data-parallel learners over the peer exchange leave their evaluation phases apart:
+    # they meet on the host before the phase's first exchange step (a no-op otherwise)
+    resync = getattr(self._agent, 'resync_exchange', None)
+    if resync is not None:
+      resync()
     return self._phase(statistics, 'train', self._training_steps, eval_mode=False)
 
   def _run_eval_phase(self, statistics):
