@@ -139,7 +139,7 @@ WITHHOLD_RANK = (int(os.environ['DQ_BENCH_WITHHOLD_RANK'])
                  and 'DQ_BENCH_WITHHOLD_RANK' in os.environ else None)
 
 
-def timed_steps(agent, steps, warmup, per_call=False, pg=None, deadline=None):
+def timed_steps(agent, steps, warmup, per_call=False, pg=None, deadline=None, probe=None):
   """The bench protocol on one agent: untimed priming, whatever ``warmup`` is, until every
   graph the timed loop replays is captured (both step parities, the 4-step chunk graphs of
   both starting parities) and the device has been busy for at least MIN_PRE_STEPS steps
@@ -147,7 +147,8 @@ def timed_steps(agent, steps, warmup, per_call=False, pg=None, deadline=None):
   the warmup; then exactly ``steps`` gradient steps between barriers + synchronize.  No
   cyclic-garbage collection pass inside the window (a full pass over a torch process's
   objects takes milliseconds).  deadline (N > 1): a parallel.Deadline armed for each
-  blocking phase.  Returns (elapsed seconds, priming steps)."""
+  blocking phase.  probe: called with 'before' / 'after' just outside the window (the device
+  idle; e.g. the peer exchange's wait counters).  Returns (elapsed seconds, priming steps)."""
   def phase(label):
     if deadline is not None:
       deadline.phase(label, DEADLINE_S)
@@ -176,6 +177,8 @@ def timed_steps(agent, steps, warmup, per_call=False, pg=None, deadline=None):
         time.sleep(DEADLINE_S + 60)     # rehearsal only: this rank never joins the barrier
       dist.barrier()
     torch.cuda.synchronize()
+    if probe is not None:
+      probe('before')
     phase('the timed window (%d steps, each with its fc / conv bucket all-reduces)' % steps)
     t0 = time.perf_counter()
     grad_steps(steps)
@@ -184,6 +187,8 @@ def timed_steps(agent, steps, warmup, per_call=False, pg=None, deadline=None):
       phase('the barrier after the timed window')
       dist.barrier()
     elapsed = time.perf_counter() - t0
+    if probe is not None:
+      probe('after')
     if deadline is not None:
       deadline.done()
   finally:
@@ -208,7 +213,7 @@ def other_configs(device, steps):
     assert np.isfinite(loss), 'non-finite loss (%s)' % name
     res[name] = {'value': round(n / elapsed, 2), 'unit': 'gradient-steps/s', 'steps': n,
                  'ms_per_step': round(1e3 * elapsed / n, 4), 'batch': agent._batch_size,
-                 'final_mean_loss': round(loss, 5)}
+                 'final_mean_loss': round(loss, 8)}
     if name == 'dqn_pong' and agent._chunk_gathers():
       # the learner loop's chunk gather: one K * B launch per chunk (K = 4), timed as the
       # headline's gather is (standalone launches, fresh random indices, HIP events)
@@ -232,6 +237,51 @@ def other_configs(device, steps):
   res['iqn_breakout']['gemm_form'] = ('split-bf16 x6 (fp32 to rounding) for the embedding, FC1 '
                                       'and dW1/dWe; exact f32 MFMA for dX and the torso')
   return res
+
+
+def replica_verdict(agent):
+  """N > 1, after a schedule's window (collective): (every replicated tensor bit-identical
+  across the ranks, DQNAgent.replica_report's per-tensor report)."""
+  rep = agent.replica_report()
+  return all(v['in_sync'] for v in rep.values()), rep
+
+
+def diagnostics(agent, waits, steps, pg, rehearse, dev):
+  """N > 1: what the first multi-GPU run needs to explain itself.  Peer exchange: the
+  construction-time self-test's verdict and, per rank, the microseconds per step its
+  waiting blocks spent at each exchange point in the window (block 0 of each waiting op,
+  100 MHz device clock) and the XCDs the last publication covered."""
+  if agent._peer is None:
+    return {}
+  w = {}
+  if 'before' in waits and 'after' in waits:
+    for k in waits['after']:
+      dt = waits['after'][k][0] - waits['before'][k][0]
+      dn = waits['after'][k][1] - waits['before'][k][1]
+      w[k] = (round(dt * 0.01 / steps, 3), round(dn / steps, 2))    # 100 MHz ticks -> us
+  mine = {'wait_us_per_step': {k: v[0] for k, v in w.items()},
+          'waits_per_step': {k: v[1] for k, v in w.items()},
+          'xcds_seen': int(agent._peer.flags[agent._peer._lib.PEER_PUB_XCDS].item())}
+  allv = [None] * dist.get_world_size(pg)
+  dist.all_gather_object(allv, mine, group=pg)
+  st = agent._peer.selftest
+  return {'peer_wait_us_per_step': {k: [v['wait_us_per_step'].get(k) for v in allv]
+                                    for k in ('grad', 'param', 'conv')},
+          'peer_waits_per_step': allv[0]['waits_per_step'],
+          'peer_publish_xcds': [v['xcds_seen'] for v in allv],
+          'peer_selftest': ({'ok': st['ok'], 'words_per_rank': st['words_per_rank'],
+                             'ms': [r['ms'] for r in st['ranks']],
+                             'xcds_seen': [r['xcds_seen'] for r in st['ranks']]}
+                            if 'ok' in st else st)}
+
+
+def pick_headline(schedules):
+  """The fastest schedule that ran on every rank with its replicas in sync (a failed or
+  diverged schedule carries 'error' and no '_elapsed')."""
+  timed = [k for k in schedules if '_elapsed' in schedules[k] and 'error' not in schedules[k]]
+  if not timed:
+    raise RuntimeError('every data-parallel schedule failed: %r' % schedules)
+  return min(timed, key=lambda k: schedules[k]['_elapsed'])
 
 
 def time_gather(agent, iters, batch=None):
@@ -361,7 +411,7 @@ def bf16_child(args):
     agent._replay.memory.sync_rng()
     loss = agent.mean_loss()
     res[name] = {'value': round(n / elapsed, 2), 'unit': 'gradient-steps/s', 'steps': n,
-                 'ms_per_step': round(1e3 * elapsed / n, 4), 'final_mean_loss': round(loss, 5),
+                 'ms_per_step': round(1e3 * elapsed / n, 4), 'final_mean_loss': round(loss, 8),
                  'finite': bool(np.isfinite(loss))}
     del agent
     gc.collect()
@@ -513,7 +563,13 @@ def main(argv=None):
       deadline.phase('the barrier after the replay fill', DEADLINE_S)
       dist.barrier()
       deadline.done()
-    elapsed, prime = timed_steps(agent, args.steps, args.warmup, args.per_call, pg, deadline)
+    waits = {}
+
+    def probe(when):
+      if agent._peer is not None:
+        waits[when] = agent._peer.wait_counters()
+    elapsed, prime = timed_steps(agent, args.steps, args.warmup, args.per_call, pg, deadline,
+                                 probe)
     per_rank = [elapsed]
     if pg is not None:
       deadline.phase('the all_reduce of the per-rank times', DEADLINE_S)
@@ -545,17 +601,30 @@ def main(argv=None):
     if err is not None:
       raise RuntimeError(err)
     assert np.isfinite(loss), 'non-finite loss'
-    schedules[name] = {
+    entry = {
         'value': round(world * args.steps / elapsed, 2), 'ms_per_step': round(1e3 * elapsed / args.steps, 4),
         'per_rank_ms_per_step': [round(1e3 * e / args.steps, 4) for e in per_rank],
-        'prime_steps': prime, 'final_mean_loss': round(loss, 5), '_elapsed': elapsed,
+        'prime_steps': prime, 'final_mean_loss': round(loss, 8), '_elapsed': elapsed,
         'comm': ('peer memory (one stream)' if agent._peer is not None else
                  args.comm if agent._rccl is not None or args.comm == 'torch' else 'torch')
         if pg is not None else None}
-  timed = [k for k in schedules if '_elapsed' in schedules[k]]
-  if not timed:
-    raise RuntimeError('every data-parallel schedule failed: %r' % schedules)
-  best = min(timed, key=lambda k: schedules[k]['_elapsed'])
+    if pg is not None:
+      # the replicas must be bit-identical after the window: a schedule whose
+      # replicas differ is a failed schedule, never the headline (every rank sees the report)
+      deadline.phase('comparing the %s schedule\'s replicas bit for bit' % name, DEADLINE_S)
+      ok, rep = replica_verdict(agent)
+      entry.update(diagnostics(agent, waits, args.steps, pg, rehearse, dev))
+      deadline.done()
+      entry['replicas_in_sync'] = ok
+      entry['replicas_compared'] = {k: v['differing'] for k, v in rep.items()}
+      if not ok:
+        entry['error'] = 'replicas diverged: elements differing from rank 0, per rank: %r' % {
+            k: v['differing'] for k, v in rep.items() if not v['in_sync']}
+        entry.pop('_elapsed')
+        print('bench: rank %d: schedule %s failed: %s' % (rank, name, entry['error']),
+              file=sys.stderr)
+    schedules[name] = entry
+  best = pick_headline(schedules)
   elapsed, prime, loss = (schedules[best]['_elapsed'], schedules[best]['prime_steps'],
                           schedules[best]['final_mean_loss'])
   for v in schedules.values():
@@ -620,7 +689,7 @@ def main(argv=None):
         # work; the step is launch- and latency-bound at B = 32, not MFMA-bound)
         'step_mfma': step_mfma(args.actions, args.batch, elapsed / args.steps),
         'cpu_baseline': cpu,
-        'final_mean_loss': round(loss, 5),
+        'final_mean_loss': round(loss, 8),
         'gc_disabled_in_timed_window': True,
         # the library that ran: its recorded -D flags ("" = the product build; _lib refuses
         # any other unless DQ_DIAGNOSTIC_BUILD=1)

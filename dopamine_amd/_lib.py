@@ -9,7 +9,7 @@ import os
 from dopamine_amd import _build
 from dopamine_amd._build import HEADER, LIB_PATH  # noqa: F401
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 OK = 0
 (ST_OK, ST_EMPTY_TREE, ST_MAX_ATTEMPTS, ST_TAPE_EXHAUSTED, ST_NEG_PRIORITY, ST_TOO_FEW, ST_BAD_INDEX,
  ST_BROADCAST) = range(8)
@@ -104,8 +104,14 @@ class Rider(ctypes.Structure):
 
 
 PEER_MAX = 8            # DQ_PEER_MAX
-PEER_FLAG_WORDS = 8     # DQ_PEER_FLAG_WORDS
-(PEER_STEP, PEER_GRAD, PEER_PARAM, PEER_CONV, PEER_ERR, PEER_TICKET, PEER_PUB_COUNT) = range(7)
+PEER_FLAG_WORDS = 16    # DQ_PEER_FLAG_WORDS
+(PEER_STEP, PEER_GRAD, PEER_PARAM, PEER_CONV, PEER_ERR, PEER_TICKET, PEER_PUB_COUNT,
+ PEER_TEST) = range(8)
+PEER_WAIT_TICKS = 8     # flags[8..10]: 100 MHz ticks waited at the grad / param / conv points
+PEER_WAIT_COUNT = 11    # flags[11..13]: waits counted there
+PEER_PUB_XCDS = 14      # flags[14]: XCDs the last publication's blocks ran on
+PEER_ERR_PEER = 16      # error word: 16 + q -- rank q had latched an error
+PEER_ERR_XCD = 32       # error word: 32 + k -- a publication saw only k XCDs
 
 
 class IpcHandle(ctypes.Structure):
@@ -117,7 +123,7 @@ class Peer(ctypes.Structure):
   _fields_ = [('world', ctypes.c_int32), ('rank', ctypes.c_int32), ('lo', ctypes.c_int64),
               ('n', ctypes.c_int64), ('grad', ctypes.c_void_p * PEER_MAX),
               ('param', ctypes.c_void_p * PEER_MAX), ('flags', ctypes.c_void_p * PEER_MAX),
-              ('max_polls', ctypes.c_int64)]
+              ('max_polls', ctypes.c_int64), ('xcds', ctypes.c_int32), ('reserved', ctypes.c_int32)]
 
 
 _P = ctypes.c_void_p
@@ -234,6 +240,7 @@ SIGNATURES = {
                                   ctypes.POINTER(CnnParams), _P, ctypes.POINTER(CnnActs), _P,
                                   _I32, _I32, ctypes.POINTER(Peer), _P, _P],
     'dq_peer_all_gather': [ctypes.POINTER(Peer), _P, _P],
+    'dq_peer_selftest': [ctypes.POINTER(Peer), ctypes.c_uint32, _P, _P],
 }
 RESTYPES = {'dq_last_error': ctypes.c_char_p, 'dq_build_flags': ctypes.c_char_p, 'dq_cnn_workspace_floats': ctypes.c_size_t,
             'dq_iqn_workspace_floats': ctypes.c_size_t,

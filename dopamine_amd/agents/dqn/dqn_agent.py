@@ -1320,6 +1320,7 @@ class DQNAgent(object):
       self._defer_fc = False
       self._join_fc()
       self._peer_flush()
+    self._maybe_check_replicas()
 
   def _train_gradient_steps(self, n):
     while n > 0:
@@ -1466,11 +1467,51 @@ class DQNAgent(object):
 
   _loss_name = 'HuberLoss'
 
-  def check_exchange(self):
-    """Raises if a wait of the peer exchange timed out (the latched error word: another
-    learner stopped or fell out of step); a synchronising read.  No-op otherwise."""
+  def check_exchange(self, collective=False):
+    """Raises if the peer exchange's error word is latched (a wait timed out: another learner
+    stopped or fell out of step; or another rank's error; or a publication that missed an
+    XCD); a synchronising read.  collective: the ranks first agree on the worst error word,
+    so every rank raises together (call it at the same point on every rank).  No-op without
+    the peer exchange."""
     if self._peer is not None:
-      self._peer.check()
+      self._peer.check(collective=collective)
+
+  def replica_report(self):
+    """Collective (every rank of the group calls it at the same point): every replicated
+    tensor -- online and target parameters, the optimizer's moments (the sharded ranges'
+    slices gathered first, _gather_opt_state) and its state -- compared bit for bit with
+    group rank 0's (parallel.replica_report).  SURVEY 8e: identical updates keep the replicas
+    bit-identical; this is the check that they did."""
+    assert self._pg is not None, 'replica_report needs a process group'
+    self._join_fc()
+    torch.cuda.synchronize(self._device)
+    self._gather_opt_state()
+    named = {'online': self.online_convnet.fp.flat, 'target': self.target_convnet.fp.flat}
+    for k, v in sorted(vars(self._opt).items()):
+      if isinstance(v, torch.Tensor) and v.data_ptr() != self.online_convnet.fp.flat.data_ptr():
+        named['opt_' + k.lstrip('_')] = v
+    return parallel.replica_report(named, self._pg)
+
+  # data-parallel learner loop: every replica_check_period gradient steps (crossed inside a
+  # train_gradient_steps call, which every rank makes with the same n), the replicas are
+  # compared bit for bit and a divergence raises on every rank (0: never)
+  replica_check_period = 100_000
+  _next_replica_check = None
+
+  def _maybe_check_replicas(self):
+    if self._pg is None or not self.replica_check_period:
+      return
+    if self._next_replica_check is None:
+      self._next_replica_check = self._opt_steps + self.replica_check_period
+    if self._opt_steps < self._next_replica_check:
+      return
+    self._next_replica_check = self._opt_steps + self.replica_check_period
+    self.check_exchange(collective=True)
+    rep = self.replica_report()
+    bad = {k: v['differing'] for k, v in rep.items() if not v['in_sync']}
+    if bad:
+      raise RuntimeError('data-parallel replicas diverged after %d gradient steps: elements '
+                         'differing from rank 0, per rank: %r' % (self._opt_steps, bad))
 
   def mean_loss(self):
     """Mean loss of the last gradient step (the summary scalar, dqn:318-321); the fused

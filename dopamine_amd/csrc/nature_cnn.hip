@@ -240,13 +240,28 @@ struct AdamOp {
 // flag buffers are mapped into every learner; the exchange runs as ops of the backward's
 // grouped launches.  Flag words per rank: [0] step counter e (local; the exchange launch's
 // last block advances it), [1] fc-bucket gradient of step e final (= e + 1), [2] this rank's
-// slice of the parameters updated, [3] conv bucket gradient final, [4] error latch (1 + the
-// flag a wait timed out on), [5] the exchange launch's block ticket.
+// slice of the parameters updated, [3] conv bucket gradient final, [4] error latch (below),
+// [5] the exchange launch's block ticket, [6] the publishing blocks' per-XCD arrival counts,
+// [7] the self-test's flag (dq_peer_selftest), [8..10] 100 MHz ticks waited at the grad /
+// param / conv exchange points (block 0 of each waiting op), [11..13] how many such waits,
+// [14] how many XCDs the last publication saw.
+// Error latch: 1 + which (this rank's wait for flag `which` timed out), kErrPeer + q (rank q
+// had latched an error: every waiter gives up with it), kErrXcd + k (a publication's blocks
+// ran on k XCDs, fewer than P.xcds: a write-back may be missing, nothing is published).
+// Once it is set the rank publishes no flag again.
 // Loads of another rank's (and, uniformly, one's own) exchanged words are system-coherent
 // (sc0 sc1: no stale line of a previous step in this GPU's caches); a flag is a system-scope
 // store behind a system release (s_waitcnt after it: the guide's compiler-hazard rule).
 enum { kPeerStep = 0, kPeerGrad = 1, kPeerParam = 2, kPeerConv = 3, kPeerErr = 4, kPeerTicket = 5,
-       kPeerPubCount = 6 };
+       kPeerPubCount = 6, kPeerTest = 7, kPeerWaitTicks = 8, kPeerWaitCount = 11,
+       kPeerPubXcds = 14 };
+enum { kErrPeer = 16, kErrXcd = 32 };
+static_assert(kPeerPubXcds < DQ_PEER_FLAG_WORDS, "flag words");
+
+// the XCD this wave runs on (HW_REG_XCC_ID bits 3:0; s_getreg_b32 simm16 = size-1 << 11 | id 20)
+__device__ __forceinline__ unsigned xcc_id() {
+  return (unsigned)__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u;
+}
 
 __device__ __forceinline__ uint64_t peer_load(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -274,31 +289,69 @@ __device__ __forceinline__ uint64_t peer_step(const dq_peer& P) {
 // loads (over xGMI, or through another process's mapping of this memory) do not see lines
 // still dirty in this device's L2s.  So kPubBlocks blocks -- consecutive workgroups, dealt
 // round-robin over the XCDs -- each write back their XCD's L2, wait for it, and count
-// themselves on a per-rank counter; the last to arrive stores the flag.  (Publishing from one
-// block left stale slices at world 8: tools/peer_world_diag.py)
+// themselves on a per-rank word of eight 8-bit per-XCD counts (HW_REG_XCC_ID); the last to
+// arrive stores the flag, and only if the blocks ran on at least P.xcds distinct XCDs -- the
+// round-robin dealing is observed, not promised (the guide's dispatch contract), so a
+// placement that missed an XCD latches kErrXcd + k instead of publishing over a dirty L2.
+// (Publishing from one block left stale slices at world 8: tools/peer_world_diag.py)
+// Diagnostic builds only (tools/build_variant.py, never the product): -DDQ_PEER_DROP_XCD_FENCE=k
+// skips the write-back on XCD k; -DDQ_PEER_HIDE_XCD=k counts XCD k's blocks as the next XCD's.
 constexpr int kPubBlocks = 16;
 __device__ __forceinline__ void peer_publish_xcd(const dq_peer& P, int which) {
   if (threadIdx.x != 0) return;
   const uint64_t e = peer_step(P);
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");        // this XCD's L2 written back
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const unsigned long long t =
-      __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(&P.flags[P.rank][kPeerPubCount]),
-                             1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if ((t + 1) % kPubBlocks == 0) {                     // every block's write-back is done
+  unsigned x = xcc_id() & 7u;
+#ifdef DQ_PEER_DROP_XCD_FENCE
+  if (x != DQ_PEER_DROP_XCD_FENCE)
+#endif
+  {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");      // this XCD's L2 written back
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+#ifdef DQ_PEER_HIDE_XCD
+  if (x == DQ_PEER_HIDE_XCD) x = (x + 1) & 7u;
+#endif
+  uint64_t* cnt = &P.flags[P.rank][kPeerPubCount];
+  const uint64_t add = 1ull << (8 * x);
+  const uint64_t now =
+      __hip_atomic_fetch_add(cnt, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + add;
+  int total = 0, seen = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int f = (int)((now >> (8 * k)) & 0xffu);
+    total += f;
+    seen += f != 0 ? 1 : 0;
+  }
+  if (total == kPubBlocks) {                           // every block's write-back is done
+    // (the next publication is a later launch: the counts restart from zero)
+    __hip_atomic_store(cnt, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&P.flags[P.rank][kPeerPubXcds], (uint64_t)seen, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t* err = &P.flags[P.rank][kPeerErr];
+    if (seen < P.xcds) {
+      if (peer_load(err) == 0) peer_store(err, (uint64_t)(kErrXcd + seen));
+      return;
+    }
+    if (peer_load(err) != 0) return;                   // a latched error: publish nothing more
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     peer_store(&P.flags[P.rank][which], e + 1);
   }
 }
 // the whole block waits until every rank's flag `which` passed step e (lane q of wave 0
-// polls rank q; bounded: a timeout latches the error word and every waiter gives up).
+// polls rank q; bounded: a timeout latches the error word).  Every 64 polls the lanes also
+// read every rank's error word: one latched anywhere (a rank that timed out, or stopped
+// publishing) ends this wait too, latching kErrPeer + q here, so every live learner gives up
+// instead of reading a failed rank's stale buffers.  account: add the wait's duration (100 MHz
+// ticks) to this rank's counters for `which` (block 0 of each waiting op).
 // Returns false on a timeout or a latched error.
-__device__ __forceinline__ bool peer_wait(const dq_peer& P, int which, uint64_t e, float* smem) {
+__device__ __forceinline__ bool peer_wait(const dq_peer& P, int which, uint64_t e, float* smem,
+                                          bool account = false) {
   int* ok = reinterpret_cast<int*>(smem);
   if (threadIdx.x < 64) {
     const int q = threadIdx.x;
     uint64_t* err = &P.flags[P.rank][kPeerErr];
+    const uint64_t t0 = account ? __builtin_amdgcn_s_memrealtime() : 0;
     bool done = q >= P.world;
     int bad = 0;
     int64_t polls = 0;
@@ -306,17 +359,32 @@ __device__ __forceinline__ bool peer_wait(const dq_peer& P, int which, uint64_t 
       if (!done) done = peer_load(&P.flags[q][which]) > e;
       if (__all(done ? 1 : 0)) break;
       if (++polls > P.max_polls) {
-        if (q == 0) peer_store(err, (uint64_t)(1 + which));
+        if (q == 0 && peer_load(err) == 0) peer_store(err, (uint64_t)(1 + which));
         bad = 1;
         break;
       }
-      if ((polls & 63) == 0) {          // another waiter of this rank gave up: so do we
-        bad = __shfl(q == 0 ? (peer_load(err) != 0 ? 1 : 0) : 0, 0);
-        if (bad) break;
+      if ((polls & 63) == 0) {          // an error latched on any rank: give up as well
+        const bool eq = q < P.world && peer_load(&P.flags[q][kPeerErr]) != 0;
+        const uint64_t any = __ballot(eq ? 1 : 0);
+        if (any != 0) {
+          if (q == 0 && peer_load(err) == 0)
+            peer_store(err, (uint64_t)(kErrPeer + __builtin_ctzll(any)));
+          bad = 1;
+          break;
+        }
       }
       __builtin_amdgcn_s_sleep(2);
     }
-    if (q == 0) *ok = bad ? 0 : 1;
+    if (q == 0) {
+      *ok = bad ? 0 : 1;
+      if (account && which >= kPeerGrad && which <= kPeerConv) {
+        const uint64_t dt = __builtin_amdgcn_s_memrealtime() - t0;
+        __hip_atomic_fetch_add(&P.flags[P.rank][kPeerWaitTicks + which - kPeerGrad], dt,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(&P.flags[P.rank][kPeerWaitCount + which - kPeerGrad], (uint64_t)1,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
     // acquire: this CU's L1 and this XCD's L2 drop lines of the peers' memory read before
     // the flags moved
     if (!bad) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
@@ -411,7 +479,7 @@ struct PeerRsAdamOp {
   int nb;
   __device__ __forceinline__ void run(int blk, float* smem) const {
     const uint64_t e = peer_step(P);
-    if (!peer_wait(P, kPeerGrad, e, smem)) return;
+    if (!peer_wait(P, kPeerGrad, e, smem, blk == 0)) return;
     const float alpha = adam_alpha_of(o.state, o.slot, o.lr);
     const float omb1 = __fsub_rn(1.0f, o.b1), omb2 = __fsub_rn(1.0f, o.b2);
     const float inv = __fdiv_rn(1.0f, (float)P.world);
@@ -439,7 +507,7 @@ struct PeerAgOp {
   __device__ __forceinline__ void run(int blk, float* smem) const {
     const uint64_t e = peer_step(P);
     if (e < (uint64_t)lag) return;                 // before the first step: nothing updated
-    if (!peer_wait(P, kPeerParam, e - lag, smem)) return;
+    if (!peer_wait(P, kPeerParam, e - lag, smem, blk == 0)) return;
     const int64_t S4 = ((P.n - P.lo) / P.world) >> 2;       // float4 per slice
     const int64_t tot = min(f1, S4 * (P.world - 1)), st = (int64_t)nb * kT;
     for (int64_t j0 = f0 + (int64_t)blk * kT + threadIdx.x; j0 < tot; j0 += 4 * st) {
@@ -477,10 +545,18 @@ struct PeerExchOp {
   __device__ __forceinline__ void run(int blk, float* smem) const {
     const uint64_t e = peer_step(P);
     if (blk < kPubBlocks) peer_publish_xcd(P, kPeerConv);
-    if (peer_wait(P, kPeerConv, e, smem)) {
+    if (peer_wait(P, kPeerConv, e, smem, blk == 0)) {
       const float alpha = adam_alpha_of(o.state, o.slot, o.lr);
       const float omb1 = __fsub_rn(1.0f, o.b1), omb2 = __fsub_rn(1.0f, o.b2);
+#ifdef DQ_PEER_FAULT_REPLICA
+      // fault injection (tools/build_variant.py only): this rank's replicated conv-bucket
+      // mean is off by 2^-20, so its replica drifts from the others' (bench.py must report
+      // the schedule as failed)
+      const float inv = __fdiv_rn(P.rank == DQ_PEER_FAULT_REPLICA ? 1.00000095f : 1.0f,
+                                  (float)P.world);
+#else
       const float inv = __fdiv_rn(1.0f, (float)P.world);
+#endif
       const int64_t e4 = P.lo >> 2, st = (int64_t)nc * kT;
       for (int64_t i = (int64_t)blk * kT + threadIdx.x; i < e4; i += 2 * st) {
         const int64_t idx[2] = {i, i + st};
@@ -491,6 +567,63 @@ struct PeerExchOp {
     peer_ticket(P, nc, e);
   }
   int blocks() const { return nc; }
+};
+
+// dq_peer_selftest: word i of rank q's pattern for this tag (a 32-bit mix, so a stale or
+// misplaced line almost never matches by chance)
+__device__ __forceinline__ unsigned selftest_word(unsigned q, unsigned tag, unsigned i) {
+  unsigned h = i * 0x9E3779B1u ^ (q + 1u) * 0x85EBCA77u ^ tag;
+  h ^= h >> 16;
+  h *= 0x7feb352du;
+  h ^= h >> 15;
+  h *= 0x846ca68bu;
+  h ^= h >> 16;
+  return h;
+}
+// every block of a full grid stores its share of this rank's pattern over grad[rank][0, n)
+// with plain 16-byte stores, as the backward's epilogues store gradients
+struct SelfTestFillOp {
+  static constexpr int kT = 256;
+  static constexpr int kLds = 0;
+  dq_peer P;
+  unsigned tag;
+  int nb;
+  __device__ __forceinline__ void run(int blk, float*) const {
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    u32x4* g = reinterpret_cast<u32x4*>(P.grad[P.rank]);
+    for (int64_t i = (int64_t)blk * kT + threadIdx.x; i < P.n / 4; i += (int64_t)nb * kT) {
+      const unsigned w = (unsigned)(4 * i);
+      g[i] = u32x4{selftest_word(P.rank, tag, w), selftest_word(P.rank, tag, w + 1),
+                   selftest_word(P.rank, tag, w + 2), selftest_word(P.rank, tag, w + 3)};
+    }
+  }
+  int blocks() const { return nb; }
+};
+// wait for every rank's self-test flag, then read every rank's buffer with the exchange's
+// loads and count the words that are not its pattern
+struct SelfTestCheckOp {
+  static constexpr int kT = 256;
+  static constexpr int kLds = 1;
+  dq_peer P;
+  unsigned tag;
+  int* out;
+  int nb;
+  __device__ __forceinline__ void run(int blk, float* smem) const {
+    const uint64_t e = peer_step(P);
+    if (!peer_wait(P, kPeerTest, e, smem)) return;
+    int bad = 0;
+    for (int q = 0; q < P.world; ++q)
+      for (int64_t i = (int64_t)blk * kT + threadIdx.x; i < P.n / 4; i += (int64_t)nb * kT) {
+        const float4 v = peer_load4(P.grad[q], i);
+        const unsigned w = (unsigned)(4 * i);
+        bad += (__float_as_uint(v.x) != selftest_word(q, tag, w)) +
+               (__float_as_uint(v.y) != selftest_word(q, tag, w + 1)) +
+               (__float_as_uint(v.z) != selftest_word(q, tag, w + 2)) +
+               (__float_as_uint(v.w) != selftest_word(q, tag, w + 3));
+      }
+    if (bad) atomicAdd(out, bad);
+  }
+  int blocks() const { return nb; }
 };
 
 // TF1 RMSProp (the arithmetic of dq_rmsprop_tf1) over a contiguous range, as AdamOp
@@ -684,13 +817,52 @@ template <class... Ops>
 constexpr int group_wpe() {
   return (LateOk<Ops>::value && ...) ? 8 : 1;
 }
+#ifdef DQ_GROUP_PROF
+// Stamp build of the grouped launches (tools/group_stamps.py; never the product): every wave
+// that runs an op writes one record -- s_memrealtime (100 MHz) at the kernel's entry and after
+// its op returned, the launch's block count, the op's index in the group, the op-local block,
+// the wave and its XCD -- to a ring slot taken by a vector atomic on a counter.  Only these
+// buffers receive stamp words.
+struct GrpRec {
+  unsigned long long t0, t1;
+  unsigned total, op_blk;      // op_blk: op index << 24 | op-local block << 8 | wave << 4 | XCD
+};
+constexpr unsigned kGrpRecs = 1u << 22;
+__device__ GrpRec g_grp_rec[kGrpRecs];
+__device__ unsigned g_grp_n;
+template <class Op>
+__device__ __forceinline__ bool dispatch_prof(const Op& op, int nb, int& blk, float* smem, int k,
+                                              unsigned long long t0) {
+  if (blk < nb) {
+    if (Op::kT >= (int)blockDim.x || (int)threadIdx.x < Op::kT) {
+      op.run(blk, smem);
+      if ((threadIdx.x & 63) == 0) {
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+        const unsigned slot = atomicAdd(&g_grp_n, 1u) & (kGrpRecs - 1);
+        g_grp_rec[slot] = GrpRec{t0, t1, gridDim.x,
+                                 ((unsigned)k << 24) | ((unsigned)blk << 8) |
+                                     ((threadIdx.x >> 6) << 4) | xcc_id()};
+      }
+    }
+    return true;
+  }
+  blk -= nb;
+  return false;
+}
+#endif
+
 template <int T, class... Ops>
 __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(group_wpe<Ops...>())))
 void k_grouped(GroupArgs<Ops...> g, Ops... ops) {
   warm_kernargs<sizeof(GroupArgs<Ops...>) + (sizeof(Ops) + ...) + 8 * sizeof...(Ops)>();
   __shared__ __attribute__((aligned(16))) float smem[max_lds<Ops...>()];
   int blk = blockIdx.x, i = 0;
+#ifdef DQ_GROUP_PROF
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  ((dispatch_prof(ops, g.nblocks[i], blk, smem, i, t0) || (++i, false)) || ...);
+#else
   ((dispatch(ops, g.nblocks[i++], blk, smem)) || ...);
+#endif
 }
 
 // Launch context: a dry run only sizes the workspace, so the two can never disagree.
@@ -1605,6 +1777,7 @@ int dq_cnn_backward_peer(const dq_cnn_params* p, const dq_cnn_params* g, int32_t
   for (int q = 0; q < P.world; ++q)
     DQ_CHECK_ARG(P.grad[q] && P.param[q] && P.flags[q], "peer: null rank buffer");
   DQ_CHECK_ARG(P.max_polls > 0, "peer: max_polls must be positive");
+  DQ_CHECK_ARG(P.xcds >= 0 && P.xcds <= 8, "peer: 0 <= xcds <= 8");
   RiderDesc r[5];
   for (int i = 0; i < n_riders; ++i) {
     memcpy(&r[i], &riders[i], sizeof(RiderDesc));
@@ -1635,6 +1808,7 @@ static int check_peer(const dq_peer* peer, const float* var) {
   for (int q = 0; q < P.world; ++q)
     DQ_CHECK_ARG(P.grad[q] && P.param[q] && P.flags[q], "peer: null rank buffer");
   DQ_CHECK_ARG(P.max_polls > 0, "peer: max_polls must be positive");
+  DQ_CHECK_ARG(P.xcds >= 0 && P.xcds <= 8, "peer: 0 <= xcds <= 8");
   return DQ_OK;
 }
 
@@ -1647,6 +1821,35 @@ int dq_peer_all_gather(const dq_peer* peer, float* var, void* stream) {
     group(c, AgParts{peer, var}.part(0), AgParts{peer, var}.part(1), AgParts{peer, var}.part(2));
   }
   DQ_CHECK_LAUNCH("dq_peer_all_gather");
+  return DQ_OK;
+}
+
+#ifdef DQ_GROUP_PROF
+// the grouped launches' stamp ring (tools/group_stamps.py): reset the counter; read it back
+int dq_debug_group_reset(void) {
+  const unsigned z = 0;
+  return hipMemcpyToSymbol(HIP_SYMBOL(dq::cnn::g_grp_n), &z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+int dq_debug_group_read(void* recs, unsigned* n_out, unsigned* cap_out) {
+  *cap_out = dq::cnn::kGrpRecs;
+  if (hipMemcpyFromSymbol(n_out, HIP_SYMBOL(dq::cnn::g_grp_n), sizeof(unsigned)) != hipSuccess)
+    return -1;
+  return hipMemcpyFromSymbol(recs, HIP_SYMBOL(dq::cnn::g_grp_rec), sizeof(dq::cnn::g_grp_rec)) ==
+                 hipSuccess ? 0 : -1;
+}
+#endif
+
+int dq_peer_selftest(const dq_peer* peer, uint32_t tag, int32_t* mismatches_out, void* stream) {
+  DQ_CHECK_ARG(peer && mismatches_out, "null argument");
+  const dq_peer& P = *peer;
+  const int rc = check_peer(peer, P.param[P.rank]);
+  if (rc != DQ_OK) return rc;
+  DQ_CHECK_ARG(P.n % 4 == 0 && P.n / 4 < (int64_t)1 << 27, "peer: n % 4 == 0, buffers < 2 GB");
+  Ctx c{(hipStream_t)stream, nullptr, false, 0};
+  group(c, SelfTestFillOp{P, tag, 2048});                      // 8 blocks per CU, every XCD
+  group(c, PeerPubOp{P, kPeerTest});
+  group(c, SelfTestCheckOp{P, tag, mismatches_out, kPeerMaxBlocks});
+  DQ_CHECK_LAUNCH("dq_peer_selftest");
   return DQ_OK;
 }
 

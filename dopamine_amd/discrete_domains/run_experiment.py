@@ -145,7 +145,27 @@ class Runner(object):
     self._environment = settings['create_environment_fn']()
     self._sess = None
     self._agent = create_agent_fn(self._sess, self._environment, summary_writer=None)
+    self._refuse_exchanging_learners()
     self._initialize_checkpointer_and_maybe_resume(settings['checkpoint_file_prefix'])
+
+  def _refuse_exchanging_learners(self):
+    """Data-parallel learners (a DQNAgent family agent with a process group) exchange their
+    gradients at EVERY gradient step, so every rank must take the same gradient steps in the
+    same order.  The Runner's phases run whole episodes per rank (run_experiment.py:319-383),
+    and each rank's episodes, and its replay's add_count gate (dqn_agent.py:418-442), differ,
+    so its ranks would take different gradient steps per phase: a waiting rank times out
+    (peer exchange) or pairs its collective with another kind (all-reduce).  Data-parallel
+    learners train through the learner-only loop (DQNAgent.train_gradient_steps, bench.py);
+    the Runner keeps per-rank checkpoints for agents that exchange nothing."""
+    if getattr(self._agent, 'exchange', None) is None or self._process_group() is None:
+      return
+    import torch.distributed as dist
+    if dist.get_world_size(self._process_group()) > 1 or getattr(self._agent, '_peer', None):
+      raise ValueError('Runner: data-parallel learners (process_group with %d ranks, exchange=%r) '
+                       'exchange gradients every gradient step, which whole-episode phases '
+                       'cannot keep in step across ranks; train them with '
+                       'train_gradient_steps (the learner-only loop)'
+                       % (dist.get_world_size(self._process_group()), self._agent.exchange))
 
   # ------------------------------------------------------------------ setup
   def _create_directories(self):
@@ -251,11 +271,6 @@ class Runner(object):
     return episodes, average
 
   def _run_train_phase(self, statistics):
-    # data-parallel learners over the peer exchange leave their evaluation phases apart:
-    # they meet on the host before the phase's first exchange step (a no-op otherwise)
-    resync = getattr(self._agent, 'resync_exchange', None)
-    if resync is not None:
-      resync()
     return self._phase(statistics, 'train', self._training_steps, eval_mode=False)
 
   def _run_eval_phase(self, statistics):
@@ -298,6 +313,10 @@ class Runner(object):
       statistics = self._run_one_iteration(iteration)
       self._log_experiment(iteration, statistics)
       self._checkpoint_experiment(iteration)
+    # the learner's device resources (communicators, peer mappings; a no-op for one replica)
+    close = getattr(self._agent, 'close', None)
+    if close is not None:
+      close()
 
 
 class TrainRunner(Runner):

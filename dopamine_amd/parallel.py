@@ -193,10 +193,17 @@ class PeerExchange(object):
   floats that joins the conv bucket); every rank keeps the Adam moments of its own slice
   only (ZeRO-1: DQNAgent._gather_opt_state gathers them for a checkpoint).  group None: one
   learner running the same protocol with itself (world 1).  Requires every learner on one
-  node with peer access between their devices (``available``)."""
+  node with peer access between their devices (``available``).
+
+  Construction ends with a self-test of the exchange's memory path (dq_peer_selftest): every
+  rank stores a pattern over its gradient buffer from every XCD, publishes it through the
+  product publication, and reads every rank's buffer through the exchange's loads.  Any
+  mismatched word, timeout or short XCD coverage on any rank raises RuntimeError on every
+  rank (the ranks agree), so a learner never trains over an exchange that reads stale memory."""
 
   MAX_POLLS = 30_000_000     # per wait (~1-2 us per poll): a dead peer latches an error in < 1 min,
   # a live one may lag by tens of seconds (first-use code loads, host noise) without one
+  SELFTEST_POLLS = 30_000_000   # the self-test's wait, whatever max_polls the exchange uses
 
   def __init__(self, group, device, grad, params, lo, n, max_polls=None):
     from dopamine_amd import _lib
@@ -204,14 +211,17 @@ class PeerExchange(object):
     self.group = group
     self.world = 1 if group is None else dist.get_world_size(group)
     self.rank = 0 if group is None else dist.get_rank(group)
+    self.device = torch.device(device)
     assert self.world <= _lib.PEER_MAX, 'the peer exchange holds at most %d ranks' % _lib.PEER_MAX
     assert lo % 4 == 0 and (n - lo) % (4 * self.world) == 0
     self.lo, self.n = int(lo), int(n)
     self.flags = torch.zeros(_lib.PEER_FLAG_WORDS, dtype=torch.int64, device=device)
+    self._grad = grad
     self._opened = []
     bufs = (grad, params, self.flags)
     ptrs = [[0] * 3 for _ in range(self.world)]
     ptrs[self.rank] = [b.data_ptr() for b in bufs]
+    tag = int.from_bytes(os.urandom(4), 'little')
     if self.world > 1:
       mine = []
       for b in bufs:
@@ -219,7 +229,8 @@ class PeerExchange(object):
         _lib.call('dq_peer_ipc_get', ctypes.c_void_p(b.data_ptr()), ctypes.byref(h))
         mine.append(bytes(ctypes.string_at(ctypes.addressof(h), ctypes.sizeof(h))))
       allh = [None] * self.world
-      dist.all_gather_object(allh, mine, group=group)
+      dist.all_gather_object(allh, (mine, tag), group=group)
+      tag = allh[0][1]                     # group rank 0's self-test tag
       torch.cuda.synchronize(device)
       err = None
       try:
@@ -227,7 +238,7 @@ class PeerExchange(object):
           if q == self.rank:
             continue
           for k in range(3):
-            h = _lib.IpcHandle.from_buffer_copy(allh[q][k])
+            h = _lib.IpcHandle.from_buffer_copy(allh[q][0][k])
             ptr, base = ctypes.c_void_p(), ctypes.c_void_p()
             _lib.call('dq_peer_ipc_open', ctypes.byref(h), ctypes.byref(ptr), ctypes.byref(base))
             self._opened.append(base.value)
@@ -242,22 +253,69 @@ class PeerExchange(object):
         raise RuntimeError('peer exchange: mapping the other learners\' buffers failed: %s'
                            % next(e for e in errs if e is not None))
     d = _lib.Peer(world=self.world, rank=self.rank, lo=self.lo, n=self.n,
-                  max_polls=int(max_polls or self.MAX_POLLS))
+                  max_polls=int(max_polls or self.MAX_POLLS), xcds=xcd_count(device))
     for q in range(self.world):
       d.grad[q], d.param[q], d.flags[q] = ptrs[q]
     self.desc = d
+    self.selftest = self._selftest(tag)
+
+  def _selftest(self, tag):
+    """dq_peer_selftest, the ranks agreeing on the verdict; raises RuntimeError (on every
+    rank) if any rank saw a mismatched word, a timeout or too few XCDs.  Returns the verdict.
+    (DQ_PEER_SKIP_SELFTEST=1 skips it in a diagnostic build only -- so that the replica
+    checks after a bench window can be shown to catch what the self-test would have.)"""
+    L = self._lib
+    if os.environ.get('DQ_PEER_SKIP_SELFTEST') == '1' and L.BUILD_FLAGS:
+      return {'skipped': True, 'build': L.BUILD_FLAGS}
+    out = torch.zeros(1, dtype=torch.int32, device=self.device)
+    t0 = time.perf_counter()
+    d = L.Peer.from_buffer_copy(self.desc)
+    d.max_polls = max(int(d.max_polls), self.SELFTEST_POLLS)
+    L.call('dq_peer_selftest', ctypes.byref(d), ctypes.c_uint32(tag & 0xffffffff),
+           ctypes.c_void_p(out.data_ptr()), L.stream_of(self.device))
+    torch.cuda.synchronize(self.device)
+    mine = {'rank': self.rank, 'mismatched_words': int(out.item()),
+            'error': int(self.flags[L.PEER_ERR].item()),
+            'xcds_seen': int(self.flags[L.PEER_PUB_XCDS].item()), 'xcds_needed': self.desc.xcds,
+            'ms': round(1e3 * (time.perf_counter() - t0), 2)}
+    allv = [mine]
+    if self.group is not None:
+      allv = [None] * self.world
+      dist.all_gather_object(allv, mine, group=self.group)   # every rank's reads are done
+    self._grad.zero_()                 # the pattern leaves this rank's gradient buffer
+    verdict = {'ok': all(v['mismatched_words'] == 0 and v['error'] == 0 for v in allv),
+               'words_per_rank': self.n * self.world, 'ranks': allv}
+    if not verdict['ok']:
+      self.close()
+      bad = [v for v in allv if v['mismatched_words'] or v['error']]
+      raise RuntimeError('peer exchange: the self-test of the exchange\'s memory path failed '
+                         '(%s)' % '; '.join('rank %d: %d stale or wrong words of %d read, %s'
+                                            % (v['rank'], v['mismatched_words'],
+                                               self.n * self.world, self.describe(v['error']))
+                                            for v in bad))
+    return verdict
 
   @staticmethod
   def available(group, device):
-    """Whether every learner of ``group`` can run the exchange: one host, peer access
-    between every pair of their devices.  Collective; every rank gets the same answer."""
+    """Whether every learner of ``group`` can run the exchange: one host, and for every other
+    learner's GPU (identified by its PCI address, not by a process-local ordinal) either the
+    same GPU or one this process sees with peer access to it.  Collective; every rank gets
+    the same answer."""
     import socket
     from dopamine_amd import _lib
-    me = (socket.gethostname(), torch.device(device).index)
+    me = (socket.gethostname(), pci_address(device))
     allm = [None] * dist.get_world_size(group)
     dist.all_gather_object(allm, me, group=group)
     ok = all(h == me[0] for h, _ in allm) and dist.get_world_size(group) <= _lib.PEER_MAX
-    ok = ok and all(int(_lib.lib.dq_peer_can_access(me[1], dv)) == 1 for _, dv in allm)
+    if ok:
+      visible = {pci_address(i): i for i in range(torch.cuda.device_count())}
+      mine = torch.device(device).index or 0
+      for _, addr in allm:
+        if addr == me[1]:
+          continue                       # the same GPU (learners sharing one device)
+        j = visible.get(addr)
+        if j is None or int(_lib.lib.dq_peer_can_access(mine, j)) != 1:
+          ok = False                     # a GPU this process cannot see or map
     flags = [None] * dist.get_world_size(group)
     dist.all_gather_object(flags, bool(ok), group=group)
     return all(flags)
@@ -270,21 +328,65 @@ class PeerExchange(object):
                    stream)
 
   def error(self):
-    """0, or 1 + the flag a wait of this learner timed out on (a synchronising read)."""
+    """0, or the latched error word (a synchronising read; describe())."""
     return int(self.flags[self._lib.PEER_ERR].item())
 
-  def check(self):
+  def describe(self, e):
+    L = self._lib
+    if e == 0:
+      return 'no error'
+    if e >= L.PEER_ERR_XCD:
+      return ('a publication\'s blocks ran on %d XCD(s), fewer than the %d whose L2 write-back '
+              'it needs' % (e - L.PEER_ERR_XCD, self.desc.xcds))
+    if e >= L.PEER_ERR_PEER:
+      return 'rank %d had latched an error, so this one stopped' % (e - L.PEER_ERR_PEER)
+    names = {1 + L.PEER_GRAD: 'gradients', 1 + L.PEER_PARAM: 'parameters',
+             1 + L.PEER_CONV: 'conv gradients', 1 + L.PEER_TEST: 'self-test pattern'}
+    return ('timed out waiting for the other learners\' %s (a learner stopped or fell out of '
+            'step)' % names.get(e, e))
+
+  def check(self, collective=False):
+    """Raises RuntimeError if this learner's error word is latched.  collective: the ranks
+    first agree (MAX all-reduce of the error words over the group), so every rank raises
+    together -- call it at the same point on every rank."""
     e = self.error()
+    worst = e
+    if collective and self.group is not None:
+      t = torch.tensor([e], dtype=torch.int64,
+                       device=self.device if dist.get_backend(self.group) == 'nccl' else 'cpu')
+      dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+      worst = int(t.item())
     if e:
-      names = {1 + self._lib.PEER_GRAD: 'gradients', 1 + self._lib.PEER_PARAM: 'parameters',
-               1 + self._lib.PEER_CONV: 'conv gradients'}
-      raise RuntimeError('peer exchange: rank %d timed out waiting for the other learners\' %s '
-                         '(a learner stopped or fell out of step)' % (self.rank, names.get(e, e)))
+      raise RuntimeError('peer exchange: rank %d: %s' % (self.rank, self.describe(e)))
+    if worst:
+      raise RuntimeError('peer exchange: rank %d: another learner latched an error (%s)'
+                         % (self.rank, self.describe(worst)))
+
+  def wait_counters(self):
+    """This rank's cumulative waits at the three exchange points: {point: (ticks of the
+    100 MHz clock, waits counted)} (block 0 of each waiting op; a synchronising read)."""
+    f = self.flags.cpu().tolist()
+    L = self._lib
+    return {name: (int(f[L.PEER_WAIT_TICKS + i]), int(f[L.PEER_WAIT_COUNT + i]))
+            for i, name in enumerate(('grad', 'param', 'conv'))}
 
   def close(self):
     for base in self._opened:
       self._lib.call('dq_peer_ipc_close', ctypes.c_void_p(base))
     self._opened = []
+
+
+def pci_address(device):
+  """(domain, bus, device) PCI address of a GPU: the same physical GPU has the same address
+  in every process, whatever HIP_VISIBLE_DEVICES numbers it."""
+  p = torch.cuda.get_device_properties(device)
+  return (int(p.pci_domain_id), int(p.pci_bus_id), int(p.pci_device_id))
+
+
+def xcd_count(device):
+  """XCDs of the device (32 CUs each on MI355X: 8 for a whole GPU, 1 in a CPX partition)."""
+  cus = torch.cuda.get_device_properties(device).multi_processor_count
+  return max(1, min(8, cus // 32))
 
 
 # exit status of a process whose deadline expired (Deadline)
@@ -337,6 +439,41 @@ class Deadline(object):
                   'exiting with status %d\n' % (self.rank, label, seconds, DEADLINE_EXIT))
         out.flush()
         os._exit(DEADLINE_EXIT)
+
+
+def replica_report(tensors, group=None):
+  """Collective: every rank compares each of ``tensors`` ({name: tensor}, the same names on
+  every rank) with group rank 0's copy, bit for bit (broadcast, then the elements whose bits
+  differ).  Returns {name: {'in_sync': bool, 'differing': [elements differing from rank 0's,
+  per group rank], 'max_abs_diff': [per group rank]}} -- the same dict on every rank."""
+  nccl = dist.get_backend(group) == 'nccl'
+  src = dist.get_process_group_ranks(group)[0] if group is not None else 0
+  world = dist.get_world_size(group)
+  rows = []
+  for name in sorted(tensors):
+    x = tensors[name].detach().contiguous().reshape(-1)
+    if not nccl:
+      x = x.cpu()
+    ref = x.clone()
+    dist.broadcast(ref, src=src, group=group)
+    ib = {4: torch.int32, 8: torch.int64}[x.element_size()]
+    diff = x.view(ib) != ref.view(ib)
+    n = int(diff.sum().item())
+    mad = 0.0
+    if n:
+      d = (x.double() - ref.double()).abs()
+      mad = float(torch.nan_to_num(d, nan=float('inf')).max().item())
+    rows.append((n, mad))
+  t = torch.tensor([v for r in rows for v in r], dtype=torch.float64,
+                   device=torch.device('cuda', torch.cuda.current_device()) if nccl else 'cpu')
+  parts = [torch.empty_like(t) for _ in range(world)]
+  dist.all_gather(parts, t, group=group)
+  out = {}
+  for i, name in enumerate(sorted(tensors)):
+    n = [int(p[2 * i].item()) for p in parts]
+    m = [float(p[2 * i + 1].item()) for p in parts]
+    out[name] = {'in_sync': not any(n), 'differing': n, 'max_abs_diff': m}
+  return out
 
 
 def replicas_in_sync(flat_params, group=None):

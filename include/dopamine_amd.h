@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define DQ_ABI_VERSION 8
+#define DQ_ABI_VERSION 9
 
 /* host-side return codes */
 #define DQ_OK 0
@@ -600,11 +600,15 @@ int dq_comm_version(void);
  *             the step counter flags[0] += 1 by the launch's last block.
  * No collective library, no second queue, no graph fork or join.  Remote loads are
  * system-coherent (sc0 sc1) behind an acquire; a flag is stored by the last of 16 blocks
- * that each wrote back their XCD's L2 behind a system release (counted in flags[6]); every
- * wait is bounded (max_polls) and a timeout latches flags[4] (DQ_PEER_FLAG_WORDS words per
- * rank, zero-initialised; flags[0] = the step counter, equal on every rank). */
+ * that each wrote back their XCD's L2 behind a system release (counted per XCD in flags[6],
+ * read from HW_REG_XCC_ID; a publication whose blocks ran on fewer than `xcds` XCDs latches an
+ * error instead of publishing); every wait is bounded (max_polls), polls every rank's error
+ * word too, and a timeout or another rank's error latches flags[4], after which the rank
+ * publishes nothing (DQ_PEER_FLAG_WORDS words per rank, zero-initialised; flags[0] = the
+ * step counter, equal on every rank; flags[8..10] / [11..13]: 100 MHz ticks waited / waits
+ * counted at the grad / param / conv points; flags[14]: XCDs seen by the last publication). */
 #define DQ_PEER_MAX 8
-#define DQ_PEER_FLAG_WORDS 8
+#define DQ_PEER_FLAG_WORDS 16
 typedef struct dq_ipc_handle {
   uint8_t handle[64];             /* hipIpcMemHandle_t of the allocation holding the pointer */
   int64_t offset;                 /* the pointer's byte offset in that allocation */
@@ -623,6 +627,8 @@ typedef struct dq_peer {
   float* param[DQ_PEER_MAX];      /* rank q's flat parameters */
   uint64_t* flags[DQ_PEER_MAX];   /* rank q's DQ_PEER_FLAG_WORDS flag words */
   int64_t max_polls;              /* per wait; then flags[4] := 1 + which flag timed out */
+  int32_t xcds;                   /* XCDs a publication's blocks must cover (0: unchecked) */
+  int32_t reserved;
 } dq_peer;
 /* dq_cnn_backward_riders of the fused Rainbow schedule (head_from 6, first 1, last 7, TF1
    Adam) with the exchange above in place of the fused optimizer's fc / conv updates: the
@@ -643,6 +649,16 @@ int dq_cnn_forward_fused_peer(const dq_cnn_params* p0, const float* x0, dq_cnn_a
                               int32_t batch, int32_t fc1_1, const dq_peer* peer, float* var,
                               void* stream);
 int dq_peer_all_gather(const dq_peer* peer, float* var, void* stream);
+/* The construction-time check of the exchange's memory path (no reference counterpart: it
+   guards config 4's data-parallel learners).  Three launches on `stream`: every
+   workgroup of a full grid stores a (rank, tag)-keyed pattern over this rank's whole flat
+   gradient buffer grad[rank][0, n) with plain stores (dirty lines in every XCD's L2, as the
+   backward's epilogues leave them); the product publication (peer_publish_xcd) raises flags[7];
+   every rank waits for every rank's flags[7] and reads every rank's buffer through the
+   exchange's system-coherent loads, adding the words that differ from that rank's pattern to
+   *mismatches_out (a device int32, zeroed by the caller).  A timeout latches flags[4].  The
+   pattern is left in the gradient buffers: the caller zeroes its own once every rank is done. */
+int dq_peer_selftest(const dq_peer* peer, uint32_t tag, int32_t* mismatches_out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -112,3 +112,80 @@ def iqn_masks(ex):
 def to_input(x_float32_nhwc):
   """The network input the reference computes in fp32 (uint8 / 255.), as float64."""
   return torch.as_tensor(np.asarray(x_float32_nhwc), dtype=torch.float32).double()
+
+
+# ----------------------------------------------------------- Σ|terms| of every gradient
+# The conditioning of a gradient element: the float64 sum of the absolute values of the
+# terms its final reduction adds -- |dz| |x| over the batch (and positions) for a weight,
+# |dz| for a bias, with dz the float64 gradient of the layer's pre-activation.  A bias
+# gradient that sums 441 B positions of both signs can be far below its terms, and its fp32
+# sum is then accurate to u times the terms, not to u times itself.  Tests compare
+# |g_device - g_float64| with this sum element by element.
+_CONVS = (('conv1', (2, 2, 2, 2), 4, 'a1'), ('conv2', (1, 2, 1, 2), 2, 'a2'),
+          ('conv3', (1, 1, 1, 1), 1, 'a3'))
+
+
+def _layers(P, x_nhwc, masks, rec):
+  """The Nature-CNN torso as forward()/torso(), recording each layer's (name, kind, input,
+  pre-activation) in rec (the pre-activations retain their gradients)."""
+  x = x_nhwc.permute(0, 3, 1, 2)
+  for name, pad, st, act in _CONVS:
+    xi = F.pad(x, pad)
+    z = F.conv2d(xi, P[name + '_w'], P[name + '_b'], stride=st)
+    z.retain_grad()
+    rec.append((name, ('conv', st), xi, z))
+    x = _relu(z, masks, act, True)
+  return x.permute(0, 2, 3, 1).reshape(x.shape[0], -1)
+
+
+def _linear(P, name, x, rec):
+  z = F.linear(x, P[name + '_w'], P[name + '_b'])
+  z.retain_grad()
+  rec.append((name, ('fc',), x, z))
+  return z
+
+
+def _abs_sums(P, rec):
+  """Σ|terms| of each recorded layer's weight and bias gradients, in the flat layout."""
+  g = torch.zeros(P.numel, dtype=torch.float64)
+  for name, kind, xi, z in rec:
+    dz = z.grad.detach().abs()
+    ax = xi.detach().abs()
+    w = P[name + '_w'].detach().clone().requires_grad_(True)
+    t = F.conv2d(ax, w, stride=kind[1]) if kind[0] == 'conv' else F.linear(ax, w)
+    t.backward(dz)
+    gw = w.grad.permute(0, 2, 3, 1) if kind[0] == 'conv' else w.grad
+    gb = dz.sum(dim=(0, 2, 3)) if kind[0] == 'conv' else dz.sum(0)
+    for suf, v in (('_w', gw), ('_b', gb)):
+      o, shape = P.offsets[name + suf]
+      g[o:o + v.numel()] = v.reshape(-1)
+  return g.numpy()
+
+
+def abs_grad(P, x_nhwc, masks, gout):
+  """(flat float64 gradient, flat Σ|terms| of it) for forward(P, x, masks) and the loss
+  gradient gout (B, n_out); P: fresh Params64 leaves.  masks: the device's activations (the
+  ReLU decisions are the device's)."""
+  rec = []
+  h = _relu(_linear(P, 'fc1', _layers(P, x_nhwc, masks, rec), rec), masks, 'h')
+  out = _linear(P, 'fc2', h, rec)
+  out.backward(torch.as_tensor(np.asarray(gout), dtype=torch.float64))
+  return P.flat_grad(), _abs_sums(P, rec)
+
+
+def iqn_abs_grad(P, x_nhwc, taus, masks, gout):
+  """abs_grad for iqn_forward (rows q B + b; masks a1, a2, a3, emb, h); the Hadamard
+  product's own sum (over the N tiled rows of each state) is the fc1 gradient's reduction."""
+  rec = []
+  state = _layers(P, x_nhwc, masks, rec)
+  B = state.shape[0]
+  nq = taus.shape[0] // B
+  E = P['emb_w'].shape[1]
+  tiled = state.repeat(nq, 1)
+  i_pi = (torch.arange(1, E + 1, dtype=torch.float32) * torch.tensor(math.pi, dtype=torch.float32))
+  emb_in = torch.cos((taus.to(torch.float32).reshape(-1, 1) * i_pi).double())
+  emb = _relu(_linear(P, 'emb', emb_in, rec), masks, 'emb')
+  h = _relu(_linear(P, 'fc1', tiled * emb, rec), masks, 'h')
+  out = _linear(P, 'fc2', h, rec)
+  out.backward(torch.as_tensor(np.asarray(gout), dtype=torch.float64))
+  return P.flat_grad(), _abs_sums(P, rec)

@@ -162,7 +162,11 @@ def test_product_sources_carry_only_the_bf16_build_switches():
   """the rejected A/B knobs and the result-dropping ablations are gone from
   the product sources; the compile-time switches left are the bf16 throughput build's two
   (dopamine_amd/_build.py BF16_FLAGS).  #ifdef DQ_C51_PROF / DQ_GATHER_PROF are stamp
-  builds (they write timing words to buffers of their own, never results)."""
+  builds, as DQ_GROUP_PROF (they write timing words to buffers of their own, never results);
+  DQ_PEER_DROP_XCD_FENCE / DQ_PEER_HIDE_XCD / DQ_PEER_FAULT_REPLICA are fault injections for the peer exchange's
+  checks (a variant that drops one XCD's write-back must be reported as a
+  failed schedule), built only by tools/build_variant.py; _lib loads such a library only with
+  DQ_DIAGNOSTIC_BUILD=1."""
   csrc = os.path.join(ROOT, 'dopamine_amd', 'csrc')
   knobs, ifdefs = set(), set()
   for f in os.listdir(csrc):
@@ -170,4 +174,5 @@ def test_product_sources_carry_only_the_bf16_build_switches():
     knobs |= set(re.findall(r'^#ifndef (DQ_\w+)', src, re.M))
     ifdefs |= set(re.findall(r'^#if(?:def)?\s+(DQ_\w+)', src, re.M))
   assert knobs == {'DQ_CNN_X6', 'DQ_X6_PAIRS'}, knobs
-  assert ifdefs <= {'DQ_C51_PROF', 'DQ_GATHER_PROF', 'DQ_BUILD_FLAGS'}, ifdefs
+  assert ifdefs <= {'DQ_C51_PROF', 'DQ_GATHER_PROF', 'DQ_GROUP_PROF', 'DQ_BUILD_FLAGS',
+                    'DQ_PEER_DROP_XCD_FENCE', 'DQ_PEER_HIDE_XCD', 'DQ_PEER_FAULT_REPLICA'}, ifdefs

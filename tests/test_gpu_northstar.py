@@ -267,7 +267,16 @@ LONG_PARAM_ATOL = 1e-6  # fp32 updates vs the float64 trajectory after 1,000 ste
 # the conv gradients are sums over B x 441 (conv1) positions that cancel to a small fraction
 # of their terms, more so as training proceeds: measured 2.2e-5 (conv1_b) at step 900 against
 # 1e-5 in the first 13 (north_star's 1e-5 bar is on Q-values and losses, which stay at 1e-6)
-LONG_GRAD_TOL = 1e-4
+# Gradients over the long horizons: each element's error against the float64 gradient on the
+# device's ReLU decisions, relative to the float64 sum of the ABSOLUTE terms of its final
+# reduction (oracle/nature_cnn.abs_grad: |dz| |x| summed over batch and positions for a
+# weight, |dz| for a bias), element by element -- what fp32 summation can promise whatever
+# the cancellation (conv1_b sums 441 B positions of both signs; relative to the tensor's max
+# |g| it read up to 2.2e-5, round 5).  The bar is GRAD_TOL's 1e-5 on that measure; the
+# max-|g|-relative figure is still printed ('grad').
+def _cond(got, ref, abs_terms):
+  got, ref = np.asarray(got, np.float64), np.asarray(ref, np.float64)
+  return float((np.abs(got - ref) / np.maximum(np.asarray(abs_terms, np.float64), 1e-30)).max())
 
 
 @pytest.mark.timeout(900)
@@ -307,8 +316,8 @@ def test_bench_path_long_horizon(kind):
   if prioritized:
     support = agent._support.cpu().double().numpy()
     N = support.shape[0]
-  errs = dict(logits=0.0, loss=0.0, priorities=0.0, grad={}, params=0.0, checks=0, chunks=0,
-              single=0, syncs=0)
+  errs = dict(logits=0.0, loss=0.0, priorities=0.0, grad={}, grad_cond={}, params=0.0, checks=0,
+              chunks=0, single=0, syncs=0)
   done = 0
 
   def step(slot, full):
@@ -325,7 +334,8 @@ def test_bench_path_long_horizon(kind):
     if full:
       masks = {k: tr['act_' + k] for k in ('a1', 'a2', 'a3', 'h')}
       P = ONC.Params64(w, offsets)
-      out = ONC.forward(P, ONC.to_input(np.moveaxis(x, 1, -1)), masks)
+      xin = ONC.to_input(np.moveaxis(x, 1, -1))
+      out = ONC.forward(P, xin, masks)
       tout = tr['target_out'].astype(np.float64)
       if prioritized:
         ref = OL.c51_loss(out.detach().numpy().reshape(B, A, N), tout.reshape(B, A, N), b[1],
@@ -338,11 +348,12 @@ def test_bench_path_long_horizon(kind):
         gout = ref['grad']
       errs['logits'] = max(errs['logits'], _rel(tr['online_out'], out.detach().numpy()))
       errs['loss'] = max(errs['loss'], _rel(tr['loss'], ref['loss']))
-      out.backward(torch.from_numpy(gout))
-      g = P.flat_grad()
+      g, ga = ONC.abs_grad(ONC.Params64(w, offsets), xin, masks, gout)
       for name, (o, shape) in offsets.items():
         n = int(np.prod(shape))
         errs['grad'][name] = max(errs['grad'].get(name, 0.0), _rel(tr['grad'][o:o + n], g[o:o + n]))
+        errs['grad_cond'][name] = max(errs['grad_cond'].get(name, 0.0),
+                                      _cond(tr['grad'][o:o + n], g[o:o + n], ga[o:o + n]))
       errs['checks'] += 1
     opt.step(w, tr['grad'].astype(np.float64))
     if prioritized:
@@ -378,7 +389,7 @@ def test_bench_path_long_horizon(kind):
   print(json.dumps({'northstar_long_horizon': kind, **errs}), flush=True)
   assert errs['syncs'] >= 9 and errs['chunks'] >= 200, errs
   assert errs['logits'] <= Q_TOL and errs['loss'] <= Q_TOL and errs['priorities'] <= Q_TOL, errs
-  assert max(errs['grad'].values()) <= LONG_GRAD_TOL, errs
+  assert max(errs['grad_cond'].values()) <= GRAD_TOL, errs
   assert errs['params'] <= LONG_PARAM_ATOL, errs
 
 
@@ -594,7 +605,7 @@ def test_iqn_breakout_long_horizon():
   opt = _Adam64(agent._opt, k0)
   orc = _oracle_replay(agent, True)
   cg = np.float64(np.float32(agent.cumulative_gamma))
-  errs = dict(q=0.0, loss=0.0, dq=0.0, grad={}, params=0.0, checks=0, syncs=0)
+  errs = dict(q=0.0, loss=0.0, dq=0.0, grad={}, grad_cond={}, params=0.0, checks=0, syncs=0)
   for s in range(IQN_LONG_STEPS):
     syncs = agent.training_steps // agent.target_update_period
     full = s % 100 == 0
@@ -623,11 +634,13 @@ def test_iqn_breakout_long_horizon():
       errs['q'] = max(errs['q'], _rel(tr['qv'], q.detach().numpy()))
       errs['loss'] = max(errs['loss'], _rel(tr['loss'], ref['loss']))
       errs['dq'] = max(errs['dq'], _rel(tr['grad_out'], ref['grad']))
-      q.backward(torch.from_numpy(ref['grad']))
-      g = P.flat_grad()
+      g, ga = ONC.iqn_abs_grad(ONC.Params64(w, offsets), ONC.to_input(np.moveaxis(x, 1, -1)),
+                               torch.from_numpy(tr['taus']).double(), masks, ref['grad'])
       for name, (o, shape) in offsets.items():
         n = int(np.prod(shape))
         errs['grad'][name] = max(errs['grad'].get(name, 0.0), _rel(tr['grad'][o:o + n], g[o:o + n]))
+        errs['grad_cond'][name] = max(errs['grad_cond'].get(name, 0.0),
+                                      _cond(tr['grad'][o:o + n], g[o:o + n], ga[o:o + n]))
       errs['checks'] += 1
       print('iqn long horizon: %d steps' % s, flush=True)   # progress (a quiet run looks hung)
     opt.step(w, tr['grad'].astype(np.float64))
@@ -638,5 +651,5 @@ def test_iqn_breakout_long_horizon():
   print(json.dumps({'northstar_long_horizon': 'iqn', **errs}), flush=True)
   assert errs['syncs'] >= 4 and errs['checks'] == 5, errs
   assert errs['q'] <= Q_TOL and errs['loss'] <= Q_TOL and errs['dq'] <= Q_TOL, errs
-  assert max(errs['grad'].values()) <= LONG_GRAD_TOL, errs
+  assert max(errs['grad_cond'].values()) <= GRAD_TOL, errs
   assert errs['params'] <= LONG_PARAM_ATOL, errs

@@ -28,7 +28,7 @@ LOOP_STEPS = 24
 
 
 def _peer_worker(rank, world, port, q, loop, same_seed=False, idle_rank=-1, max_polls=None,
-                 n_steps=None):
+                 n_steps=None, stall=None):
   import sys
   sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
   import torch.distributed as dist
@@ -37,7 +37,7 @@ def _peer_worker(rank, world, port, q, loop, same_seed=False, idle_rank=-1, max_
   torch.cuda.set_device(0)
   dist.init_process_group('gloo', rank=rank, world_size=world)
   from dopamine_amd import parallel
-  if max_polls is not None:
+  if max_polls is not None and (stall is None or rank == stall[1]):
     parallel.PeerExchange.MAX_POLLS = max_polls
   agent = _agent(dist.group.WORLD, 0 if same_seed else rank,
                  net_seed=0 if same_seed else 1000 * rank, exchange='peer')
@@ -46,6 +46,32 @@ def _peer_worker(rank, world, port, q, loop, same_seed=False, idle_rank=-1, max_
     q.put((rank, 'idle'))
     dist.barrier()          # the others' host barrier before their first exchange step
     dist.barrier()          # and their closing one
+    dist.destroy_process_group()
+    return
+  if stall is not None:
+    # rank stall[0] sleeps between two gradient steps; rank stall[1] (short max_polls) times
+    # out waiting for it, latches its error and publishes nothing more
+    import time
+    t0 = time.time()
+    for i in range(4):
+      if rank == stall[0] and i == 2:
+        time.sleep(3.0)
+      for _ in range(agent.update_period):
+        agent._train_step()
+    torch.cuda.synchronize()
+    t1 = time.time()
+    try:
+      agent.mean_loss()
+      msg = None
+    except RuntimeError as e:
+      msg = str(e)
+    try:
+      agent.check_exchange(collective=True)
+      cmsg = None
+    except RuntimeError as e:
+      cmsg = str(e)
+    q.put((rank, msg, cmsg, agent._peer.error(), t1 - t0))
+    dist.barrier()
     dist.destroy_process_group()
     return
   try:
@@ -66,12 +92,16 @@ def _peer_worker(rank, world, port, q, loop, same_seed=False, idle_rank=-1, max_
                                        for k in agent._graph_sets), list(agent._graph_sets)
   ok = parallel.replicas_in_sync(agent.online_convnet.fp.flat)
   ok = ok and parallel.replicas_in_sync(agent.target_convnet.fp.flat)
-  agent._gather_opt_state()         # every slice's moments, as a checkpoint sees them
+  rep = agent.replica_report()      # gathers every slice's moments, as a checkpoint sees them
   ok = ok and parallel.replicas_in_sync(agent._opt.m) and parallel.replicas_in_sync(agent._opt.v)
+  ok = ok and all(v['in_sync'] for v in rep.values())
   st = agent._opt.state.cpu().numpy()
   if rank == 0:
     q.put((rank, ok, flat.numpy(), agent._opt.m.cpu().numpy(), agent._opt.v.cpu().numpy(), st,
-           int(agent._peer.flags[0].item()), err))
+           int(agent._peer.flags[0].item()), err,
+           {'selftest': agent._peer.selftest, 'waits': agent._peer.wait_counters(),
+            'replicas': sorted(rep), 'xcds': agent._peer.desc.xcds,
+            'pub_xcds': int(agent._peer.flags[agent._peer._lib.PEER_PUB_XCDS].item())}))
   agent.close()
   dist.barrier()
   dist.destroy_process_group()
@@ -89,7 +119,7 @@ def _spawn(world, loop, **kw):
   import queue
   import time
   try:
-    want = world if kw.get('idle_rank', -1) >= 0 else 1
+    want = world if kw.get('idle_rank', -1) >= 0 or kw.get('stall') else 1
     t0 = time.time()
     while len(res) < want and time.time() - t0 < 400:
       try:
@@ -112,7 +142,7 @@ def test_peer_world1_equals_single_learner_bitwise(loop):
   run against the learner itself -- bitwise the single learner (parameters, moments, beta
   powers), and the step counter counts the gradient steps."""
   res, codes = _spawn(1, loop)
-  _, ok, flat, m, v, st, steps, _ = res[0]
+  _, ok, flat, m, v, st, steps, _, info = res[0]
   assert codes == [0] and ok
   single = _agent(None, 0)
   sflat = _run(single, loop).numpy()
@@ -131,11 +161,21 @@ def test_peer_two_ranks_equal_mean_gradient_reference(loop):
   TF1 Adam reference; the replicas stay bit-identical."""
   n = LOOP_STEPS if loop else STEPS
   res, codes = _spawn(2, loop, n_steps=n)
-  _, ok, flat, m, v, st, steps, _ = res[0]
+  _, ok, flat, m, v, st, steps, _, info = res[0]
   assert codes == [0, 0] and ok and steps == n
   ref, rm, rv = _mean_gradient_reference(loop, moments=True, n_steps=n)
   assert np.array_equal(flat, ref)
   assert np.array_equal(m, rm) and np.array_equal(v, rv)
+  # VERDICT r5 item 1: the construction-time self-test passed on both ranks, every publication
+  # covered every XCD, and the wait counters counted each exchange point's waits
+  st = info['selftest']
+  assert st['ok'] and [r['mismatched_words'] for r in st['ranks']] == [0, 0], st
+  assert [r['xcds_seen'] for r in st['ranks']] == [info['xcds']] * 2 and info['xcds'] == 8, info
+  assert info['pub_xcds'] == 8
+  w = info['waits']
+  assert w['grad'][1] == 2 * n and w['conv'][1] == n and w['param'][1] >= n, w
+  assert sorted(info['replicas']) == ['online', 'opt_m', 'opt_state', 'opt_v', 'target']
+  print('selftest', st, 'waits', w)
 
 
 @pytest.mark.timeout(900)
@@ -146,7 +186,7 @@ def test_peer_world_n_equal_mean_gradient_reference(world):
   config 4's): bitwise the mean-gradient TF1 Adam reference, parameters and gathered
   moments."""
   res, codes = _spawn(world, True, n_steps=LOOP_STEPS)
-  _, ok, flat, m, v, st, steps, _ = res[0]
+  _, ok, flat, m, v, st, steps, _, info = res[0]
   assert codes == [0] * world
   assert steps == LOOP_STEPS, steps
   ref, rm, rv = _mean_gradient_reference(True, moments=True, world=world, n_steps=LOOP_STEPS)
@@ -167,3 +207,20 @@ def test_peer_wait_times_out_instead_of_hanging():
   assert by_rank[1][1] == 'idle'
   assert by_rank[0][1] == 'error' and 'timed out' in by_rank[0][2], by_rank[0]
   assert codes == [0, 0]
+
+
+@pytest.mark.timeout(600)
+def test_peer_error_on_one_rank_stops_every_rank():
+  """ADVICE r5: rank 1 (short max_polls) times out while rank 0 sleeps between two steps;
+  rank 1 latches its error and publishes nothing more, and rank 0, once it resumes, finds
+  rank 1's error word while waiting (within 64 polls, not after its own max_polls) and gives
+  up too.  Each rank's local check names its cause; the collective check raises on both."""
+  res, codes = _spawn(2, False, max_polls=20000, stall=(0, 1))
+  by_rank = {r[0]: r[1:] for r in res}
+  msg0, cmsg0, e0, dt0 = by_rank[0]
+  msg1, cmsg1, e1, dt1 = by_rank[1]
+  assert codes == [0, 0]
+  assert 2 <= e1 <= 4 and 'timed out' in msg1, by_rank[1]
+  assert e0 == 16 + 1 and 'rank 1 had latched an error' in msg0, by_rank[0]
+  assert dt0 < 30, dt0            # rank 0 gave up at once (its own bound is ~1 min)
+  assert cmsg0 and cmsg1

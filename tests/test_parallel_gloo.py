@@ -349,3 +349,99 @@ def test_two_rank_runner_checkpoints_are_per_rank_and_resume_together(tmp_path):
   assert res2[0][0] == 2 and res2[1][0] == 2
   logs = sorted(os.listdir(os.path.join(base, 'logs')))
   assert logs and all(f.startswith('log_') for f in logs)
+
+
+# ------------------------------------------------- replica verdict of the N > 1 bench
+def _replica_worker(rank, world, port, q):
+  os.environ['MASTER_ADDR'] = '127.0.0.1'
+  os.environ['MASTER_PORT'] = str(port)
+  dist.init_process_group('gloo', rank=rank, world_size=world)
+  from dopamine_amd import parallel
+  g = torch.Generator().manual_seed(3)
+  a = torch.randn(1000, generator=g)
+  b = torch.randn(333, generator=g).double()
+  same = parallel.replica_report({'online': a, 'opt_state': b})
+  a2 = a.clone()
+  if rank == 1:
+    a2[417] = float('nan')        # a diverged replica (NaN-safe: bits compared, not values)
+    a2[5] += 1e-7
+  diverged = parallel.replica_report({'online': a2, 'opt_state': b})
+  q.put((rank, same, diverged))
+  dist.barrier()
+  dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_replica_report_finds_a_diverged_replica_bit_for_bit():
+  """after each N > 1 schedule's window bench.py compares every replicated
+  tensor with group rank 0's bit for bit; a replica that differs in two elements (one of them a
+  NaN) is reported on every rank with its per-rank counts."""
+  ctx = mp.get_context('spawn')
+  q = ctx.Queue()
+  port = _free_port()
+  procs = [ctx.Process(target=_replica_worker, args=(r, 2, port, q)) for r in range(2)]
+  for p in procs:
+    p.start()
+  res = dict((r, rest) for r, *rest in (q.get(timeout=120) for _ in range(2)))
+  for p in procs:
+    p.join(timeout=60)
+    assert p.exitcode == 0
+  for r in (0, 1):
+    same, diverged = res[r]
+    assert all(v['in_sync'] and v['differing'] == [0, 0] for v in same.values())
+    assert not diverged['online']['in_sync'] and diverged['online']['differing'] == [0, 2]
+    assert diverged['online']['max_abs_diff'][1] == float('inf')
+    assert diverged['opt_state']['in_sync']
+
+
+def test_bench_headline_skips_failed_and_diverged_schedules():
+  """bench.py's headline is the fastest schedule that ran with its replicas in sync: a faster
+  schedule whose replicas diverged (or that failed on a rank) is never the headline."""
+  import bench
+  s = {'peer': {'value': 9.0, 'error': 'replicas diverged: ...', 'replicas_in_sync': False},
+       'allreduce': {'value': 6.0, '_elapsed': 2.0, 'replicas_in_sync': True},
+       'zero1': {'error': 'failed on another rank'}}
+  assert bench.pick_headline(s) == 'allreduce'
+  s['peer'] = {'value': 9.0, '_elapsed': 1.0, 'replicas_in_sync': True}
+  assert bench.pick_headline(s) == 'peer'
+  with pytest.raises(RuntimeError):
+    bench.pick_headline({'peer': {'error': 'x'}})
+
+
+class _ExchangingStub(_StubAgent):
+  exchange = 'collective'
+
+
+def _refuse_worker(rank, world, port, base, q):
+  os.environ['MASTER_ADDR'] = '127.0.0.1'
+  os.environ['MASTER_PORT'] = str(port)
+  dist.init_process_group('gloo', rank=rank, world_size=world)
+  from dopamine_amd.discrete_domains import run_experiment
+  pg = dist.group.WORLD
+  try:
+    run_experiment.Runner(base, lambda sess, env, summary_writer=None: _ExchangingStub(pg), _Env,
+                          num_iterations=1, training_steps=5, evaluation_steps=0)
+    q.put((rank, None))
+  except ValueError as e:
+    q.put((rank, str(e)))
+  dist.barrier()
+  dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_runner_refuses_data_parallel_learners(tmp_path):
+  """the Runner's whole-episode phases cannot keep data-parallel learners' gradient
+  steps in step across ranks, so it refuses them at construction on every rank (instead of
+  a wait timing out or collectives pairing up wrongly mid-run)."""
+  ctx = mp.get_context('spawn')
+  q = ctx.Queue()
+  port = _free_port()
+  procs = [ctx.Process(target=_refuse_worker, args=(r, 2, port, str(tmp_path / 'run'), q))
+           for r in range(2)]
+  for p in procs:
+    p.start()
+  res = dict(q.get(timeout=120) for _ in range(2))
+  for p in procs:
+    p.join(timeout=60)
+    assert p.exitcode == 0
+  assert all(res[r] and 'train_gradient_steps' in res[r] for r in (0, 1)), res

@@ -2,7 +2,9 @@
 flags into ab/<name>/, link them with the in-tree objects of the others.
   python tools/build_variant.py <name> <tu[,tu..]> [-DFLAG ...]
 e.g.  python tools/build_variant.py c51prof learner -DDQ_C51_PROF
-The variant loads through DQ_DIAGNOSTIC_BUILD=1 DOPAMINE_AMD_LIB=ab/<name>/libdopamine_amd.so."""
+The variant loads through DQ_DIAGNOSTIC_BUILD=1 DOPAMINE_AMD_LIB=ab/<name>/libdopamine_amd.so.
+DQ_VARIANT_ROOT=<dir> puts it under <dir>/<name> instead (e.g. variants/, which -- unlike ab/ --
+travels to the GPU box with gpurun; both are git-ignored)."""
 import os
 import subprocess
 import sys
@@ -16,7 +18,7 @@ def main():
   name, extra = sys.argv[1], sys.argv[3:]
   # "tu" recompiles the in-tree source, "tu=path" another file in its place (e.g. a git show)
   tus = dict((t.split('=') + [None])[:2] for t in sys.argv[2].split(','))
-  out_dir = os.path.join(ROOT, 'ab', name)
+  out_dir = os.path.join(ROOT, os.environ.get('DQ_VARIANT_ROOT', 'ab'), name)
   os.makedirs(out_dir, exist_ok=True)
   bdir = os.path.join(ROOT, 'dopamine_amd', 'build')
   # the variant records what it is (dq_build_flags); replay.hip, which exports it, is always
