@@ -1596,5 +1596,17 @@ class DQNAgent(object):
     path = os.path.join(checkpoint_dir, 'tf_ckpt-{}'.format(iteration_number))
     saved = torch.load(path, weights_only=True)
     for k, v in self._ckpt_tensors().items():
-      v.copy_(saved[k].to(v.device))
+      s = saved[k]
+      if s.shape == v.shape:
+        v.copy_(s.to(v.device))
+      elif s.dim() == 1 and v.dim() == 1 and s.numel() < v.numel():
+        # a flat buffer saved before the Nature-CNN layouts ended in the fc bucket's zero
+        # padding (networks.FC_BUCKET_ALIGN): every tensor sits in the prefix, the padding
+        # stays zero (its gradient is zero, so no optimizer ever moves it)
+        v.zero_()
+        v[:s.numel()].copy_(s.to(v.device))
+      else:
+        raise ValueError('tf_ckpt-{}: {} has shape {}, this agent expects {} (a checkpoint of '
+                         'another network or layout)'.format(iteration_number, k,
+                                                             tuple(s.shape), tuple(v.shape)))
     return True

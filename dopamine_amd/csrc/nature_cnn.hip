@@ -821,27 +821,30 @@ constexpr int group_wpe() {
 // Stamp build of the grouped launches (tools/group_stamps.py; never the product): every wave
 // that runs an op writes one record -- s_memrealtime (100 MHz) at the kernel's entry and after
 // its op returned, the launch's block count, the op's index in the group, the op-local block,
-// the wave and its XCD -- to a ring slot taken by a vector atomic on a counter.  Only these
-// buffers receive stamp words.
+// the wave and its XCD -- into its own slot of a per-wave-position ring (position = block x
+// 16 + wave; the slot from a counter only that position reads and advances: no atomics, no
+// shared words, one launch at a time on the stream).  Only these buffers receive stamp words.
 struct GrpRec {
   unsigned long long t0, t1;
   unsigned total, op_blk;      // op_blk: op index << 24 | op-local block << 8 | wave << 4 | XCD
 };
-constexpr unsigned kGrpRecs = 1u << 22;
-__device__ GrpRec g_grp_rec[kGrpRecs];
-__device__ unsigned g_grp_n;
+constexpr unsigned kGrpPos = 1024 * 16, kGrpRing = 128;
+__device__ GrpRec g_grp_rec[kGrpPos][kGrpRing];
+__device__ unsigned g_grp_seq[kGrpPos];
 template <class Op>
 __device__ __forceinline__ bool dispatch_prof(const Op& op, int nb, int& blk, float* smem, int k,
                                               unsigned long long t0) {
   if (blk < nb) {
     if (Op::kT >= (int)blockDim.x || (int)threadIdx.x < Op::kT) {
       op.run(blk, smem);
-      if ((threadIdx.x & 63) == 0) {
+      const unsigned p = blockIdx.x * 16 + (threadIdx.x >> 6);
+      if ((threadIdx.x & 63) == 0 && p < kGrpPos) {
         const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-        const unsigned slot = atomicAdd(&g_grp_n, 1u) & (kGrpRecs - 1);
-        g_grp_rec[slot] = GrpRec{t0, t1, gridDim.x,
-                                 ((unsigned)k << 24) | ((unsigned)blk << 8) |
-                                     ((threadIdx.x >> 6) << 4) | xcc_id()};
+        const unsigned sq = g_grp_seq[p];
+        g_grp_seq[p] = sq + 1;
+        g_grp_rec[p][sq % kGrpRing] = GrpRec{t0, t1, gridDim.x,
+                                             ((unsigned)k << 24) | ((unsigned)blk << 8) |
+                                                 ((threadIdx.x >> 6) << 4) | xcc_id()};
       }
     }
     return true;
@@ -1827,12 +1830,15 @@ int dq_peer_all_gather(const dq_peer* peer, float* var, void* stream) {
 #ifdef DQ_GROUP_PROF
 // the grouped launches' stamp ring (tools/group_stamps.py): reset the counter; read it back
 int dq_debug_group_reset(void) {
-  const unsigned z = 0;
-  return hipMemcpyToSymbol(HIP_SYMBOL(dq::cnn::g_grp_n), &z, sizeof(z)) == hipSuccess ? 0 : -1;
+  static unsigned z[dq::cnn::kGrpPos];
+  return hipMemcpyToSymbol(HIP_SYMBOL(dq::cnn::g_grp_seq), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
-int dq_debug_group_read(void* recs, unsigned* n_out, unsigned* cap_out) {
-  *cap_out = dq::cnn::kGrpRecs;
-  if (hipMemcpyFromSymbol(n_out, HIP_SYMBOL(dq::cnn::g_grp_n), sizeof(unsigned)) != hipSuccess)
+// recs: kGrpPos x kGrpRing records; seq: kGrpPos counters; dims: {kGrpPos, kGrpRing}
+int dq_debug_group_read(void* recs, unsigned* seq, unsigned* dims) {
+  dims[0] = dq::cnn::kGrpPos;
+  dims[1] = dq::cnn::kGrpRing;
+  if (hipMemcpyFromSymbol(seq, HIP_SYMBOL(dq::cnn::g_grp_seq), sizeof(dq::cnn::g_grp_seq)) !=
+      hipSuccess)
     return -1;
   return hipMemcpyFromSymbol(recs, HIP_SYMBOL(dq::cnn::g_grp_rec), sizeof(dq::cnn::g_grp_rec)) ==
                  hipSuccess ? 0 : -1;

@@ -197,6 +197,11 @@ class Runner(object):
     self._start_iteration = 0
     newest = checkpointer.get_latest_checkpoint_number(self._runner_checkpoint_dir())
     pg = self._process_group()
+    if (pg is not None and newest < 0 and
+        checkpointer.get_latest_checkpoint_number(self._checkpoint_dir) >= 0):
+      logging.warning('%s holds a single-process checkpoint; learners in a process group resume '
+                      'only from their rank directories (%s), so this run starts afresh',
+                      self._checkpoint_dir, self._runner_checkpoint_dir())
     if pg is not None:
       from dopamine_amd import parallel
       newest = parallel.agree_min(newest, pg)

@@ -70,7 +70,10 @@ def c51_loss(online_logits, target_logits, actions, rewards, terminals, support,
   grad = np.zeros_like(ol)
   # TF SoftmaxCrossEntropyWithLogits backprop = softmax - labels.
   grad[np.arange(B), actions] = (w / B)[:, None] * (sm - proj)
-  return dict(loss=loss, weights=w, grad=grad, proj=proj, argmax=astar,
+  # grad_abs: the magnitudes of the difference's two terms (oracle/nature_cnn.abs_grad)
+  grad_abs = np.zeros_like(ol)
+  grad_abs[np.arange(B), actions] = (w / B)[:, None] * (sm + proj)
+  return dict(loss=loss, weights=w, grad=grad, grad_abs=grad_abs, proj=proj, argmax=astar,
               priorities=np.sqrt(loss + dtype(1e-10)), mean_loss=(w * loss).mean())
 
 
@@ -89,7 +92,9 @@ def dqn_huber(online_q, target_q, actions, rewards, terminals, cumulative_gamma,
   loss = 0.5 * quad * quad + delta * (a - quad)
   grad = np.zeros_like(oq)
   grad[np.arange(B), actions] = np.clip(err, -delta, delta) / B
-  return dict(loss=loss, grad=grad, target=target, mean_loss=loss.mean())
+  grad_abs = np.zeros_like(oq)       # |q| + |target| of the difference err (abs_grad)
+  grad_abs[np.arange(B), actions] = (np.abs(chosen) + np.abs(target)) / B
+  return dict(loss=loss, grad=grad, grad_abs=grad_abs, target=target, mean_loss=loss.mean())
 
 
 def iqn_loss(online_qv, target_qv, target_qv_action, taus, actions, rewards, terminals,
@@ -126,7 +131,12 @@ def iqn_loss(online_qv, target_qv, target_qv_action, taus, actions, rewards, ter
   dtheta = -(w * dh / kappa).sum(1) / Np / B                           # (B, N)
   grad = np.zeros_like(oq).reshape(N, B, A)
   grad[:, np.arange(B), actions] = dtheta.T
-  return dict(loss=loss, grad=grad.reshape(N * B, A), mean_loss=loss.mean(), argmax=astar)
+  # grad_abs: each term's magnitude, |T| + |theta| where u = T - theta enters linearly
+  dabs = np.where(au <= kappa, np.abs(T)[:, :, None] + np.abs(theta)[:, None, :], kappa)
+  gabs = np.zeros_like(oq).reshape(N, B, A)
+  gabs[:, np.arange(B), actions] = ((w * dabs / kappa).sum(1) / Np / B).T
+  return dict(loss=loss, grad=grad.reshape(N * B, A), grad_abs=gabs.reshape(N * B, A),
+              mean_loss=loss.mean(), argmax=astar)
 
 
 class TF1Adam:

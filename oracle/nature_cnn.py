@@ -116,76 +116,113 @@ def to_input(x_float32_nhwc):
 
 # ----------------------------------------------------------- Σ|terms| of every gradient
 # The conditioning of a gradient element: the float64 sum of the absolute values of the
-# terms its final reduction adds -- |dz| |x| over the batch (and positions) for a weight,
-# |dz| for a bias, with dz the float64 gradient of the layer's pre-activation.  A bias
-# gradient that sums 441 B positions of both signs can be far below its terms, and its fp32
-# sum is then accurate to u times the terms, not to u times itself.  Tests compare
-# |g_device - g_float64| with this sum element by element.
-_CONVS = (('conv1', (2, 2, 2, 2), 4, 'a1'), ('conv2', (1, 2, 1, 2), 2, 'a2'),
-          ('conv3', (1, 1, 1, 1), 1, 'a3'))
+# terms its final reduction adds, each operand taken at its own one-level magnitude -- a
+# layer input as Σ|w| |a| + |b| of the layer that produced it (masked), a pre-activation
+# gradient as Σ|w| |dz| of the layer that consumed it (masked), the loss gradient as the
+# caller gives it.  fp32 arithmetic errs on every operand by a small multiple of u times
+# that magnitude, so an element's error is bounded by a small multiple of u times this sum
+# whatever cancellation its signed sum (or either operand's) has: a bias gradient summing
+# 441 B positions of both signs, a weight reading an activation that is itself a near-zero
+# difference.  Tests compare |g_device - g_float64| with it element by element.
+class _Layer(object):
+  def __init__(self, name, fn, inputs, exact=None):
+    self.name, self.fn, self.inputs = name, fn, inputs     # inputs: producer layers / tensors
+    self.exact = exact or {}                                # input index -> exact tensor
 
 
-def _layers(P, x_nhwc, masks, rec):
-  """The Nature-CNN torso as forward()/torso(), recording each layer's (name, kind, input,
-  pre-activation) in rec (the pre-activations retain their gradients)."""
+def _conv(pad, stride):
+  return lambda xs, w, b: F.conv2d(F.pad(xs[0], pad), w, b, stride=stride)
+
+
+def _flat_nhwc(a):
+  return a.permute(0, 2, 3, 1).reshape(a.shape[0], -1)
+
+
+def _graph(P, x_nhwc, masks, taus=None):
+  """The layers of forward() / iqn_forward() as a DAG: (layers, their ReLU masks in their
+  output layouts (None: no ReLU), the output layer)."""
   x = x_nhwc.permute(0, 3, 1, 2)
-  for name, pad, st, act in _CONVS:
-    xi = F.pad(x, pad)
-    z = F.conv2d(xi, P[name + '_w'], P[name + '_b'], stride=st)
-    z.retain_grad()
-    rec.append((name, ('conv', st), xi, z))
-    x = _relu(z, masks, act, True)
-  return x.permute(0, 2, 3, 1).reshape(x.shape[0], -1)
+  mask = lambda name, nhwc, shape: _relu(torch.ones(shape, dtype=torch.float64), masks, name, nhwc)
+  L = []
+  c1 = _Layer('conv1', _conv((2, 2, 2, 2), 4), [None], {0: x})
+  c2 = _Layer('conv2', _conv((1, 2, 1, 2), 2), [c1])
+  c3 = _Layer('conv3', _conv((1, 1, 1, 1), 1), [c2])
+  L += [c1, c2, c3]
+  if taus is None:
+    f1 = _Layer('fc1', lambda xs, w, b: F.linear(_flat_nhwc(xs[0]), w, b), [c3])
+  else:
+    B = x.shape[0]
+    nq = taus.shape[0] // B
+    E = P['emb_w'].shape[1]
+    i_pi = (torch.arange(1, E + 1, dtype=torch.float32) * torch.tensor(math.pi, dtype=torch.float32))
+    cos = torch.cos((taus.to(torch.float32).reshape(-1, 1) * i_pi).double())
+    em = _Layer('emb', lambda xs, w, b: F.linear(xs[0], w, b), [None], {0: cos})
+    L.append(em)
+    f1 = _Layer('fc1', lambda xs, w, b: F.linear(_flat_nhwc(xs[0]).repeat(nq, 1) * xs[1], w, b),
+                [c3, em])
+  f2 = _Layer('fc2', lambda xs, w, b: F.linear(xs[0], w, b), [f1])
+  L += [f1, f2]
+  names = {'conv1': ('a1', True), 'conv2': ('a2', True), 'conv3': ('a3', True), 'emb': ('emb', False),
+           'fc1': ('h', False)}
+  return L, names, mask, f2
 
 
-def _linear(P, name, x, rec):
-  z = F.linear(x, P[name + '_w'], P[name + '_b'])
-  z.retain_grad()
-  rec.append((name, ('fc',), x, z))
-  return z
-
-
-def _abs_sums(P, rec):
-  """Σ|terms| of each recorded layer's weight and bias gradients, in the flat layout."""
-  g = torch.zeros(P.numel, dtype=torch.float64)
-  for name, kind, xi, z in rec:
-    dz = z.grad.detach().abs()
-    ax = xi.detach().abs()
-    w = P[name + '_w'].detach().clone().requires_grad_(True)
-    t = F.conv2d(ax, w, stride=kind[1]) if kind[0] == 'conv' else F.linear(ax, w)
-    t.backward(dz)
-    gw = w.grad.permute(0, 2, 3, 1) if kind[0] == 'conv' else w.grad
-    gb = dz.sum(dim=(0, 2, 3)) if kind[0] == 'conv' else dz.sum(0)
+def _abs_terms(P, x_nhwc, masks, gout, gout_abs, taus=None):
+  L, names, mask, top = _graph(P, x_nhwc, masks, taus)
+  act, z, m = {}, {}, {}
+  for l in L:                                              # the float64 forward
+    xs = [l.exact[i] if p is None else act[p.name] for i, p in enumerate(l.inputs)]
+    z[l.name] = l.fn(xs, P[l.name + '_w'], P[l.name + '_b'])
+    z[l.name].retain_grad()
+    if l is not top:
+      m[l.name] = mask(names[l.name][0], names[l.name][1], z[l.name].shape)
+      act[l.name] = z[l.name] * m[l.name]
+  z[top.name].backward(torch.as_tensor(np.asarray(gout), dtype=torch.float64))
+  grad = P.flat_grad()
+  aw = {l.name: P[l.name + '_w'].detach().abs() for l in L}
+  ab = {l.name: P[l.name + '_b'].detach().abs() for l in L}
+  # one-level forward magnitudes of every activation (from its true inputs)
+  a_abs = {}
+  for l in L:
+    if l is top:
+      continue
+    xs = [(l.exact[i] if p is None else act[p.name]).detach().abs() for i, p in enumerate(l.inputs)]
+    with torch.no_grad():
+      a_abs[l.name] = l.fn(xs, aw[l.name], ab[l.name]) * m[l.name]
+  # one-level backward magnitudes of every pre-activation gradient (from its true upstream)
+  dz_abs = {top.name: torch.as_tensor(np.asarray(gout_abs), dtype=torch.float64)}
+  for l in reversed(L):
+    for i, p in enumerate(l.inputs):
+      if p is None:
+        continue
+      xs = [(l.exact[j] if q is None else act[q.name]).detach().abs().clone().requires_grad_(j == i)
+            for j, q in enumerate(l.inputs)]
+      l.fn(xs, aw[l.name], None).backward(z[l.name].grad.detach().abs())
+      d = xs[i].grad * m[p.name]
+      dz_abs[p.name] = dz_abs[p.name] + d if p.name in dz_abs else d
+  # Σ|terms| of each weight / bias gradient: the layer's input magnitudes against its
+  # pre-activation gradient's
+  out = np.zeros(P.numel)
+  for l in L:
+    xs = [(l.exact[i].abs() if p is None else a_abs[p.name]) for i, p in enumerate(l.inputs)]
+    w = torch.zeros_like(aw[l.name], requires_grad=True)
+    l.fn(xs, w, None).backward(dz_abs[l.name])
+    gw = w.grad.permute(0, 2, 3, 1) if w.grad.dim() == 4 else w.grad
+    d = dz_abs[l.name]
+    gb = d.sum(dim=(0, 2, 3)) if d.dim() == 4 else d.sum(0)
     for suf, v in (('_w', gw), ('_b', gb)):
-      o, shape = P.offsets[name + suf]
-      g[o:o + v.numel()] = v.reshape(-1)
-  return g.numpy()
+      o, _ = P.offsets[l.name + suf]
+      out[o:o + v.numel()] = v.reshape(-1).numpy()
+  return grad, out
 
 
-def abs_grad(P, x_nhwc, masks, gout):
-  """(flat float64 gradient, flat Σ|terms| of it) for forward(P, x, masks) and the loss
-  gradient gout (B, n_out); P: fresh Params64 leaves.  masks: the device's activations (the
-  ReLU decisions are the device's)."""
-  rec = []
-  h = _relu(_linear(P, 'fc1', _layers(P, x_nhwc, masks, rec), rec), masks, 'h')
-  out = _linear(P, 'fc2', h, rec)
-  out.backward(torch.as_tensor(np.asarray(gout), dtype=torch.float64))
-  return P.flat_grad(), _abs_sums(P, rec)
+def abs_grad(P, x_nhwc, masks, gout, gout_abs):
+  """(flat float64 gradient, flat Σ|terms| of each element) for forward(P, x, masks) with
+  the loss gradient gout (B, n_out) and its magnitudes gout_abs; P: fresh Params64 leaves;
+  masks: the device's activations (its ReLU decisions)."""
+  return _abs_terms(P, x_nhwc, masks, gout, gout_abs)
 
 
-def iqn_abs_grad(P, x_nhwc, taus, masks, gout):
-  """abs_grad for iqn_forward (rows q B + b; masks a1, a2, a3, emb, h); the Hadamard
-  product's own sum (over the N tiled rows of each state) is the fc1 gradient's reduction."""
-  rec = []
-  state = _layers(P, x_nhwc, masks, rec)
-  B = state.shape[0]
-  nq = taus.shape[0] // B
-  E = P['emb_w'].shape[1]
-  tiled = state.repeat(nq, 1)
-  i_pi = (torch.arange(1, E + 1, dtype=torch.float32) * torch.tensor(math.pi, dtype=torch.float32))
-  emb_in = torch.cos((taus.to(torch.float32).reshape(-1, 1) * i_pi).double())
-  emb = _relu(_linear(P, 'emb', emb_in, rec), masks, 'emb')
-  h = _relu(_linear(P, 'fc1', tiled * emb, rec), masks, 'h')
-  out = _linear(P, 'fc2', h, rec)
-  out.backward(torch.as_tensor(np.asarray(gout), dtype=torch.float64))
-  return P.flat_grad(), _abs_sums(P, rec)
+def iqn_abs_grad(P, x_nhwc, taus, masks, gout, gout_abs):
+  """abs_grad for iqn_forward (rows q B + b; masks a1, a2, a3, emb, h)."""
+  return _abs_terms(P, x_nhwc, masks, gout, gout_abs, taus)

@@ -269,11 +269,13 @@ LONG_PARAM_ATOL = 1e-6  # fp32 updates vs the float64 trajectory after 1,000 ste
 # 1e-5 in the first 13 (north_star's 1e-5 bar is on Q-values and losses, which stay at 1e-6)
 # Gradients over the long horizons: each element's error against the float64 gradient on the
 # device's ReLU decisions, relative to the float64 sum of the ABSOLUTE terms of its final
-# reduction (oracle/nature_cnn.abs_grad: |dz| |x| summed over batch and positions for a
-# weight, |dz| for a bias), element by element -- what fp32 summation can promise whatever
-# the cancellation (conv1_b sums 441 B positions of both signs; relative to the tensor's max
-# |g| it read up to 2.2e-5, round 5).  The bar is GRAD_TOL's 1e-5 on that measure; the
-# max-|g|-relative figure is still printed ('grad').
+# reduction, each operand at its one-level magnitude (oracle/nature_cnn.abs_grad: a layer
+# input as Σ|w||a| + |b| of its producer, a pre-activation gradient as Σ|w||dz| of its
+# consumer, the loss gradient as the sum of its terms' magnitudes), element by element -- what
+# fp32 arithmetic can promise whatever the cancellation (conv1_b sums 441 B positions of both
+# signs; relative to the tensor's max |g| it read up to 2.2e-5, round 5).  Validated on fp32
+# CPU arithmetic: <= 2.8e-6 on every tensor (the same measure, torch fp32 vs float64).  The bar
+# is GRAD_TOL's 1e-5 on that measure; the max-|g|-relative figure is still printed ('grad').
 def _cond(got, ref, abs_terms):
   got, ref = np.asarray(got, np.float64), np.asarray(ref, np.float64)
   return float((np.abs(got - ref) / np.maximum(np.asarray(abs_terms, np.float64), 1e-30)).max())
@@ -342,13 +344,13 @@ def test_bench_path_long_horizon(kind):
                           b[2], b[6], support, cg, b[8], dtype=np.float64)
         errs['priorities'] = max(errs['priorities'], float(
             (np.abs(tr['priorities'] - ref['priorities']) / np.abs(ref['priorities'])).max()))
-        gout = ref['grad'].reshape(B, A * N)
+        gout, gabs = ref['grad'].reshape(B, A * N), ref['grad_abs'].reshape(B, A * N)
       else:
         ref = OL.dqn_huber(out.detach().numpy(), tout, b[1], b[2], b[6], cg, dtype=np.float64)
-        gout = ref['grad']
+        gout, gabs = ref['grad'], ref['grad_abs']
       errs['logits'] = max(errs['logits'], _rel(tr['online_out'], out.detach().numpy()))
       errs['loss'] = max(errs['loss'], _rel(tr['loss'], ref['loss']))
-      g, ga = ONC.abs_grad(ONC.Params64(w, offsets), xin, masks, gout)
+      g, ga = ONC.abs_grad(ONC.Params64(w, offsets), xin, masks, gout, gabs)
       for name, (o, shape) in offsets.items():
         n = int(np.prod(shape))
         errs['grad'][name] = max(errs['grad'].get(name, 0.0), _rel(tr['grad'][o:o + n], g[o:o + n]))
@@ -635,7 +637,8 @@ def test_iqn_breakout_long_horizon():
       errs['loss'] = max(errs['loss'], _rel(tr['loss'], ref['loss']))
       errs['dq'] = max(errs['dq'], _rel(tr['grad_out'], ref['grad']))
       g, ga = ONC.iqn_abs_grad(ONC.Params64(w, offsets), ONC.to_input(np.moveaxis(x, 1, -1)),
-                               torch.from_numpy(tr['taus']).double(), masks, ref['grad'])
+                               torch.from_numpy(tr['taus']).double(), masks, ref['grad'],
+                               ref['grad_abs'])
       for name, (o, shape) in offsets.items():
         n = int(np.prod(shape))
         errs['grad'][name] = max(errs['grad'].get(name, 0.0), _rel(tr['grad'][o:o + n], g[o:o + n]))
@@ -653,3 +656,32 @@ def test_iqn_breakout_long_horizon():
   assert errs['q'] <= Q_TOL and errs['loss'] <= Q_TOL and errs['dq'] <= Q_TOL, errs
   assert max(errs['grad_cond'].values()) <= GRAD_TOL, errs
   assert errs['params'] <= LONG_PARAM_ATOL, errs
+
+
+@pytest.mark.timeout(600)
+def test_mean_loss_is_the_last_traced_step():
+  """the bench line's final_mean_loss (RainbowAgent.mean_loss after
+  train_gradient_steps: mean(w * CE), the reference's summary, rb:298-301) is that of the
+  LAST gradient step the call ran -- the step the trace records last -- for a chunk-graph
+  call, a single-step call, and a window like the driver's (priming, warmup, 20 steps)."""
+  import bench
+  torch.cuda.set_device(0)
+  agent = bench.build_agent(9, 1_000_000, 32, torch.device('cuda', 0))
+  agent.enable_trace()
+  random.seed(0)
+  bench.fill_synthetic(agent._replay.memory, 9, seed=1)
+  _prime(agent)
+  U = agent._UNROLL
+
+  def last_traced(slot):      # RainbowAgent.mean_loss's arithmetic on the traced step's tensors
+    loss = agent._trace['loss'][slot]
+    w = 1.0 / torch.sqrt(agent._trace['sampling_probabilities'][slot] + 1e-10)
+    return float((loss * (w / w.max())).mean().item())
+
+  agent.train_gradient_steps(1)                          # a single step: slot U + parity
+  assert agent.mean_loss() == last_traced(U + (agent._opt_steps - 1) % 2)
+  for _ in range(3):
+    agent.train_gradient_steps(U)                        # one chunk: its last step, slot U - 1
+    assert agent.mean_loss() == last_traced(U - 1)
+  elapsed, _ = bench.timed_steps(agent, 20, 5)           # the driver's window shape
+  assert agent.mean_loss() == last_traced(U - 1)

@@ -2,7 +2,8 @@
 # rank on cuda:0 over gloo (DQ_BENCH_REHEARSE=1), printing the N > 1 line's self-checks
 # (replicas compared bit for bit, self-test verdict, per-rank waits at each exchange point).
 #   gpurun -- bash tools/gpu_rehearse.sh <out-name> <what>
-# what: tests | w2 | w4 | w8 | faults (a comma list).  faults: world-2 rehearsals on the
+# what: tests | w2 | w4 | w8 | faults | replica (a comma list).  replica: the variant whose
+# rank 1 computes its replicated conv-bucket mean 2^-20 off (its replica must be caught).  faults: world-2 rehearsals on the
 # fault-injection variants (variants/, built here by tools/build_variant.py with
 # DQ_VARIANT_ROOT=variants): one XCD's blocks hidden from the publication's count, one XCD's
 # write-back dropped (self-test on, then off so that only the replica check can catch it).
@@ -39,6 +40,9 @@ fi
 for w in 2 4 8; do
   if [[ $WHAT == *w$w* ]]; then bench_n $w rehearse_w$w || exit $?; fi
 done
+if [[ $WHAT == *replica* ]]; then
+  bench_n 2 fault_replica DQ_DIAGNOSTIC_BUILD=1 DOPAMINE_AMD_LIB=variants/peer_fault_replica/libdopamine_amd.so || exit $?
+fi
 if [[ $WHAT == *faults* ]]; then
   bench_n 2 fault_hide_xcd DQ_DIAGNOSTIC_BUILD=1 DOPAMINE_AMD_LIB=variants/peer_hide_xcd/libdopamine_amd.so || exit $?
   bench_n 2 fault_drop_fence DQ_DIAGNOSTIC_BUILD=1 DOPAMINE_AMD_LIB=variants/peer_drop_fence/libdopamine_amd.so || exit $?
