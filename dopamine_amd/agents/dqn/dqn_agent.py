@@ -1599,7 +1599,8 @@ class DQNAgent(object):
       s = saved[k]
       if s.shape == v.shape:
         v.copy_(s.to(v.device))
-      elif s.dim() == 1 and v.dim() == 1 and s.numel() < v.numel():
+      elif (s.dim() == 1 and v.numel() == self.online_convnet.fp.numel and
+            s.numel() == self.online_convnet.fp.content_numel):
         # a flat buffer saved before the Nature-CNN layouts ended in the fc bucket's zero
         # padding (networks.FC_BUCKET_ALIGN): every tensor sits in the prefix, the padding
         # stays zero (its gradient is zero, so no optimizer ever moves it)

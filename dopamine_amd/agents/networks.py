@@ -34,6 +34,7 @@ class FlatParams(object):
       n = int(np.prod(shape))
       self.offsets[name] = (off, tuple(shape))
       off += (n + 3) // 4 * 4
+    self.content_numel = off          # the tensors' floats, before the tail padding
     if tail_align is not None:
       name, multiple = tail_align
       off += -(off - self.offsets[name][0]) % multiple

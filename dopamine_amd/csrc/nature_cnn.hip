@@ -1350,7 +1350,9 @@ void backward_grouped(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, in
         if (in(2)) group_r(c, rd(2), dW_fc1a, dX_c3, dW_fc2a);
         if (kHeadFrom == 6) {
           // conv2's weight-gradient slabs (they need only da2) beside conv3's in launch 3
-          // (+0.9%), the head's conv1 in launch 5, its conv2 and conv3 in the next forward
+          // (+0.9%), the head's conv1 in launch 5, its conv2 and conv3 in the next forward.
+          // (Launch 3 with the sub-pixel tiles first: 19.6 instead of 17.0 us -- conv3's last
+          // slabs then wait for the sub-pixel tiles' slots, tools/group_stamps.py)
           if (in(3)) group_r(c, rd(3), dW_c3, sp00, sp01, sp10, sp11, dW_c2);
           if (in(4)) group_r(c, rd(4), sum_c3, dW_c1);
           if (in(5)) {

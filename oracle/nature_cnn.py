@@ -118,8 +118,11 @@ def to_input(x_float32_nhwc):
 # The conditioning of a gradient element: the float64 sum of the absolute values of the
 # terms its final reduction adds, each operand taken at its own one-level magnitude -- a
 # layer input as Σ|w| |a| + |b| of the layer that produced it (masked), a pre-activation
-# gradient as Σ|w| |dz| of the layer that consumed it (masked), the loss gradient as the
-# caller gives it.  fp32 arithmetic errs on every operand by a small multiple of u times
+# gradient as Σ|w| |dz| of the layer that consumed it (masked), the loss gradient as the sum
+# of its terms' magnitudes (oracle/learner.py grad_abs), which the dense head (fc2, fc1)
+# carries down: the loss gradient's cancellation (C51's softmax - projection, Huber's q -
+# target, IQN's sum over N' target quantiles) reaches fc1, the embedding and conv3's inputs
+# undiluted, while below it each convolution's own long reduction dominates.  fp32 arithmetic errs on every operand by a small multiple of u times
 # that magnitude, so an element's error is bounded by a small multiple of u times this sum
 # whatever cancellation its signed sum (or either operand's) has: a bias gradient summing
 # 441 B positions of both signs, a weight reading an activation that is itself a near-zero
@@ -167,7 +170,7 @@ def _graph(P, x_nhwc, masks, taus=None):
   return L, names, mask, f2
 
 
-def _abs_terms(P, x_nhwc, masks, gout, gout_abs, taus=None):
+def _abs_terms(P, x_nhwc, masks, gout, gout_abs, taus=None, full=False):
   L, names, mask, top = _graph(P, x_nhwc, masks, taus)
   act, z, m = {}, {}, {}
   for l in L:                                              # the float64 forward
@@ -186,7 +189,8 @@ def _abs_terms(P, x_nhwc, masks, gout, gout_abs, taus=None):
   for l in L:
     if l is top:
       continue
-    xs = [(l.exact[i] if p is None else act[p.name]).detach().abs() for i, p in enumerate(l.inputs)]
+    xs = [(l.exact[i].abs() if p is None else
+           (a_abs[p.name] if full else act[p.name].detach().abs())) for i, p in enumerate(l.inputs)]
     with torch.no_grad():
       a_abs[l.name] = l.fn(xs, aw[l.name], ab[l.name]) * m[l.name]
   # one-level backward magnitudes of every pre-activation gradient (from its true upstream)
@@ -197,7 +201,11 @@ def _abs_terms(P, x_nhwc, masks, gout, gout_abs, taus=None):
         continue
       xs = [(l.exact[j] if q is None else act[q.name]).detach().abs().clone().requires_grad_(j == i)
             for j, q in enumerate(l.inputs)]
-      l.fn(xs, aw[l.name], None).backward(z[l.name].grad.detach().abs())
+      # the dense head (fc2, fc1) passes on magnitudes carried from the loss's own terms; a
+      # convolution passes on one level from its true gradient
+      carried = full or l.name in ('fc1', 'fc2')
+      l.fn(xs, aw[l.name], None).backward(
+          dz_abs[l.name] if carried else z[l.name].grad.detach().abs())
       d = xs[i].grad * m[p.name]
       dz_abs[p.name] = dz_abs[p.name] + d if p.name in dz_abs else d
   # Σ|terms| of each weight / bias gradient: the layer's input magnitudes against its

@@ -206,6 +206,7 @@ def test_agent_loads_a_checkpoint_saved_before_the_fc_bucket_padding(tmp_path):
   saved = torch.load(path, weights_only=True)
   n = max(o + (int(np.prod(sh)) + 3) // 4 * 4                 # the unpadded layout's length
           for o, sh in a.online_convnet.fp.offsets.values())
+  assert n == a.online_convnet.fp.content_numel
   assert saved['online'].numel() > n
   old = {k: (v[:n].clone() if v.dim() == 1 and v.numel() == saved['online'].numel() else v)
          for k, v in saved.items()}
