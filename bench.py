@@ -54,7 +54,10 @@ def parse(argv=None):
                        'peer (the exchange over peer memory inside the backward, one stream: '
                        'DQNAgent exchange=\'peer\'), allreduce (the gradient buckets\' '
                        'all-reduce on a second stream), zero1 (its reduce-scatter / slice Adam / '
-                       'all-gather form); default peer,allreduce')
+                       'all-gather form).  Default: peer, and allreduce only if peer failed on '
+                       'some rank (a failed construction or self-test, a latched exchange '
+                       'error, replicas that differ) -- the first N > 1 run on a node does '
+                       'not stake its line on a second schedule once one has run cleanly')
   ap.add_argument('--comm', choices=('native', 'torch'), default='native',
                   help='N > 1 over RCCL: the learner\'s own communicators (parallel.RcclComm) '
                        'or torch.distributed\'s collectives')
@@ -526,12 +529,16 @@ def main(argv=None):
   # N > 1: the data-parallel schedules are timed one after the other on fresh
   # agents, and the headline is the fastest (every one is reported)
   names = ['single'] if pg is None else (args.schedules or 'peer,allreduce').split(',')
+  first_clean = pg is not None and args.schedules is None   # the default: stop at the first clean one
   kwargs_of = {'single': {}, 'peer': {'exchange': 'peer'}, 'allreduce': {},
                'zero1': {'shard_optimizer': True}}
   assert all(n in kwargs_of for n in names), names
   schedules = {}
   agent = None
   for name in names:
+    if first_clean and any('_elapsed' in v for v in schedules.values()):
+      schedules[name] = {'skipped': 'an earlier schedule ran cleanly on every rank'}
+      continue
     if agent is not None:
       agent.close()                   # its RCCL communicators (N > 1) before the next pair
       del agent

@@ -128,9 +128,13 @@ def to_input(x_float32_nhwc):
 # 441 B positions of both signs, a weight reading an activation that is itself a near-zero
 # difference.  Tests compare |g_device - g_float64| with it element by element.
 class _Layer(object):
-  def __init__(self, name, fn, inputs, exact=None):
+  def __init__(self, name, fn, inputs, exact=None, exact_abs=None):
     self.name, self.fn, self.inputs = name, fn, inputs     # inputs: producer layers / tensors
-    self.exact = exact or {}                                # input index -> exact tensor
+    self.exact = exact or {}                                # input index -> given tensor
+    self.exact_abs = exact_abs or {}                        # ... its magnitude, if not |x|
+
+  def in_abs(self, i):
+    return self.exact_abs[i] if i in self.exact_abs else self.exact[i].abs()
 
 
 def _conv(pad, stride):
@@ -159,7 +163,10 @@ def _graph(P, x_nhwc, masks, taus=None):
     E = P['emb_w'].shape[1]
     i_pi = (torch.arange(1, E + 1, dtype=torch.float32) * torch.tensor(math.pi, dtype=torch.float32))
     cos = torch.cos((taus.to(torch.float32).reshape(-1, 1) * i_pi).double())
-    em = _Layer('emb', lambda xs, w, b: F.linear(xs[0], w, b), [None], {0: cos})
+    # the device takes the cosine in fp32 (one rounding of |cos| <= 1): its magnitude as an
+    # operand is |cos| + 2^-23, not |cos| (near a zero of the cosine the rounding dominates)
+    em = _Layer('emb', lambda xs, w, b: F.linear(xs[0], w, b), [None], {0: cos},
+                {0: cos.abs() + 2.0 ** -23})
     L.append(em)
     f1 = _Layer('fc1', lambda xs, w, b: F.linear(_flat_nhwc(xs[0]).repeat(nq, 1) * xs[1], w, b),
                 [c3, em])
@@ -189,7 +196,7 @@ def _abs_terms(P, x_nhwc, masks, gout, gout_abs, taus=None, full=False):
   for l in L:
     if l is top:
       continue
-    xs = [(l.exact[i].abs() if p is None else
+    xs = [(l.in_abs(i) if p is None else
            (a_abs[p.name] if full else act[p.name].detach().abs())) for i, p in enumerate(l.inputs)]
     with torch.no_grad():
       a_abs[l.name] = l.fn(xs, aw[l.name], ab[l.name]) * m[l.name]
@@ -212,7 +219,7 @@ def _abs_terms(P, x_nhwc, masks, gout, gout_abs, taus=None, full=False):
   # pre-activation gradient's
   out = np.zeros(P.numel)
   for l in L:
-    xs = [(l.exact[i].abs() if p is None else a_abs[p.name]) for i, p in enumerate(l.inputs)]
+    xs = [(l.in_abs(i) if p is None else a_abs[p.name]) for i, p in enumerate(l.inputs)]
     w = torch.zeros_like(aw[l.name], requires_grad=True)
     l.fn(xs, w, None).backward(dz_abs[l.name])
     gw = w.grad.permute(0, 2, 3, 1) if w.grad.dim() == 4 else w.grad
