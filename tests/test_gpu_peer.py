@@ -28,7 +28,7 @@ LOOP_STEPS = 24
 
 
 def _peer_worker(rank, world, port, q, loop, same_seed=False, idle_rank=-1, max_polls=None,
-                 n_steps=None, stall=None):
+                 n_steps=None, stall=None, capacity=None):
   import sys
   sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
   import torch.distributed as dist
@@ -40,7 +40,8 @@ def _peer_worker(rank, world, port, q, loop, same_seed=False, idle_rank=-1, max_
   if max_polls is not None and (stall is None or rank == stall[1]):
     parallel.PeerExchange.MAX_POLLS = max_polls
   agent = _agent(dist.group.WORLD, 0 if same_seed else rank,
-                 net_seed=0 if same_seed else 1000 * rank, exchange='peer')
+                 net_seed=0 if same_seed else 1000 * rank, exchange='peer',
+                 **({} if capacity is None else {'capacity': capacity}))
   assert agent._peer is not None and agent._sharded() and not agent._collective()
   if rank == idle_rank:
     q.put((rank, 'idle'))
@@ -195,6 +196,22 @@ def test_peer_world_n_equal_mean_gradient_reference(world):
                                      'max %g' % (ok, int((d > 0).sum()), d.size,
                                                  np.flatnonzero(d)[:8], float(d.max())))
   assert ok
+  assert np.array_equal(m, rm) and np.array_equal(v, rv)
+
+
+@pytest.mark.timeout(1200)
+def test_peer_world8_at_config4_capacity_equals_mean_gradient_reference():
+  """Config 4's shape (the peer tests ran at 30k transitions): 8 processes on
+  cuda:0, each with its own 1M-transition buffer and network seed, in the learner loop --
+  parameters and gathered moments bitwise the rank-ordered mean-gradient TF1 Adam reference
+  over the same eight 1M buffers, the self-test passed on every rank."""
+  res, codes = _spawn(8, True, n_steps=LOOP_STEPS, capacity=1_000_000)
+  _, ok, flat, m, v, st, steps, _, info = res[0]
+  assert codes == [0] * 8 and ok and steps == LOOP_STEPS
+  assert info['selftest']['ok'] and len(info['selftest']['ranks']) == 8
+  ref, rm, rv = _mean_gradient_reference(True, moments=True, world=8, capacity=1_000_000,
+                                         n_steps=LOOP_STEPS)
+  assert np.array_equal(flat, ref)
   assert np.array_equal(m, rm) and np.array_equal(v, rv)
 
 
