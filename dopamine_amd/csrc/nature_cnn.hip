@@ -1514,17 +1514,17 @@ void backward_peer(Ctx& c, const dq_cnn_params* p, const dq_cnn_params* g, int B
   // defer_ag: the head of the range (AgParts), the rest by the next forward's conv launches)
   const PeerAgOp ag = defer_ag ? AgParts{&P, oa->var}.head()
                                : PeerAgOp{P, oa->var, na, 0, 0, INT64_MAX};
-  if (P.world > 1) {
-    if (head)
-      group_r(c, rd(5), PeerPubOp{P, kPeerParam}, sum_c2, sum_c1, head->conv1(), ag);
-    else
-      group_r(c, rd(5), PeerPubOp{P, kPeerParam}, sum_c2, sum_c1, ag);
-  } else if (head) {
-    group_r(c, rd(5), PeerPubOp{P, kPeerParam}, sum_c2, sum_c1, head->conv1());
-  } else {
+  if (P.world > 1)
+    group_r(c, rd(5), PeerPubOp{P, kPeerParam}, sum_c2, sum_c1, ag);
+  else
     group_r(c, rd(5), PeerPubOp{P, kPeerParam}, sum_c2, sum_c1);
-  }
-  group(c, PeerExchOp{P, od, oa->var, oa->m, oa->v, nc});
+  // launch 6: the exchange's blocks first (they publish, then wait), the target head's conv1
+  // beside them -- it reads only the target parameters and the batch gathered in launch 4,
+  // so its tiles fill the CUs while the exchange waits for the other learners
+  if (head)
+    group(c, PeerExchOp{P, od, oa->var, oa->m, oa->v, nc}, head->conv1());
+  else
+    group(c, PeerExchOp{P, od, oa->var, oa->m, oa->v, nc});
 }
 
 // backward_grouped with the runtime head_from (7: the whole target head runs in the next
