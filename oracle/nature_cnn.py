@@ -206,7 +206,11 @@ def _abs_terms(P, x_nhwc, masks, gout, gout_abs, taus=None, full=False):
     for i, p in enumerate(l.inputs):
       if p is None:
         continue
-      xs = [(l.exact[j] if q is None else act[q.name]).detach().abs().clone().requires_grad_(j == i)
+      # the other operands of a product (IQN's fc1: state ⊙ emb) at their one-level forward
+      # magnitudes: an fp32 operand errs by u times its magnitude, not its (maybe cancelled)
+      # value, and that error scales the input gradient (xs[i]'s own value does not enter)
+      xs = [((l.exact[j].abs() if q is None else act[q.name].abs()) if j == i else
+             (l.in_abs(j) if q is None else a_abs[q.name])).detach().clone().requires_grad_(j == i)
             for j, q in enumerate(l.inputs)]
       # the dense head (fc2, fc1) passes on magnitudes carried from the loss's own terms; a
       # convolution passes on one level from its true gradient
@@ -229,6 +233,34 @@ def _abs_terms(P, x_nhwc, masks, gout, gout_abs, taus=None, full=False):
       o, _ = P.offsets[l.name + suf]
       out[o:o + v.numel()] = v.reshape(-1).numpy()
   return grad, out
+
+
+def mask_flips(P, x_nhwc, masks, taus=None):
+  """Where the device's ReLU decisions differ from float64's, and by how much they may.
+  Layer by layer on the device's decisions upstream (so each layer is judged on its own
+  inputs), the float64 pre-activation z of every ReLU unit against its one-level magnitude
+  Σ|w||a| + |b|: fp32 arithmetic errs on z by a small multiple of u times that magnitude,
+  so a unit whose decision is NOT within rounding of 0 must take float64's branch.  Returns
+  {activation name: {'flips', 'units', 'worst'}}, worst = max |z| / magnitude over the
+  flipped units (0 if none) -- a mask or tile bug flips units of O(1) ratio."""
+  L, names, mask, top = _graph(P, x_nhwc, masks, taus)
+  act, out = {}, {}
+  with torch.no_grad():
+    for l in L:
+      if l is top:
+        continue
+      w, b = P[l.name + '_w'].detach(), P[l.name + '_b'].detach()
+      xs = [l.exact[i] if p is None else act[p.name] for i, p in enumerate(l.inputs)]
+      xa = [l.in_abs(i) if p is None else act[p.name].abs() for i, p in enumerate(l.inputs)]
+      z = l.fn(xs, w, b)
+      mag = l.fn(xa, w.abs(), b.abs())
+      m = mask(names[l.name][0], names[l.name][1], z.shape)
+      flip = (z > 0) != (m > 0)
+      ratio = z.abs() / torch.clamp(mag, min=1e-300)
+      out[names[l.name][0]] = dict(flips=int(flip.sum()), units=int(z.numel()),
+                                   worst=float(ratio[flip].max()) if bool(flip.any()) else 0.0)
+      act[l.name] = z * m
+  return out
 
 
 def abs_grad(P, x_nhwc, masks, gout, gout_abs):
