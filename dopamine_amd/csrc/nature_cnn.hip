@@ -529,6 +529,17 @@ struct PeerAgOp {
   int blocks() const { return nb; }
 };
 
+#ifdef DQ_GROUP_PROF
+// stamp build only (tools/group_stamps.py GS_PEER=1): thread 0 of each of the exchange
+// launch's first 16 blocks stamps entry / published / waited / updated / ticket into a ring
+// of its own (one writer per ring, like the grouped launches' records)
+constexpr int kPeerPhRing = 128;
+__device__ unsigned long long g_peer_ph[16][kPeerPhRing][5];
+__device__ unsigned g_peer_ph_seq[16];
+#define DQ_PEER_PH(k) if (threadIdx.x == 0 && blk < 16) ph[k] = __builtin_amdgcn_s_memrealtime()
+#else
+#define DQ_PEER_PH(k)
+#endif
 // the exchange launch (6): blocks 0..kPubBlocks-1 publish the conv bucket; every block waits for every
 // rank's, takes the rank-ordered mean of [0, lo) and applies TF1 Adam (replicated; block 0
 // also advances the beta powers).  Every block takes a ticket; the last advances the step
@@ -543,9 +554,16 @@ struct PeerExchOp {
   float* v;
   int nc;
   __device__ __forceinline__ void run(int blk, float* smem) const {
+#ifdef DQ_GROUP_PROF
+    unsigned long long ph[5] = {0, 0, 0, 0, 0};
+#endif
+    DQ_PEER_PH(0);
     const uint64_t e = peer_step(P);
     if (blk < kPubBlocks) peer_publish_xcd(P, kPeerConv);
-    if (peer_wait(P, kPeerConv, e, smem, blk == 0)) {
+    DQ_PEER_PH(1);
+    const bool ok = peer_wait(P, kPeerConv, e, smem, blk == 0);
+    DQ_PEER_PH(2);
+    if (ok) {
       const float alpha = adam_alpha_of(o.state, o.slot, o.lr);
       const float omb1 = __fsub_rn(1.0f, o.b1), omb2 = __fsub_rn(1.0f, o.b2);
 #ifdef DQ_PEER_FAULT_REPLICA
@@ -564,7 +582,16 @@ struct PeerExchOp {
       }
       if (blk == 0 && threadIdx.x == 0) adam_bump(o.state, o.slot, o.b1, o.b2);
     }
+    DQ_PEER_PH(3);
     peer_ticket(P, nc, e);
+    DQ_PEER_PH(4);
+#ifdef DQ_GROUP_PROF
+    if (threadIdx.x == 0 && blk < 16) {
+      const unsigned sq = g_peer_ph_seq[blk];
+      g_peer_ph_seq[blk] = sq + 1;
+      for (int k = 0; k < 5; ++k) g_peer_ph[blk][sq % kPeerPhRing][k] = ph[k];
+    }
+#endif
   }
   int blocks() const { return nc; }
 };
@@ -1834,6 +1861,14 @@ int dq_peer_all_gather(const dq_peer* peer, float* var, void* stream) {
 int dq_debug_group_reset(void) {
   static unsigned z[dq::cnn::kGrpPos];
   return hipMemcpyToSymbol(HIP_SYMBOL(dq::cnn::g_grp_seq), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+// the exchange launch's phase stamps: recs 16 x kPeerPhRing x 5 u64, seq 16 counters
+int dq_debug_peer_phases(void* recs, unsigned* seq) {
+  if (hipMemcpyFromSymbol(seq, HIP_SYMBOL(dq::cnn::g_peer_ph_seq), sizeof(dq::cnn::g_peer_ph_seq)) !=
+      hipSuccess)
+    return -1;
+  return hipMemcpyFromSymbol(recs, HIP_SYMBOL(dq::cnn::g_peer_ph), sizeof(dq::cnn::g_peer_ph)) ==
+                 hipSuccess ? 0 : -1;
 }
 // recs: kGrpPos x kGrpRing records; seq: kGrpPos counters; dims: {kGrpPos, kGrpRing}
 int dq_debug_group_read(void* recs, unsigned* seq, unsigned* dims) {

@@ -40,7 +40,16 @@ def main():
   L = _lib.lib
   L.dq_debug_group_reset.argtypes = []
   L.dq_debug_group_read.argtypes = [ctypes.c_void_p] * 3
-  agent = bench.build_agent(9, 1_000_000, 32, dev)
+  pg, kw = None, {}
+  if os.environ.get('GS_PEER') == '1':      # the one-rank peer schedule (bench --force-dist)
+    import torch.distributed as dist
+    from dopamine_amd import parallel
+    parallel.FORCE_COLLECTIVES = True
+    os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+    os.environ.setdefault('MASTER_PORT', '29534')
+    dist.init_process_group('nccl', rank=0, world_size=1, device_id=dev)
+    pg, kw = dist.group.WORLD, {'exchange': 'peer'}
+  agent = bench.build_agent(9, 1_000_000, 32, dev, pg=pg, **kw)
   import random
   random.seed(0)
   bench.fill_synthetic(agent._replay.memory, 9, seed=1)
@@ -106,6 +115,22 @@ def main():
       print('  %-4d %7d %7d %9.2f %9.2f %11.2f  %d/%d' % (
           k, int(np.median(v[:, 1])), int(np.median(v[:, 0])), np.median(v[:, 2]),
           np.median(v[:, 3]), np.median(v[:, 4]), last.count(k), len(occ)))
+
+  if pg is not None:                         # the exchange launch's phases (PeerExchOp)
+    L.dq_debug_peer_phases.argtypes = [ctypes.c_void_p] * 2
+    ph = np.zeros((16, 128, 5), np.uint64)
+    sq = np.zeros(16, np.uint32)
+    assert L.dq_debug_peer_phases(ph.ctypes.data, sq.ctypes.data) == 0
+    n = int(min(sq.min(), 128))
+    ph = ph[:, :n].astype(np.int64)
+    start = ph[:, :, 0].min(axis=0)          # per occurrence: the first block's entry
+    rel = (ph - start[None, :, None]) / 100.0
+    print('\nexchange launch phases (us from its first exchange block\'s entry; %d occurrences, '
+          'median over occurrences of the blocks\' max / min):' % n)
+    for k, what in enumerate(['entry', 'published (blocks < 16)', 'wait passed', 'conv Adam done',
+                              'ticket taken']):
+      print('  %-26s max %.2f  min %.2f' % (what, np.median(rel[:, :, k].max(axis=0)),
+                                            np.median(rel[:, :, k].min(axis=0))))
 
 
 if __name__ == '__main__':
