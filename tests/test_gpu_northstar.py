@@ -17,7 +17,9 @@ the same snapshot (parameters, optimizer state, sum tree, Python/numpy RNG state
   float64 Nature-CNN (oracle/nature_cnn.py) -- max |err| <= 1e-5 * max |ref|;
 * per-sample losses: max |err| <= 1e-5 * max |ref|; Rainbow's new priorities
   sqrt(CE + 1e-10): |err| <= 1e-5 * |ref| elementwise (fp64 c51 / Huber oracle);
-* the flat gradient: per parameter tensor, max |err| <= GRAD_TOL * max |ref|;
+* the flat gradient: per parameter tensor, max |err| <= GRAD_TOL * max |ref|, on the
+  device's ReLU decisions -- and every decision that differs from float64's must sit within
+  rounding of 0 (MASK_TOL of the unit's one-level magnitude, oracle/nature_cnn.mask_flips);
 * after each chunk, the parameters vs the float64 optimizer trajectory (TF1 Adam /
   centered RMSProp in float64 from the same state): |err| <= PARAM_ATOL.
 The oracle's sum tree takes the device's float32 priorities after they are checked,
@@ -43,7 +45,7 @@ GRAD_TOL = 1e-5      # flat gradient, per tensor, relative to the tensor's max |
 # The same gradient with float64 deciding every ReLU itself: a pre-activation within fp32
 # rounding of 0 flips a unit and moves a tensor's gradient by up to ~1e-2 of its scale
 # (measured: 9.3e-3 conv2_w in the C51 test, 5.5e-3 fc1_w in IQN double_dqn); a systematic
-# mask or tile bug moves it by O(1)
+# mask or tile bug moves it by O(1) -- and the flips themselves are checked: MASK_TOL below
 GRAD_UNPINNED_TOL = 5e-2
 PARAM_ATOL = 5e-8    # parameters after fp32 updates vs the float64 trajectory (|w| ~ 0.05)
 CHUNKS = 3
